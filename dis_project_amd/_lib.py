@@ -1,0 +1,260 @@
+"""ctypes binding of ``liblfm.so`` (the C-ABI declared in ``include/lfm.h``).
+
+This module is the only place that touches the shared library. There is no CPU
+fallback: if ``liblfm.so`` is missing, or no HIP device is visible when a context is
+requested, the calls raise :class:`LfmError` — loudly, by design.
+
+HIP runtime note: ``liblfm.so`` needs ``libamdhip64.so.7``. When PyTorch is imported
+*before* this module, the dynamic loader binds that name to the copy PyTorch already
+loaded (same SONAME), so one process never holds two HIP runtimes. Processes that
+use both must therefore import torch first (``bench.py`` does).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import POINTER, c_char, c_char_p, c_double, c_int, c_int64, c_size_t, c_void_p
+
+import numpy as np
+
+LIB_NAME = "liblfm.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+LFM_OK = 0
+LFM_E_ARG = 1
+LFM_E_HIP = 2
+LFM_E_NOT_PD = 3
+LFM_E_OOM = 4
+LFM_E_RCCL = 5
+LFM_E_STATE = 6
+
+LFM_UPLO_FULL = 0
+LFM_UPLO_LOWER = 1
+
+_ERR_NAMES = {
+    LFM_E_ARG: "LFM_E_ARG",
+    LFM_E_HIP: "LFM_E_HIP",
+    LFM_E_NOT_PD: "LFM_E_NOT_PD",
+    LFM_E_OOM: "LFM_E_OOM",
+    LFM_E_RCCL: "LFM_E_RCCL",
+    LFM_E_STATE: "LFM_E_STATE",
+}
+
+_dptr = POINTER(c_double)
+
+
+class LfmError(RuntimeError):
+    """A non-OK status from liblfm (code + the library's own message)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{_ERR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+class LfmHyp(ctypes.Structure):
+    _fields_ = [
+        ("num_genes", c_int64),
+        ("true_d", _dptr),
+        ("true_s", _dptr),
+        ("true_b", _dptr),
+        ("l", c_double),
+        ("obs_stddev", c_double),
+        ("jitter", c_double),
+    ]
+
+
+class LfmProblem(ctypes.Structure):
+    _fields_ = [("x", _dptr), ("y", _dptr), ("n", c_int64), ("hyp", LfmHyp)]
+
+
+class LfmKstat(ctypes.Structure):
+    _fields_ = [
+        ("name", c_char * 32),
+        ("launches", c_int64),
+        ("total_ms", c_double),
+        ("flops", c_double),
+        ("bytes", c_double),
+    ]
+
+
+# (name, restype, argtypes) — every entry point of include/lfm.h
+_c_ctx = c_void_p
+SIGNATURES = [
+    ("lfm_abi_version", c_int, []),
+    ("lfm_device_count", c_int, [POINTER(c_int)]),
+    ("lfm_ctx_create", c_int, [c_int, POINTER(c_void_p)]),
+    ("lfm_ctx_destroy", None, [_c_ctx]),
+    ("lfm_last_error", c_char_p, [_c_ctx]),
+    ("lfm_ctx_synchronize", c_int, [_c_ctx]),
+    ("lfm_ctx_set_block", c_int, [_c_ctx, c_int]),
+    ("lfm_mean_function_f64", c_int, [_c_ctx, _dptr, c_int64, POINTER(LfmHyp), _dptr]),
+    ("lfm_cross_covariance_f64", c_int,
+     [_c_ctx, _dptr, c_int64, _dptr, c_int64, POINTER(LfmHyp), _dptr, c_int64]),
+    ("lfm_gram_f64", c_int,
+     [_c_ctx, _dptr, c_int64, POINTER(LfmHyp), c_double, c_int, _dptr, c_int64]),
+    ("lfm_gram_f32", c_int,
+     [_c_ctx, _dptr, c_int64, POINTER(LfmHyp), c_double, c_int, POINTER(ctypes.c_float), c_int64]),
+    ("lfm_mll_f64", c_int, [_c_ctx, _dptr, _dptr, c_int64, POINTER(LfmHyp), c_int, _dptr]),
+    ("lfm_mll_batch_f64", c_int,
+     [_c_ctx, c_int64, POINTER(LfmProblem), c_int, _dptr, POINTER(c_int)]),
+    ("lfm_log_prob_f64", c_int, [_c_ctx, _dptr, _dptr, c_int64, c_int64, _dptr, _dptr]),
+    ("lfm_h_f64", c_int,
+     [_c_ctx, POINTER(LfmHyp), POINTER(c_int64), POINTER(c_int64), _dptr, _dptr, c_int64, _dptr]),
+    ("lfm_dev_alloc", c_int, [_c_ctx, c_size_t, POINTER(c_void_p)]),
+    ("lfm_dev_free", c_int, [_c_ctx, c_void_p]),
+    ("lfm_memcpy_h2d", c_int, [_c_ctx, c_void_p, c_void_p, c_size_t]),
+    ("lfm_memcpy_d2h", c_int, [_c_ctx, c_void_p, c_void_p, c_size_t]),
+    ("lfm_mll_f64_dev", c_int, [_c_ctx, c_void_p, c_void_p, c_int64, POINTER(LfmHyp), c_int, _dptr]),
+    ("lfm_gram_f64_dev", c_int,
+     [_c_ctx, c_void_p, c_int64, POINTER(LfmHyp), c_double, c_int, c_void_p, c_int64]),
+    ("lfm_gram_f32_dev", c_int,
+     [_c_ctx, c_void_p, c_int64, POINTER(LfmHyp), c_double, c_int, c_void_p, c_int64]),
+    ("lfm_profile_enable", c_int, [_c_ctx, c_int]),
+    ("lfm_profile_reset", c_int, [_c_ctx]),
+    ("lfm_profile_read", c_int, [_c_ctx, POINTER(LfmKstat), c_int, POINTER(c_int)]),
+    ("lfm_farm_unique_id", c_int, [_c_ctx, POINTER(ctypes.c_ubyte)]),
+    ("lfm_farm_init", c_int, [_c_ctx, POINTER(ctypes.c_ubyte), c_int, c_int]),
+    ("lfm_farm_allgather_f64", c_int, [_c_ctx, _dptr, c_int64, _dptr]),
+    ("lfm_farm_destroy", c_int, [_c_ctx]),
+    ("lfm_probe_mfma_f64", c_int, [_c_ctx, c_int, c_int, _dptr, _dptr]),
+    ("lfm_probe_mfma_f64_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr]),
+]
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load liblfm.so (once) and declare every C-ABI signature. Raises if absent."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or os.environ.get("LFM_LIBRARY", LIB_PATH)
+        if not os.path.exists(p):
+            raise LfmError(
+                LFM_E_STATE,
+                f"{p} not found: build it first (python -c 'import __graft_entry__ as g; g.build()'"
+                " or make -C dis_project_amd/csrc). There is no CPU fallback.",
+            )
+        lib = ctypes.CDLL(p)
+        for name, res, args in SIGNATURES:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.lfm_abi_version() != 1:
+            raise LfmError(LFM_E_STATE, "liblfm ABI version mismatch")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def as_f64(a, shape=None) -> np.ndarray:
+    arr = np.ascontiguousarray(np.asarray(a, dtype=np.float64))
+    if shape is not None:
+        arr = arr.reshape(shape)
+    return arr
+
+
+def dptr(a: np.ndarray):
+    return a.ctypes.data_as(_dptr)
+
+
+class HypArgs:
+    """Keeps the numpy buffers behind an LfmHyp alive for the duration of a call."""
+
+    def __init__(self, true_d, true_s, true_b, l, obs_stddev, jitter):
+        self.d = as_f64(true_d).reshape(-1)
+        self.s = as_f64(true_s).reshape(-1)
+        self.b = as_f64(true_b).reshape(-1)
+        if not (self.d.size == self.s.size == self.b.size) or self.d.size == 0:
+            raise ValueError("true_d, true_s, true_b must be non-empty and of equal length")
+        self.struct = LfmHyp(
+            self.d.size, dptr(self.d), dptr(self.s), dptr(self.b),
+            float(l), float(obs_stddev), float(jitter),
+        )
+
+    @property
+    def ref(self):
+        return ctypes.byref(self.struct)
+
+
+class Context:
+    """One liblfm context = one device + one HIP stream + a reusable workspace."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load_library()
+        h = c_void_p()
+        rc = self.lib.lfm_ctx_create(int(device), ctypes.byref(h))
+        if rc != LFM_OK:
+            n = c_int(0)
+            self.lib.lfm_device_count(ctypes.byref(n))
+            raise LfmError(rc, f"lfm_ctx_create(device={device}) failed; visible HIP devices: "
+                               f"{n.value}. liblfm needs an MI355X (gfx950); there is no CPU fallback.")
+        self.handle = h
+        self.device = int(device)
+
+    # -- error plumbing
+    def check(self, rc: int, allow_not_pd: bool = False) -> int:
+        if rc == LFM_OK or (allow_not_pd and rc == LFM_E_NOT_PD):
+            return rc
+        msg = self.lib.lfm_last_error(self.handle)
+        raise LfmError(rc, msg.decode() if msg else "")
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.lfm_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- profiling
+    def profile(self, on: bool = True):
+        self.check(self.lib.lfm_profile_enable(self.handle, int(on)))
+
+    def profile_reset(self):
+        self.check(self.lib.lfm_profile_reset(self.handle))
+
+    def profile_read(self) -> dict:
+        arr = (LfmKstat * 32)()
+        cnt = c_int(0)
+        self.check(self.lib.lfm_profile_read(self.handle, arr, 32, ctypes.byref(cnt)))
+        out = {}
+        for i in range(min(cnt.value, 32)):
+            s = arr[i]
+            out[s.name.decode()] = dict(launches=s.launches, total_ms=s.total_ms,
+                                        flops=s.flops, bytes=s.bytes)
+        return out
+
+
+_contexts: dict[int, Context] = {}
+
+
+def default_device() -> int:
+    for var in ("LFM_DEVICE", "LOCAL_RANK"):
+        v = os.environ.get(var)
+        if v is not None and v != "":
+            return int(v)
+    return 0
+
+
+def get_context(device: int | None = None) -> Context:
+    dev = default_device() if device is None else int(device)
+    ctx = _contexts.get(dev)
+    if ctx is None:
+        ctx = Context(dev)
+        _contexts[dev] = ctx
+    return ctx
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = c_int(0)
+    lib.lfm_device_count(ctypes.byref(n))
+    return n.value

@@ -1,0 +1,100 @@
+"""Seeded synthetic workloads for the five BASELINE.json configs.
+
+``C1``  p53 5 genes x 7 timepoints, reference init hyperparameters (model.py:99-114,
+        jitter 1e-4 from main.py:41), N = 35.
+``C2``  64 genes x 256 timepoints, N = 16384, fp64, one MLL evaluation.
+``C3``  C2 data x 32 random restarts (raw ~ N(0,1) -> Softplus / Sigmoid(0.5, 3.5)).
+``C4``  256 genes x 256 timepoints, N = 65536, fp32 gram fill.
+``C5``  3 replicates x 5 leave-one-gene-out ablations, N = 28 each (notebook.py:33-75).
+
+Every config is generated with numpy's default_rng so the container and the GPU box
+rebuild bit-identical inputs from the seed alone.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from .dataset import BARENCO_GENES, Dataset, SyntheticP53Data, dataset_3d, grid_inputs
+from .model import ExactLFM
+
+
+def softplus(x):
+    """tfb.Softplus forward (model.py:66, 79, 86, 93)."""
+    return np.logaddexp(0.0, np.asarray(x, np.float64))
+
+
+def softplus_inverse(y):
+    y = np.asarray(y, np.float64)
+    return y + np.log(-np.expm1(-y))
+
+
+def sigmoid_bounded(x, low=0.5, high=3.5):
+    """tfb.Sigmoid(low=0.5, high=3.5) forward (model.py:111)."""
+    return low + (high - low) / (1.0 + np.exp(-np.asarray(x, np.float64)))
+
+
+@dataclass
+class Workload:
+    name: str
+    model: ExactLFM
+    data: Dataset
+
+    @property
+    def n(self) -> int:
+        return self.data.n
+
+
+def grid_workload(name, G, T, seed_params, seed_y, jitter=1e-4, obs_stddev=1.0, l=2.5):
+    rng = np.random.default_rng(seed_params)
+    D = rng.uniform(0.2, 1.0, G)
+    S = rng.uniform(0.5, 1.5, G)
+    B = rng.uniform(0.01, 0.1, G)
+    x = grid_inputs(G, T)
+    ry = np.random.default_rng(seed_y)
+    y = np.repeat(B / D, T) + 0.5 * ry.standard_normal(G * T)
+    model = ExactLFM(jitter=jitter, obs_stddev=obs_stddev, num_genes=G, true_d=D, true_s=S,
+                     true_b=B, l=l)
+    return Workload(name, model, Dataset(x, y.reshape(-1, 1)))
+
+
+def c1_p53(seed=1) -> Workload:
+    data = SyntheticP53Data(replicate=0, seed=seed)
+    x, y, _ = dataset_3d(data)
+    return Workload("p53_5x7", ExactLFM(jitter=1e-4, num_genes=5), Dataset(x, y))
+
+
+def c2(G=64, T=256) -> Workload:
+    return grid_workload(f"synthetic_{G}x{T}_fp64", G, T, seed_params=2, seed_y=3)
+
+
+def c3_restarts(base: Workload, count=32, first_seed=100):
+    """Restart r: raw ~ N(0,1) (seed 100 + r), constrained through the model's bijectors."""
+    G = base.model.num_genes
+    models = []
+    for r in range(count):
+        raw = np.random.default_rng(first_seed + r).standard_normal(3 * G + 2)
+        models.append(base.model.replace(true_d=softplus(raw[:G]), true_s=softplus(raw[G:2 * G]),
+                                         true_b=softplus(raw[2 * G:3 * G]),
+                                         obs_stddev=float(softplus(raw[3 * G])),
+                                         l=float(sigmoid_bounded(raw[3 * G + 1]))))
+    return models
+
+
+def c4(G=256, T=256) -> Workload:
+    return grid_workload(f"synthetic_{G}x{T}_fp32", G, T, seed_params=4, seed_y=5)
+
+
+def c5_ablations(seeds=(10, 11, 12)):
+    """3 synthetic 5-gene replicates x drop-one-gene -> 15 problems at N = 28."""
+    out = []
+    for r, seed in enumerate(seeds):
+        for drop in BARENCO_GENES:
+            genes = [g for g in BARENCO_GENES if g != drop]
+            data = SyntheticP53Data(replicate=0, selected_genes=genes, seed=seed)
+            x, y, _ = dataset_3d(data)
+            out.append(Workload(f"rep{r}_minus_{drop}", ExactLFM(jitter=1e-4, num_genes=4),
+                                Dataset(x, y)))
+    return out

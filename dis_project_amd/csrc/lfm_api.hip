@@ -1,0 +1,861 @@
+// lfm_api.hip — the extern "C" boundary of include/lfm.h: context, workspace, input
+// staging, x-layout detection, dispatch, profiling and the RCCL result farm.
+//
+// Every entry point binds the ctx's device, enqueues on the ctx's stream and is
+// synchronous at return (one hipStreamSynchronize per call).
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdio>
+#include <cstring>
+
+#include "lfm_internal.h"
+
+using namespace lfm;
+
+namespace lfm {
+
+const char* const kClassName[K_NCLASS] = {"tables",   "gram_grid", "gram_direct",
+                                          "augment",  "potrf",     "trsm",
+                                          "syrk",     "finalize",  "small_mll",
+                                          "mean"};
+
+int set_err(lfm_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+int hip_fail(lfm_ctx* ctx, hipError_t e, const char* what) {
+  if (e == hipSuccess) return LFM_OK;
+  const int code = (e == hipErrorOutOfMemory) ? LFM_E_OOM : LFM_E_HIP;
+  return set_err(ctx, code, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+int ensure(lfm_ctx* ctx, void** p, size_t* cap, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  if (*p && *cap >= bytes) return LFM_OK;
+  if (*p) {
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "sync before realloc");
+    hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+  }
+  hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return set_err(ctx, LFM_E_OOM,
+                   "hipMalloc(" + std::to_string(bytes) + " B): " + hipGetErrorString(e));
+  }
+  *cap = bytes;
+  return LFM_OK;
+}
+
+int ensure_pinned(lfm_ctx* ctx, size_t bytes) {
+  if (ctx->hpin && ctx->hpin_bytes >= bytes) return LFM_OK;
+  if (ctx->hpin) {
+    hipStreamSynchronize(ctx->stream);
+    hipHostFree(ctx->hpin);
+    ctx->hpin = nullptr;
+  }
+  hipError_t e = hipHostMalloc((void**)&ctx->hpin, bytes, hipHostMallocDefault);
+  if (e != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc");
+  ctx->hpin_bytes = bytes;
+  return LFM_OK;
+}
+
+// ----------------------------------------------------------- profiling
+void prof_begin(lfm_ctx* ctx, int cls, hipEvent_t* a) {
+  (void)cls;
+  *a = nullptr;
+  if (!ctx->prof) return;
+  if (ctx->pool.empty()) {
+    hipEvent_t e;
+    hipEventCreate(&e);
+    ctx->pool.push_back(e);
+  }
+  *a = ctx->pool.back();
+  ctx->pool.pop_back();
+  hipEventRecord(*a, ctx->stream);
+}
+
+void prof_end(lfm_ctx* ctx, int cls, hipEvent_t a, double flops, double bytes) {
+  if (!ctx->prof || !a) return;
+  if (ctx->pool.empty()) {
+    hipEvent_t e;
+    hipEventCreate(&e);
+    ctx->pool.push_back(e);
+  }
+  hipEvent_t b = ctx->pool.back();
+  ctx->pool.pop_back();
+  hipEventRecord(b, ctx->stream);
+  ctx->pending.push_back(ProfEvent{cls, a, b, flops, bytes});
+}
+
+int prof_flush(lfm_ctx* ctx) {
+  for (auto& p : ctx->pending) {
+    float ms = 0;
+    hipEventElapsedTime(&ms, p.a, p.b);
+    lfm_kstat& s = ctx->stats[p.cls];
+    s.launches += 1;
+    s.total_ms += ms;
+    s.flops += p.flops;
+    s.bytes += p.bytes;
+    ctx->pool.push_back(p.a);
+    ctx->pool.push_back(p.b);
+  }
+  ctx->pending.clear();
+  return LFM_OK;
+}
+
+// -------------------------------------------------------- layout detect
+int gene_clamp_host(double g, int64_t G) { return gene_index(g, (int)G); }
+
+GridLayout detect_grid(const double* x, int64_t n, int64_t G) {
+  GridLayout L;
+  if (n < 1 || G < 1 || n > INT_MAX) return L;
+  const int g0 = gene_index(x[1], (int)G);
+  int64_t T = 1;
+  while (T < n && gene_index(x[3 * T + 1], (int)G) == g0) ++T;
+  if (n % T != 0) return L;
+  const int64_t nblk = n / T;
+  L.times.resize(T);
+  for (int64_t t = 0; t < T; ++t) L.times[t] = x[3 * t];
+  L.block_gene.resize(nblk);
+  for (int64_t b = 0; b < nblk; ++b) {
+    const int gb = gene_index(x[3 * b * T + 1], (int)G);
+    L.block_gene[b] = gb;
+    for (int64_t t = 0; t < T; ++t) {
+      const double* r = x + 3 * (b * T + t);
+      if (r[2] != 1.0) return L;                        // all rows gene rows (flag 1)
+      if (gene_index(r[1], (int)G) != gb) return L;     // one gene per block
+      if (std::memcmp(&r[0], &L.times[t], sizeof(double)) != 0) return L;  // shared times
+    }
+  }
+  const double t0 = L.times[0];
+  const double dt = T > 1 ? (L.times[T - 1] - t0) / (double)(T - 1) : 0.0;
+  double scale = 1.0;
+  for (double t : L.times) scale = std::max(scale, std::fabs(t));
+  for (int64_t t = 0; t < T; ++t)
+    if (!(std::fabs(L.times[t] - (t0 + (double)t * dt)) <= 1e-12 * scale)) return L;
+  L.T = (int)T;
+  L.nblk = (int)nblk;
+  L.t0 = t0;
+  L.dt = dt;
+  L.ok = true;
+  return L;
+}
+
+}  // namespace lfm
+
+// ------------------------------------------------------------- staging
+namespace {
+
+struct Staged {
+  HypDev h{};
+  GridLayout lay;
+  const double* d_times = nullptr;
+  const int* d_bg = nullptr;
+};
+
+int check_hyp(lfm_ctx* ctx, const lfm_hyp* hyp) {
+  if (!hyp) return set_err(ctx, LFM_E_ARG, "hyp is NULL");
+  if (hyp->num_genes < 1 || hyp->num_genes > (1 << 20))
+    return set_err(ctx, LFM_E_ARG, "num_genes must be in [1, 2^20]");
+  if (!hyp->true_d || !hyp->true_s || !hyp->true_b)
+    return set_err(ctx, LFM_E_ARG, "hyp true_d / true_s / true_b must not be NULL");
+  return LFM_OK;
+}
+
+// Uploads D, S, B (and, for a grid layout, the time vector and block genes) into ctx->par.
+int stage_hyp(lfm_ctx* ctx, const lfm_hyp* hyp, const double* x_host, int64_t n, bool want_grid,
+              Staged* st) {
+  int r = check_hyp(ctx, hyp);
+  if (r) return r;
+  const int64_t G = hyp->num_genes;
+  if (want_grid && x_host) st->lay = detect_grid(x_host, n, G);
+  const int64_t T = st->lay.ok ? st->lay.T : 0;
+  const int64_t nblk = st->lay.ok ? st->lay.nblk : 0;
+  const size_t nd = (size_t)(3 * G + T);
+  const size_t bytes = nd * 8 + (size_t)nblk * 4 + 16;
+  r = ensure(ctx, (void**)&ctx->par, &ctx->par_bytes, bytes);
+  if (r) return r;
+  r = ensure_pinned(ctx, std::max<size_t>(bytes + 1024, 1 << 16));
+  if (r) return r;
+  // the previous call's copy out of hpin has completed (every call ends synchronised)
+  double* hp = ctx->hpin;
+  std::memcpy(hp, hyp->true_d, G * 8);
+  std::memcpy(hp + G, hyp->true_s, G * 8);
+  std::memcpy(hp + 2 * G, hyp->true_b, G * 8);
+  if (T) std::memcpy(hp + 3 * G, st->lay.times.data(), T * 8);
+  if (nblk) std::memcpy(reinterpret_cast<char*>(hp) + nd * 8, st->lay.block_gene.data(), nblk * 4);
+  hipError_t e = hipMemcpyAsync(ctx->par, hp, bytes, hipMemcpyHostToDevice, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "upload hyperparameters");
+  st->h = HypDev{ctx->par, ctx->par + G, ctx->par + 2 * G, (int)G, hyp->l};
+  st->d_times = ctx->par + 3 * G;
+  st->d_bg = reinterpret_cast<const int*>(reinterpret_cast<const char*>(ctx->par) + nd * 8);
+  return LFM_OK;
+}
+
+struct DeviceGuard {
+  DeviceGuard(int dev) { hipSetDevice(dev); }
+};
+
+int finish(lfm_ctx* ctx) {
+  hipError_t e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "stream synchronize");
+  prof_flush(ctx);
+  return LFM_OK;
+}
+
+int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
+
+// Fill the lower triangle of ctx->A (lda = Mp) with Sigma = (K + jitter I) + sigma^2 I for x on
+// the device, the residual row n and identity padding; then factor and reduce.
+int mll_blocked(lfm_ctx* ctx, const Staged& st, const double* d_x, const double* d_y,
+                const double* d_loc, int64_t n, const lfm_hyp* hyp, int negative, double* out) {
+  const int64_t Mp = round_up(n + 1, 128);
+  int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)Mp * Mp * sizeof(double));
+  if (r) return r;
+  const double noise = hyp->obs_stddev * hyp->obs_stddev;  // objectives.py:66
+  if (st.lay.ok) {
+    r = ensure(ctx, (void**)&ctx->tab, &ctx->tab_bytes,
+               tables_doubles(st.h.G, st.lay.T) * sizeof(double));
+    if (r) return r;
+    r = launch_tables(ctx, st.h, st.lay, st.d_times, ctx->tab);
+    if (r) return r;
+    r = launch_gram_grid<double>(ctx, st.h, st.lay, ctx->tab, st.d_bg, n, hyp->jitter, noise,
+                                 LFM_UPLO_LOWER, ctx->A, Mp);
+  } else {
+    r = launch_gram_direct<double>(ctx, st.h, d_x, n, d_x, n, hyp->jitter, noise, LFM_UPLO_LOWER,
+                                   ctx->A, Mp);
+  }
+  if (r) return r;
+  r = launch_augment(ctx, st.h, d_x, d_y, d_loc, n, ctx->A, Mp, Mp);
+  if (r) return r;
+  r = chol_factor_solve(ctx, ctx->A, Mp, n, Mp, negative, ctx->result);
+  if (r) return r;
+  double* hres = ctx->hpin + (ctx->hpin_bytes / 8 - 8);
+  hipMemcpyAsync(hres, ctx->result, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+  r = finish(ctx);
+  if (r) return r;
+  *out = hres[0];
+  if ((int)hres[3] != INT_MAX) {
+    const double nan = std::nan("");
+    *out = nan;
+    return set_err(ctx, LFM_E_NOT_PD,
+                   "Cholesky failed: non-positive pivot at index " +
+                       std::to_string((long long)hres[3]));
+  }
+  return LFM_OK;
+}
+
+int validate_x(lfm_ctx* ctx, const void* x, int64_t n) {
+  if (!ctx) return LFM_E_ARG;
+  if (!x) return set_err(ctx, LFM_E_ARG, "x is NULL");
+  if (n < 1) return set_err(ctx, LFM_E_ARG, "n must be >= 1");
+  if (n > (int64_t)1 << 30) return set_err(ctx, LFM_E_ARG, "n too large");
+  return LFM_OK;
+}
+
+int check_mean_shape(lfm_ctx* ctx, int64_t n, const lfm_hyp* hyp) {
+  // mean_function (model.py:145-149) repeats B/D in blocks of n // num_genes; the
+  // reference's broadcast only succeeds when those blocks tile n exactly.
+  if (n % hyp->num_genes != 0)
+    return set_err(ctx, LFM_E_ARG,
+                   "mean_function needs n divisible by num_genes (model.py:145-149)");
+  return LFM_OK;
+}
+
+// small-N batch through one launch; probs already validated
+int small_batch(lfm_ctx* ctx, int64_t np, const lfm_problem* probs, const int64_t* idx,
+                int negative, double* out, int* status) {
+  // packed device buffer: per problem x(3n) y(n) D S B (3G) doubles; then SmallProb array
+  size_t nd = 0;
+  int maxn = 1;
+  for (int64_t q = 0; q < np; ++q) {
+    const lfm_problem& p = probs[idx[q]];
+    nd += 4 * (size_t)p.n + 3 * (size_t)p.hyp.num_genes;
+    maxn = std::max<int>(maxn, (int)p.n);
+  }
+  const size_t bytes_d = nd * 8;
+  const size_t bytes_p = (size_t)np * sizeof(SmallProb);
+  const size_t bytes_o = (size_t)np * (8 + 4);
+  const size_t total = round_up(bytes_d, 16) + round_up(bytes_p, 16) + bytes_o + 64;
+  int r = ensure(ctx, (void**)&ctx->xin, &ctx->xin_bytes, total);
+  if (r) return r;
+  r = ensure_pinned(ctx, total + 4096);
+  if (r) return r;
+  char* hb = reinterpret_cast<char*>(ctx->hpin);
+  char* db = reinterpret_cast<char*>(ctx->xin);
+  double* hd = reinterpret_cast<double*>(hb);
+  SmallProb* hp = reinterpret_cast<SmallProb*>(hb + round_up(bytes_d, 16));
+  const double* dd = reinterpret_cast<const double*>(db);
+  size_t off = 0;
+  for (int64_t q = 0; q < np; ++q) {
+    const lfm_problem& p = probs[idx[q]];
+    const int64_t n = p.n, G = p.hyp.num_genes;
+    SmallProb sp;
+    std::memcpy(hd + off, p.x, 3 * n * 8);
+    sp.x = dd + off;
+    off += 3 * n;
+    std::memcpy(hd + off, p.y, n * 8);
+    sp.y = dd + off;
+    off += n;
+    std::memcpy(hd + off, p.hyp.true_d, G * 8);
+    sp.D = dd + off;
+    off += G;
+    std::memcpy(hd + off, p.hyp.true_s, G * 8);
+    sp.S = dd + off;
+    off += G;
+    std::memcpy(hd + off, p.hyp.true_b, G * 8);
+    sp.B = dd + off;
+    off += G;
+    off += 0;
+    sp.n = (int)n;
+    sp.G = (int)G;
+    sp.l = p.hyp.l;
+    sp.jitter = p.hyp.jitter;
+    sp.noise = p.hyp.obs_stddev * p.hyp.obs_stddev;
+    hp[q] = sp;
+  }
+  const size_t up = round_up(bytes_d, 16) + bytes_p;
+  hipError_t e = hipMemcpyAsync(db, hb, up, hipMemcpyHostToDevice, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "upload small batch");
+  double* d_out = reinterpret_cast<double*>(db + round_up(bytes_d, 16) + round_up(bytes_p, 16));
+  int* d_st = reinterpret_cast<int*>(d_out + np);
+  r = launch_small_batch(ctx, reinterpret_cast<const SmallProb*>(db + round_up(bytes_d, 16)),
+                         (int)np, maxn, negative, d_out, d_st);
+  if (r) return r;
+  double* h_out = reinterpret_cast<double*>(hb + round_up(bytes_d, 16) + round_up(bytes_p, 16));
+  e = hipMemcpyAsync(h_out, d_out, np * 12, hipMemcpyDeviceToHost, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "download small batch");
+  r = finish(ctx);
+  if (r) return r;
+  const int* h_st = reinterpret_cast<const int*>(h_out + np);
+  for (int64_t q = 0; q < np; ++q) {
+    out[idx[q]] = h_out[q];
+    if (status) status[idx[q]] = h_st[q] ? LFM_E_NOT_PD : LFM_OK;
+  }
+  return LFM_OK;
+}
+
+}  // namespace
+
+template <typename OutT>
+static int gram_impl(lfm_ctx* ctx, const double* x_host, const double* d_x, int64_t n,
+                     const lfm_hyp* hyp, double diag_add, int uplo, OutT* d_out, int64_t ldo) {
+  Staged st;
+  int r = stage_hyp(ctx, hyp, x_host, n, true, &st);
+  if (r) return r;
+  if (st.lay.ok) {
+    r = ensure(ctx, (void**)&ctx->tab, &ctx->tab_bytes,
+               tables_doubles(st.h.G, st.lay.T) * sizeof(double));
+    if (r) return r;
+    r = launch_tables(ctx, st.h, st.lay, st.d_times, ctx->tab);
+    if (r) return r;
+    return launch_gram_grid<OutT>(ctx, st.h, st.lay, ctx->tab, st.d_bg, n, diag_add, 0.0, uplo,
+                                  d_out, ldo);
+  }
+  return launch_gram_direct<OutT>(ctx, st.h, d_x, n, d_x, n, diag_add, 0.0, uplo, d_out, ldo);
+}
+
+template <typename OutT>
+static int gram_host(lfm_ctx* ctx, const double* x, int64_t n, const lfm_hyp* hyp,
+                     double diag_add, int uplo, OutT* out, int64_t ldo) {
+  int r = validate_x(ctx, x, n);
+  if (r) return r;
+  if (!out || ldo < n) return set_err(ctx, LFM_E_ARG, "out is NULL or ldo < n");
+  if (uplo != LFM_UPLO_FULL && uplo != LFM_UPLO_LOWER) return set_err(ctx, LFM_E_ARG, "bad uplo");
+  DeviceGuard g(ctx->device);
+  r = ensure(ctx, (void**)&ctx->xin, &ctx->xin_bytes, (size_t)n * 3 * 8);
+  if (r) return r;
+  r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * sizeof(OutT));
+  if (r) return r;
+  OutT* dA = reinterpret_cast<OutT*>(ctx->A);
+  hipMemcpyAsync(ctx->xin, x, n * 3 * 8, hipMemcpyHostToDevice, ctx->stream);
+  if (uplo == LFM_UPLO_LOWER) hipMemsetAsync(dA, 0, (size_t)n * n * sizeof(OutT), ctx->stream);
+  r = gram_impl<OutT>(ctx, x, ctx->xin, n, hyp, diag_add, uplo, dA, n);
+  if (r) return r;
+  hipError_t e = hipMemcpy2DAsync(out, ldo * sizeof(OutT), dA, n * sizeof(OutT),
+                                  n * sizeof(OutT), n, hipMemcpyDeviceToHost, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "download gram");
+  return finish(ctx);
+}
+
+template <typename OutT>
+static int gram_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* hyp,
+                    double diag_add, int uplo, OutT* d_out, int64_t ldo) {
+  int r = validate_x(ctx, d_x, n);
+  if (r) return r;
+  if (!d_out || ldo < n) return set_err(ctx, LFM_E_ARG, "out is NULL or ldo < n");
+  if (uplo != LFM_UPLO_FULL && uplo != LFM_UPLO_LOWER) return set_err(ctx, LFM_E_ARG, "bad uplo");
+  DeviceGuard g(ctx->device);
+  std::vector<double> xh((size_t)n * 3);
+  hipError_t e = hipMemcpyAsync(xh.data(), d_x, n * 3 * 8, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "read back x for layout detection");
+  r = gram_impl<OutT>(ctx, xh.data(), d_x, n, hyp, diag_add, uplo, d_out, ldo);
+  if (r) return r;
+  return finish(ctx);
+}
+
+// =================================================================== C ABI
+extern "C" {
+
+int lfm_abi_version(void) { return LFM_ABI_VERSION; }
+
+int lfm_device_count(int* out) {
+  if (!out) return LFM_E_ARG;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *out = n;
+  return e == hipSuccess ? LFM_OK : LFM_E_HIP;
+}
+
+int lfm_ctx_create(int device, lfm_ctx** out) {
+  if (!out) return LFM_E_ARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return LFM_E_HIP;
+  if (device < 0 || device >= ndev) return LFM_E_ARG;
+  lfm_ctx* ctx = new lfm_ctx();
+  ctx->device = device;
+  std::memset(ctx->stats, 0, sizeof(ctx->stats));
+  for (int i = 0; i < K_NCLASS; ++i)
+    std::snprintf(ctx->stats[i].name, sizeof(ctx->stats[i].name), "%s", kClassName[i]);
+  hipSetDevice(device);
+  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipMalloc((void**)&ctx->linvT, 128 * 128 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&ctx->status, 64);
+  if (e == hipSuccess) e = hipMalloc((void**)&ctx->result, 64 * sizeof(double));
+  if (e != hipSuccess) {
+    lfm_ctx_destroy(ctx);
+    return LFM_E_HIP;
+  }
+  *out = ctx;
+  return LFM_OK;
+}
+
+void lfm_ctx_destroy(lfm_ctx* ctx) {
+  if (!ctx) return;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  lfm_farm_destroy(ctx);
+  for (void* p : {(void*)ctx->A, (void*)ctx->tab, (void*)ctx->tab32, (void*)ctx->par,
+                  (void*)ctx->xin, (void*)ctx->linvT, (void*)ctx->parts, (void*)ctx->status,
+                  (void*)ctx->result, (void*)ctx->farm_buf})
+    if (p) hipFree(p);
+  if (ctx->hpin) hipHostFree(ctx->hpin);
+  for (auto& p : ctx->pending) {
+    hipEventDestroy(p.a);
+    hipEventDestroy(p.b);
+  }
+  for (auto e : ctx->pool) hipEventDestroy(e);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+const char* lfm_last_error(const lfm_ctx* ctx) { return ctx ? ctx->err.c_str() : "null ctx"; }
+
+int lfm_ctx_synchronize(lfm_ctx* ctx) {
+  if (!ctx) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return finish(ctx);
+}
+
+int lfm_ctx_set_block(lfm_ctx* ctx, int nb) {
+  if (!ctx) return LFM_E_ARG;
+  if (nb != 0 && nb != 128) return set_err(ctx, LFM_E_ARG, "block size must be 128 (or 0)");
+  ctx->nb = 128;
+  return LFM_OK;
+}
+
+int lfm_mean_function_f64(lfm_ctx* ctx, const double* x, int64_t n, const lfm_hyp* hyp,
+                          double* out) {
+  int r = validate_x(ctx, x, n);
+  if (r) return r;
+  if (!out) return set_err(ctx, LFM_E_ARG, "out is NULL");
+  DeviceGuard g(ctx->device);
+  Staged st;
+  r = stage_hyp(ctx, hyp, x, n, false, &st);
+  if (r) return r;
+  r = check_mean_shape(ctx, n, hyp);
+  if (r) return r;
+  r = ensure(ctx, (void**)&ctx->xin, &ctx->xin_bytes, (size_t)n * 4 * 8);
+  if (r) return r;
+  hipMemcpyAsync(ctx->xin, x, n * 3 * 8, hipMemcpyHostToDevice, ctx->stream);
+  r = launch_mean(ctx, st.h, ctx->xin, n, ctx->xin + 3 * n);
+  if (r) return r;
+  hipMemcpyAsync(out, ctx->xin + 3 * n, n * 8, hipMemcpyDeviceToHost, ctx->stream);
+  return finish(ctx);
+}
+
+int lfm_h_f64(lfm_ctx* ctx, const lfm_hyp* hyp, const int64_t* j, const int64_t* k,
+              const double* t1, const double* t2, int64_t n, double* out) {
+  if (!ctx) return LFM_E_ARG;
+  if (!j || !k || !t1 || !t2 || !out || n < 1) return set_err(ctx, LFM_E_ARG, "bad h arguments");
+  DeviceGuard g(ctx->device);
+  Staged st;
+  int r = stage_hyp(ctx, hyp, nullptr, 0, false, &st);
+  if (r) return r;
+  r = ensure(ctx, (void**)&ctx->xin, &ctx->xin_bytes, (size_t)n * 5 * 8);
+  if (r) return r;
+  int64_t* dj = reinterpret_cast<int64_t*>(ctx->xin);
+  int64_t* dk = dj + n;
+  double* dt1 = ctx->xin + 2 * n;
+  double* dt2 = ctx->xin + 3 * n;
+  double* dout = ctx->xin + 4 * n;
+  hipMemcpyAsync(dj, j, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipMemcpyAsync(dk, k, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipMemcpyAsync(dt1, t1, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipMemcpyAsync(dt2, t2, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  r = launch_h(ctx, st.h, dj, dk, dt1, dt2, n, dout);
+  if (r) return r;
+  hipMemcpyAsync(out, dout, n * 8, hipMemcpyDeviceToHost, ctx->stream);
+  return finish(ctx);
+}
+
+int lfm_cross_covariance_f64(lfm_ctx* ctx, const double* x, int64_t n, const double* x2,
+                             int64_t m, const lfm_hyp* hyp, double* out, int64_t ldo) {
+  int r = validate_x(ctx, x, n);
+  if (r) return r;
+  r = validate_x(ctx, x2, m);
+  if (r) return r;
+  if (!out || ldo < m) return set_err(ctx, LFM_E_ARG, "out is NULL or ldo < m");
+  DeviceGuard g(ctx->device);
+  Staged st;
+  r = stage_hyp(ctx, hyp, nullptr, 0, false, &st);
+  if (r) return r;
+  r = ensure(ctx, (void**)&ctx->xin, &ctx->xin_bytes, (size_t)(n + m) * 3 * 8);
+  if (r) return r;
+  r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * m * 8);
+  if (r) return r;
+  hipMemcpyAsync(ctx->xin, x, n * 3 * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipMemcpyAsync(ctx->xin + 3 * n, x2, m * 3 * 8, hipMemcpyHostToDevice, ctx->stream);
+  r = launch_gram_direct<double>(ctx, st.h, ctx->xin, n, ctx->xin + 3 * n, m, 0.0, 0.0,
+                                 LFM_UPLO_FULL, ctx->A, m);
+  if (r) return r;
+  hipError_t e = hipMemcpy2DAsync(out, ldo * 8, ctx->A, m * 8, m * 8, n, hipMemcpyDeviceToHost,
+                                  ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "download cross-covariance");
+  return finish(ctx);
+}
+
+
+
+int lfm_gram_f64(lfm_ctx* ctx, const double* x, int64_t n, const lfm_hyp* hyp, double diag_add,
+                 int uplo, double* out, int64_t ldo) {
+  return gram_host<double>(ctx, x, n, hyp, diag_add, uplo, out, ldo);
+}
+
+int lfm_gram_f32(lfm_ctx* ctx, const double* x, int64_t n, const lfm_hyp* hyp, double diag_add,
+                 int uplo, float* out, int64_t ldo) {
+  return gram_host<float>(ctx, x, n, hyp, diag_add, uplo, out, ldo);
+}
+
+
+int lfm_gram_f64_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* hyp,
+                     double diag_add, int uplo, double* d_out, int64_t ldo) {
+  return gram_dev<double>(ctx, d_x, n, hyp, diag_add, uplo, d_out, ldo);
+}
+
+int lfm_gram_f32_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* hyp,
+                     double diag_add, int uplo, float* d_out, int64_t ldo) {
+  return gram_dev<float>(ctx, d_x, n, hyp, diag_add, uplo, d_out, ldo);
+}
+
+int lfm_mll_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n, const lfm_hyp* hyp,
+                int negative, double* out) {
+  int r = validate_x(ctx, x, n);
+  if (r) return r;
+  if (!y || !out) return set_err(ctx, LFM_E_ARG, "y / out is NULL");
+  r = check_hyp(ctx, hyp);
+  if (r) return r;
+  r = check_mean_shape(ctx, n, hyp);
+  if (r) return r;
+  DeviceGuard g(ctx->device);
+  if (n <= SMALL_MAX) {
+    lfm_problem p{x, y, n, *hyp};
+    int64_t idx = 0;
+    int st = 0;
+    r = small_batch(ctx, 1, &p, &idx, negative, out, &st);
+    if (r) return r;
+    if (st) return set_err(ctx, LFM_E_NOT_PD, "Cholesky failed: non-positive pivot");
+    return LFM_OK;
+  }
+  Staged st;
+  r = stage_hyp(ctx, hyp, x, n, true, &st);
+  if (r) return r;
+  r = ensure(ctx, (void**)&ctx->xin, &ctx->xin_bytes, (size_t)n * 4 * 8);
+  if (r) return r;
+  hipMemcpyAsync(ctx->xin, x, n * 3 * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipMemcpyAsync(ctx->xin + 3 * n, y, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  return mll_blocked(ctx, st, ctx->xin, ctx->xin + 3 * n, nullptr, n, hyp, negative, out);
+}
+
+int lfm_mll_f64_dev(lfm_ctx* ctx, const double* d_x, const double* d_y, int64_t n,
+                    const lfm_hyp* hyp, int negative, double* out) {
+  int r = validate_x(ctx, d_x, n);
+  if (r) return r;
+  if (!d_y || !out) return set_err(ctx, LFM_E_ARG, "y / out is NULL");
+  r = check_hyp(ctx, hyp);
+  if (r) return r;
+  r = check_mean_shape(ctx, n, hyp);
+  if (r) return r;
+  DeviceGuard g(ctx->device);
+  std::vector<double> xh((size_t)n * 3);
+  hipError_t e = hipMemcpyAsync(xh.data(), d_x, n * 3 * 8, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "read back x for layout detection");
+  if (n <= SMALL_MAX) {
+    std::vector<double> yh((size_t)n);
+    e = hipMemcpy(yh.data(), d_y, n * 8, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(ctx, e, "read back y");
+    return lfm_mll_f64(ctx, xh.data(), yh.data(), n, hyp, negative, out);
+  }
+  Staged st;
+  r = stage_hyp(ctx, hyp, xh.data(), n, true, &st);
+  if (r) return r;
+  return mll_blocked(ctx, st, d_x, d_y, nullptr, n, hyp, negative, out);
+}
+
+int lfm_mll_batch_f64(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, int negative,
+                      double* out, int* status) {
+  if (!ctx) return LFM_E_ARG;
+  if (nprob < 0 || (nprob > 0 && (!probs || !out)))
+    return set_err(ctx, LFM_E_ARG, "bad batch arguments");
+  DeviceGuard g(ctx->device);
+  std::vector<int64_t> small, big;
+  for (int64_t q = 0; q < nprob; ++q) {
+    const lfm_problem& p = probs[q];
+    int r = validate_x(ctx, p.x, p.n);
+    if (r) return r;
+    if (!p.y) return set_err(ctx, LFM_E_ARG, "problem y is NULL");
+    r = check_hyp(ctx, &p.hyp);
+    if (r) return r;
+    r = check_mean_shape(ctx, p.n, &p.hyp);
+    if (r) return r;
+    (p.n <= SMALL_MAX ? small : big).push_back(q);
+  }
+  int worst = LFM_OK;
+  if (!small.empty()) {
+    int r = small_batch(ctx, (int64_t)small.size(), probs, small.data(), negative, out, status);
+    if (r) return r;
+  }
+  for (int64_t q : big) {
+    int r = lfm_mll_f64(ctx, probs[q].x, probs[q].y, probs[q].n, &probs[q].hyp, negative, &out[q]);
+    if (status) status[q] = r;
+    if (r && r != LFM_E_NOT_PD) return r;
+  }
+  if (status)
+    for (int64_t q = 0; q < nprob; ++q)
+      if (status[q] == LFM_E_NOT_PD) worst = LFM_E_NOT_PD;
+  return worst;
+}
+
+int lfm_log_prob_f64(lfm_ctx* ctx, const double* loc, const double* scale, int64_t n,
+                     int64_t lds, const double* y, double* out) {
+  if (!ctx) return LFM_E_ARG;
+  if (!loc || !scale || !y || !out || n < 1 || lds < n)
+    return set_err(ctx, LFM_E_ARG, "bad log_prob arguments");
+  DeviceGuard g(ctx->device);
+  const int64_t Mp = round_up(n + 1, 128);
+  int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)Mp * Mp * sizeof(double));
+  if (r) return r;
+  r = ensure(ctx, (void**)&ctx->xin, &ctx->xin_bytes, (size_t)n * 2 * 8);
+  if (r) return r;
+  hipMemcpyAsync(ctx->xin, loc, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipMemcpyAsync(ctx->xin + n, y, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipError_t e = hipMemcpy2DAsync(ctx->A, Mp * 8, scale, lds * 8, n * 8, n, hipMemcpyHostToDevice,
+                                  ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "upload scale");
+  r = ensure_pinned(ctx, 1 << 16);
+  if (r) return r;
+  HypDev h{nullptr, nullptr, nullptr, 1, 1.0};
+  r = launch_augment(ctx, h, nullptr, ctx->xin + n, ctx->xin, n, ctx->A, Mp, Mp);
+  if (r) return r;
+  r = chol_factor_solve(ctx, ctx->A, Mp, n, Mp, 0, ctx->result);
+  if (r) return r;
+  double* hres = ctx->hpin + (ctx->hpin_bytes / 8 - 8);
+  hipMemcpyAsync(hres, ctx->result, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+  r = finish(ctx);
+  if (r) return r;
+  *out = hres[0];
+  if ((int)hres[3] != INT_MAX) {
+    *out = std::nan("");
+    return set_err(ctx, LFM_E_NOT_PD,
+                   "Cholesky failed: non-positive pivot at index " +
+                       std::to_string((long long)hres[3]));
+  }
+  return LFM_OK;
+}
+
+int lfm_dev_alloc(lfm_ctx* ctx, size_t bytes, void** out) {
+  if (!ctx || !out) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipMalloc(out, bytes ? bytes : 16);
+  return hip_fail(ctx, e, "lfm_dev_alloc");
+}
+
+int lfm_dev_free(lfm_ctx* ctx, void* p) {
+  if (!ctx) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  return hip_fail(ctx, hipFree(p), "lfm_dev_free");
+}
+
+int lfm_memcpy_h2d(lfm_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "h2d");
+  return finish(ctx);
+}
+
+int lfm_memcpy_d2h(lfm_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (!ctx) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "d2h");
+  return finish(ctx);
+}
+
+int lfm_profile_enable(lfm_ctx* ctx, int on) {
+  if (!ctx) return LFM_E_ARG;
+  ctx->prof = on != 0;
+  return LFM_OK;
+}
+
+int lfm_profile_reset(lfm_ctx* ctx) {
+  if (!ctx) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  finish(ctx);
+  for (int i = 0; i < K_NCLASS; ++i) {
+    ctx->stats[i].launches = 0;
+    ctx->stats[i].total_ms = 0;
+    ctx->stats[i].flops = 0;
+    ctx->stats[i].bytes = 0;
+  }
+  return LFM_OK;
+}
+
+int lfm_profile_read(lfm_ctx* ctx, lfm_kstat* stats, int max, int* count) {
+  if (!ctx || !count) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  finish(ctx);
+  *count = K_NCLASS;
+  for (int i = 0; i < std::min(max, (int)K_NCLASS); ++i) stats[i] = ctx->stats[i];
+  return LFM_OK;
+}
+
+// ------------------------------------------------------------- RCCL farm
+// librccl is opened lazily so the library loads (and the CPU tests run) without it.
+namespace {
+struct Rccl {
+  void* h = nullptr;
+  ncclResult_t (*getUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*commInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*allGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t,
+                            hipStream_t) = nullptr;
+  ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
+  const char* (*errStr)(ncclResult_t) = nullptr;
+};
+Rccl g_rccl;
+
+int rccl_load(lfm_ctx* ctx) {
+  if (g_rccl.h) return LFM_OK;
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) return set_err(ctx, LFM_E_RCCL, std::string("dlopen librccl: ") + dlerror());
+  g_rccl.getUniqueId = (decltype(g_rccl.getUniqueId))dlsym(h, "ncclGetUniqueId");
+  g_rccl.commInitRank = (decltype(g_rccl.commInitRank))dlsym(h, "ncclCommInitRank");
+  g_rccl.allGather = (decltype(g_rccl.allGather))dlsym(h, "ncclAllGather");
+  g_rccl.commDestroy = (decltype(g_rccl.commDestroy))dlsym(h, "ncclCommDestroy");
+  g_rccl.errStr = (decltype(g_rccl.errStr))dlsym(h, "ncclGetErrorString");
+  if (!g_rccl.getUniqueId || !g_rccl.commInitRank || !g_rccl.allGather || !g_rccl.commDestroy)
+    return set_err(ctx, LFM_E_RCCL, "librccl lacks a required symbol");
+  g_rccl.h = h;
+  return LFM_OK;
+}
+
+int rccl_fail(lfm_ctx* ctx, ncclResult_t r, const char* what) {
+  if (r == ncclSuccess) return LFM_OK;
+  return set_err(ctx, LFM_E_RCCL,
+                 std::string(what) + ": " + (g_rccl.errStr ? g_rccl.errStr(r) : "rccl error"));
+}
+}  // namespace
+
+int lfm_farm_unique_id(lfm_ctx* ctx, unsigned char id[128]) {
+  if (!ctx || !id) return LFM_E_ARG;
+  int r = rccl_load(ctx);
+  if (r) return r;
+  DeviceGuard g(ctx->device);
+  ncclUniqueId u;
+  r = rccl_fail(ctx, g_rccl.getUniqueId(&u), "ncclGetUniqueId");
+  if (r) return r;
+  std::memcpy(id, u.internal, 128);
+  return LFM_OK;
+}
+
+int lfm_farm_init(lfm_ctx* ctx, const unsigned char id[128], int nranks, int rank) {
+  if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return LFM_E_ARG;
+  int r = rccl_load(ctx);
+  if (r) return r;
+  DeviceGuard g(ctx->device);
+  if (ctx->comm) lfm_farm_destroy(ctx);
+  ncclUniqueId u;
+  std::memcpy(u.internal, id, 128);
+  ncclComm_t comm = nullptr;
+  r = rccl_fail(ctx, g_rccl.commInitRank(&comm, nranks, u, rank), "ncclCommInitRank");
+  if (r) return r;
+  ctx->comm = comm;
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  return LFM_OK;
+}
+
+int lfm_farm_allgather_f64(lfm_ctx* ctx, const double* send, int64_t count, double* recv) {
+  if (!ctx || !send || !recv || count < 1) return LFM_E_ARG;
+  if (!ctx->comm) return set_err(ctx, LFM_E_STATE, "farm not initialised");
+  DeviceGuard g(ctx->device);
+  const size_t bytes = (size_t)count * 8 * (1 + ctx->nranks);
+  int r = ensure(ctx, (void**)&ctx->farm_buf, &ctx->farm_bytes, bytes);
+  if (r) return r;
+  double* dsend = ctx->farm_buf;
+  double* drecv = ctx->farm_buf + count;
+  hipMemcpyAsync(dsend, send, count * 8, hipMemcpyHostToDevice, ctx->stream);
+  r = rccl_fail(ctx,
+                g_rccl.allGather(dsend, drecv, (size_t)count, ncclFloat64, (ncclComm_t)ctx->comm,
+                                 ctx->stream),
+                "ncclAllGather");
+  if (r) return r;
+  hipMemcpyAsync(recv, drecv, (size_t)count * ctx->nranks * 8, hipMemcpyDeviceToHost, ctx->stream);
+  return finish(ctx);
+}
+
+int lfm_farm_destroy(lfm_ctx* ctx) {
+  if (!ctx) return LFM_E_ARG;
+  if (ctx->comm && g_rccl.commDestroy) g_rccl.commDestroy((ncclComm_t)ctx->comm);
+  ctx->comm = nullptr;
+  ctx->nranks = 0;
+  ctx->rank = -1;
+  return LFM_OK;
+}
+
+int lfm_probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double* ms) {
+  if (!ctx || !tflops || !ms || nblocks < 1 || iters < 1) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_mfma_f64(ctx, nblocks, iters, tflops, ms);
+}
+
+int lfm_probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d) {
+  if (!ctx || !a || !b || !d) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_mfma_f64_layout(ctx, a, b, d);
+}
+
+}  // extern "C"

@@ -1,0 +1,168 @@
+// lfm_internal.h — shared declarations of the HIP implementation behind include/lfm.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/lfm.h"
+
+namespace lfm {
+
+// Kernel classes tracked by the profiler (lfm_profile_*).
+enum KClass {
+  K_TABLES = 0,   // per-gene erf/exp tables of the structured gram
+  K_GRAM_GRID,    // structured (shared uniform time grid) gram fill
+  K_GRAM_DIRECT,  // general per-pair gram fill (any x, any flags)
+  K_AUGMENT,      // residual row + padding rows of the augmented factor
+  K_POTRF,        // diagonal-block factor + inverse (one workgroup)
+  K_TRSM,         // panel solve  X = A * Linv^T  (fp64 MFMA)
+  K_SYRK,         // trailing update C -= P P^T   (fp64 MFMA)
+  K_FINALIZE,     // logdet + quadratic form -> scalar
+  K_SMALL,        // one-workgroup-per-problem fused small-N MLL
+  K_MEAN,         // mean_function
+  K_NCLASS
+};
+
+extern const char* const kClassName[K_NCLASS];
+
+// Structure of x detected on the host: rows come in blocks of T consecutive rows
+// that share one uniform time vector t[tau] = t0 + tau*dt, one gene index per
+// block and flag 1 — the layout dataset_3d (src/dataset.py:358-399) produces.
+struct GridLayout {
+  bool ok = false;
+  int T = 0;          // timepoints per block
+  int nblk = 0;       // number of blocks (= n / T)
+  double t0 = 0, dt = 0;
+  std::vector<double> times;   // [T]  the actual time values of block 0
+  std::vector<int> block_gene; // [nblk] clamped gene index per block
+};
+
+struct ProfEvent {
+  int cls;
+  hipEvent_t a, b;
+  double flops, bytes;
+};
+
+}  // namespace lfm
+
+struct lfm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  int nb = 128;  // Cholesky block size
+
+  // device workspace, grown on demand
+  double* A = nullptr;   size_t A_bytes = 0;     // augmented factor (Mp x Mp) / generic matrix
+  double* tab = nullptr; size_t tab_bytes = 0;   // gene tables (fp64)
+  float* tab32 = nullptr; size_t tab32_bytes = 0;// gene tables (fp32 copy)
+  double* par = nullptr; size_t par_bytes = 0;   // packed hyperparameters + layout
+  double* xin = nullptr; size_t xin_bytes = 0;   // staged x / y / loc inputs
+  double* linvT = nullptr;                       // NB x NB inverse of the diagonal block, transposed
+  double* parts = nullptr; size_t parts_cap = 0; // per-block logdet partials
+  int* status = nullptr;                         // [0] first failing pivot (INT_MAX = none)
+  double* result = nullptr;                      // [0..] scalar results
+
+  // pinned host staging
+  double* hpin = nullptr; size_t hpin_bytes = 0;
+
+  // profiling
+  bool prof = false;
+  std::vector<lfm::ProfEvent> pending;
+  std::vector<hipEvent_t> pool;
+  lfm_kstat stats[lfm::K_NCLASS];
+
+  // farm (RCCL)
+  void* comm = nullptr;
+  int nranks = 0, rank = -1;
+  double* farm_buf = nullptr; size_t farm_bytes = 0;
+};
+
+// ---------------------------------------------------------------- helpers
+namespace lfm {
+
+int set_err(lfm_ctx* ctx, int code, const std::string& msg);
+int hip_fail(lfm_ctx* ctx, hipError_t e, const char* what);
+int ensure(lfm_ctx* ctx, void** p, size_t* cap, size_t bytes);
+int ensure_pinned(lfm_ctx* ctx, size_t bytes);
+
+// profiling hooks around a launch on ctx->stream
+void prof_begin(lfm_ctx* ctx, int cls, hipEvent_t* a);
+void prof_end(lfm_ctx* ctx, int cls, hipEvent_t a, double flops, double bytes);
+int prof_flush(lfm_ctx* ctx);
+
+GridLayout detect_grid(const double* x, int64_t n, int64_t G);
+int gene_clamp_host(double g, int64_t G);
+
+// device-side gene index semantics: trunc toward zero, negative wraps, clamp
+__host__ __device__ inline int gene_index(double g, int G) {
+  double tg = trunc(g);
+  if (tg < 0) tg += (double)G;
+  if (!(tg >= 0)) tg = 0;              // also catches NaN
+  if (tg > (double)(G - 1)) tg = (double)(G - 1);
+  return (int)tg;
+}
+__host__ __device__ inline long long flag_int(double f) {
+  double tf = trunc(f);
+  if (!(tf == tf)) return 0;
+  if (tf > 4e18) tf = 4e18;
+  if (tf < -4e18) tf = -4e18;
+  return (long long)tf;
+}
+
+// ------------------------------------------------------ launch wrappers
+// Packed parameter block on the device (doubles):
+//   [0,G) D   [G,2G) S   [2G,3G) B   then layout-specific arrays.
+struct HypDev {
+  const double* D;
+  const double* S;
+  const double* B;
+  int G;
+  double l;
+};
+
+// One problem of the fused small-N kernel (device pointers into one packed buffer).
+struct SmallProb {
+  const double* x;
+  const double* y;
+  const double* D;
+  const double* S;
+  const double* B;
+  int n, G;
+  double l, jitter, noise;
+};
+constexpr int SMALL_MAX = 128;  // largest n handled by small_mll_kernel
+
+// gram kernels (lfm_gram.hip)
+int launch_tables(lfm_ctx* ctx, const HypDev& h, const GridLayout& lay, const double* d_times,
+                  double* tab);
+// diagonal elements get (v + da1) + da2 — (K + jitter I) + sigma^2 I, objectives.py:71-72
+template <typename OutT>
+int launch_gram_grid(lfm_ctx* ctx, const HypDev& h, const GridLayout& lay, const double* tab,
+                     const int* bg, int64_t n, double da1, double da2, int uplo, OutT* out,
+                     int64_t ldo);
+template <typename OutT>
+int launch_gram_direct(lfm_ctx* ctx, const HypDev& h, const double* x, int64_t n,
+                       const double* x2, int64_t m, double da1, double da2, int uplo, OutT* out,
+                       int64_t ldo);
+int launch_mean(lfm_ctx* ctx, const HypDev& h, const double* x, int64_t n, double* out);
+int launch_h(lfm_ctx* ctx, const HypDev& h, const int64_t* j, const int64_t* k, const double* t1,
+             const double* t2, int64_t n, double* out);
+int launch_augment(lfm_ctx* ctx, const HypDev& h, const double* x, const double* y,
+                   const double* loc, int64_t n, double* A, int64_t lda, int64_t Mp);
+
+// cholesky kernels (lfm_chol.hip)
+int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,
+                      double* d_out);
+size_t tables_doubles(int G, int T);
+int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn,
+                       int negative, double* d_out, int* d_status);
+
+// diagnostics (lfm_probe.hip)
+int probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double* ms);
+int probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d);
+
+}  // namespace lfm

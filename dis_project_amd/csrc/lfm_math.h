@@ -1,0 +1,76 @@
+// lfm_math.h — per-pair SIM kernel math (device), shared by the gram and small-N kernels.
+// Each function restates the reference expression it cites, in the same operation order.
+#pragma once
+#include "lfm_internal.h"
+
+namespace lfm {
+
+static constexpr double kSqrtPi = 1.7724538509055160273;
+
+// ------------------------------------------------------------- per-pair math
+// h(j,k,t1,t2), model.py:315-365.
+__device__ __forceinline__ double h_ref(const HypDev& p, int j, int k, double t1, double t2) {
+  const double l = p.l;
+  const double gk = p.D[k] * l / 2.0;                           // gamma(k), model.py:367-369
+  const double tdist = t2 - t1;
+  const double multiplier = exp(gk * gk) / (p.D[j] + p.D[k]);
+  const double first_multiplier = exp(-p.D[k] * tdist);
+  const double first_erf = erf((tdist / l) - gk) + erf(t1 / l + gk);
+  const double second_multiplier = exp(-(p.D[k] * t2 + p.D[j] * t1));
+  const double second_erf = erf((t2 / l) - gk) + erf(gk);
+  return multiplier * (first_multiplier * first_erf - second_multiplier * second_erf);
+}
+
+// kernel_xx, model.py:197-235.
+__device__ __forceinline__ double kxx_ref(const HypDev& p, double ta, int j, double tb, int k) {
+  const double mult = p.S[j] * p.S[k] * p.l * kSqrtPi * 0.5;
+  return mult * (h_ref(p, k, j, tb, ta) + h_ref(p, j, k, ta, tb));
+}
+
+// kernel_xf, model.py:237-282 (the row whose flag is non-zero is the gene row).
+__device__ __forceinline__ double kxf_ref(const HypDev& p, double ta, double ga, double fa,
+                                          double tb, double gb) {
+  const bool a_is_latent = (fa == 0.0);
+  const double tg = a_is_latent ? tb : ta;
+  const double gg = a_is_latent ? gb : ga;
+  const double tl = a_is_latent ? ta : tb;
+  const int j = gene_index(gg, p.G);
+  const double l = p.l;
+  const double gj = p.D[j] * l / 2.0;
+  const double t_dist = tg - tl;
+  const double first_term = 0.5 * l * kSqrtPi * p.S[j];
+  const double e1 = exp(gj * gj);
+  const double e2 = exp(-p.D[j] * t_dist);
+  const double erfs = erf((t_dist / l) - gj) + erf(tl / l + gj);
+  return first_term * e1 * e2 * erfs;
+}
+
+// kernel_ff, model.py:284-312 (divides by 2*l, not l^2: kept for parity).
+__device__ __forceinline__ double kff_ref(const HypDev& p, double ta, double tb) {
+  const double d = ta - tb;
+  return exp(-((d * d) / (2.0 * p.l)));
+}
+
+// Flag-switched kernel, model.py:152-195. Branches whose integer switch is zero
+// are not evaluated (the reference evaluates them and multiplies by 0).
+__device__ __forceinline__ double kernel_ref(const HypDev& p, double ta, double ga, double fa,
+                                             double tb, double gb, double fb) {
+  const long long f1 = flag_int(fa), f2 = flag_int(fb);
+  const long long s_xx = f1 * f2, s_ff = (1 - f1) * (1 - f2);
+  const long long s_xf = f1 * (1 - f2), s_fx = (1 - f1) * f2;
+  double v = 0.0;
+  if (s_xx) v += (double)s_xx * kxx_ref(p, ta, gene_index(ga, p.G), tb, gene_index(gb, p.G));
+  if (s_ff) v += (double)s_ff * kff_ref(p, ta, tb);
+  if (s_xf) v += (double)s_xf * kxf_ref(p, ta, ga, fa, tb, gb);
+  if (s_fx) v += (double)s_fx * kxf_ref(p, tb, gb, fb, ta, ga);
+  return v;
+}
+
+// mean_function, model.py:143-149: m[i] = (B/D)[i / (n/G)] * int(x[i,2]).
+__device__ __forceinline__ double mean_at(const HypDev& p, const double* x, int64_t i,
+                                          int64_t bs) {
+  const int g = (int)(i / bs);
+  return (p.B[g] / p.D[g]) * (double)flag_int(x[i * 3 + 2]);
+}
+
+}  // namespace lfm

@@ -1,0 +1,170 @@
+/*
+ * lfm.h — C-ABI of the MI355X-native SIM latent-force-model hot path.
+ *
+ * This is the drop-in boundary for the GPJax hot path of wejpurvis/DIS_project:
+ * the SIM multi-output covariance (src/model.py:152-414) and the Cholesky-based
+ * log marginal likelihood (src/objectives.py:21-78 -> gpjax 0.8.2
+ * GaussianDistribution.log_prob). The reference is pure Python/JAX and has no
+ * FFI of its own; each entry point below names the reference interface it
+ * replaces. Plain pointers and sizes only (no framework types).
+ *
+ * Conventions
+ *   - x arrays are N x 3 row-major fp64: (time, gene index, flag), the layout of
+ *     dataset_3d (src/dataset.py:358-399).
+ *   - All host buffers are owned by the caller and are not retained after return.
+ *     Every call is synchronous at return unless its name ends in _async.
+ *   - Device workspace (the Mp x Mp factor, tables, scratch) is owned by the ctx,
+ *     grown on demand and reused. A ctx is bound to one device and is NOT
+ *     thread-safe: create one ctx per device per host thread.
+ *   - Return value: LFM_OK (0) or an LFM_E_* code; lfm_last_error() has the text.
+ *     LFM_E_NOT_PD mirrors JAX's silent NaN on a failed Cholesky: the scalar
+ *     output is set to NaN and the failing pivot index is in lfm_last_error().
+ */
+#ifndef LFM_H
+#define LFM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LFM_ABI_VERSION 1
+
+enum {
+  LFM_OK = 0,
+  LFM_E_ARG = 1,    /* bad shape / pointer / value                        */
+  LFM_E_HIP = 2,    /* HIP runtime error (text in lfm_last_error)          */
+  LFM_E_NOT_PD = 3, /* Cholesky pivot <= 0 or NaN; scalar result is NaN    */
+  LFM_E_OOM = 4,    /* device allocation failed                            */
+  LFM_E_RCCL = 5,   /* RCCL not loadable / collective failed               */
+  LFM_E_STATE = 6   /* call out of order (e.g. farm not initialised)       */
+};
+
+/* gram / cross-covariance output selection */
+enum { LFM_UPLO_FULL = 0, LFM_UPLO_LOWER = 1 };
+
+typedef struct lfm_ctx lfm_ctx;
+
+/*
+ * Constrained hyperparameters of ExactLFM (src/model.py:64-121).
+ *   true_d / true_s / true_b : [num_genes] decay D, sensitivity S, basal B
+ *   l                        : lengthscale (model.py:111-121)
+ *   obs_stddev               : observation std-dev; sigma^2 = obs_stddev^2 (objectives.py:66)
+ *   jitter                   : static jitter added to the gram diagonal (objectives.py:71)
+ * Gene indices read from x[:,1] are truncated toward zero, negative ones wrap by
+ * +num_genes and the result is clamped to [0, num_genes-1] (JAX gather semantics).
+ */
+typedef struct {
+  int64_t num_genes;
+  const double* true_d;
+  const double* true_s;
+  const double* true_b;
+  double l;
+  double obs_stddev;
+  double jitter;
+} lfm_hyp;
+
+/* One independent marginal-likelihood problem of a batch (restart / ablation). */
+typedef struct {
+  const double* x; /* [n x 3] host */
+  const double* y; /* [n]     host */
+  int64_t n;
+  lfm_hyp hyp;
+} lfm_problem;
+
+/* Per-kernel-class timing, filled when profiling is on (HIP events on the ctx stream). */
+typedef struct {
+  char name[32];
+  int64_t launches;
+  double total_ms;   /* sum of per-launch HIP-event durations              */
+  double flops;      /* algorithmic flops over all launches                */
+  double bytes;      /* algorithmic HBM bytes over all launches            */
+} lfm_kstat;
+
+/* ---------------------------------------------------------------- context */
+int lfm_abi_version(void);
+int lfm_device_count(int* out);
+int lfm_ctx_create(int device, lfm_ctx** out);
+void lfm_ctx_destroy(lfm_ctx* ctx);
+const char* lfm_last_error(const lfm_ctx* ctx);
+int lfm_ctx_synchronize(lfm_ctx* ctx);
+/* Block size of the blocked Cholesky (64 or 128); 0 restores the default. */
+int lfm_ctx_set_block(lfm_ctx* ctx, int nb);
+
+/* --------------------------------------------- ExactLFM surface (model.py) */
+/* mean_function (model.py:124-149): out[i] = (B/D)[i / (n / num_genes)] * int(x[i,2]). */
+int lfm_mean_function_f64(lfm_ctx* ctx, const double* x, int64_t n, const lfm_hyp* hyp,
+                          double* out);
+
+/* cross_covariance(kernel, x, x2) (model.py:372-394): out[i*ldo + j] = kernel(x[i], x2[j]),
+ * the flag-switched kernel of model.py:152-195 (kxx / kff / kxf / kfx). */
+int lfm_cross_covariance_f64(lfm_ctx* ctx, const double* x, int64_t n, const double* x2,
+                             int64_t m, const lfm_hyp* hyp, double* out, int64_t ldo);
+
+/* h(j, k, t1, t2) of model.py:315-365 element-wise over n tuples (gene indices clamped
+ * as above); exposes the convolution term on its own for known-answer tests. */
+int lfm_h_f64(lfm_ctx* ctx, const lfm_hyp* hyp, const int64_t* j, const int64_t* k,
+              const double* t1, const double* t2, int64_t n, double* out);
+
+/* gram(kernel, x) (model.py:396-414) plus diag_add on the diagonal; uplo = LFM_UPLO_FULL
+ * writes the dense n x n, LFM_UPLO_LOWER computes only j <= i (the upper part of a host
+ * output is zero-filled, of a device output left untouched). */
+int lfm_gram_f64(lfm_ctx* ctx, const double* x, int64_t n, const lfm_hyp* hyp, double diag_add,
+                 int uplo, double* out, int64_t ldo);
+/* fp32 gram (arithmetic and output in fp32; per-gene tables built in fp64). */
+int lfm_gram_f32(lfm_ctx* ctx, const double* x, int64_t n, const lfm_hyp* hyp, double diag_add,
+                 int uplo, float* out, int64_t ldo);
+
+/* --------------------------------- CustomConjMLL.step (objectives.py:21-78) */
+/* out = constant * log N(y; m, K + jitter I + obs_stddev^2 I), constant = -1 if negative. */
+int lfm_mll_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n, const lfm_hyp* hyp,
+                int negative, double* out);
+/* nprob independent problems; out[p] per problem (NaN where not PD); status[p] optional. */
+int lfm_mll_batch_f64(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, int negative,
+                      double* out, int* status);
+
+/* ------------------- GaussianDistribution(loc, scale).log_prob(y) (gpjax 0.8.2) */
+/* scale is a dense SPD n x n (row-major, leading dim lds; lower triangle read). */
+int lfm_log_prob_f64(lfm_ctx* ctx, const double* loc, const double* scale, int64_t n,
+                     int64_t lds, const double* y, double* out);
+
+/* ----------------------- device-resident variants (inputs already in HBM) */
+int lfm_dev_alloc(lfm_ctx* ctx, size_t bytes, void** out);
+int lfm_dev_free(lfm_ctx* ctx, void* p);
+int lfm_memcpy_h2d(lfm_ctx* ctx, void* dst, const void* src, size_t bytes);
+int lfm_memcpy_d2h(lfm_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* As lfm_mll_f64 with x / y already on the ctx's device. */
+int lfm_mll_f64_dev(lfm_ctx* ctx, const double* d_x, const double* d_y, int64_t n,
+                    const lfm_hyp* hyp, int negative, double* out);
+/* As lfm_gram_f64 / _f32 with x and out on the device. */
+int lfm_gram_f64_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* hyp,
+                     double diag_add, int uplo, double* d_out, int64_t ldo);
+int lfm_gram_f32_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* hyp,
+                     double diag_add, int uplo, float* d_out, int64_t ldo);
+
+/* ------------------------------------------------------------- profiling */
+int lfm_profile_enable(lfm_ctx* ctx, int on);
+int lfm_profile_reset(lfm_ctx* ctx);
+/* Copies up to max entries; *count = number of kernel classes seen. */
+int lfm_profile_read(lfm_ctx* ctx, lfm_kstat* stats, int max, int* count);
+
+/* -------------------------------- multi-GPU farm: RCCL all-gather over xGMI */
+/* Rank 0 creates the 128-byte unique id; the caller ships it to every rank. */
+int lfm_farm_unique_id(lfm_ctx* ctx, unsigned char id[128]);
+int lfm_farm_init(lfm_ctx* ctx, const unsigned char id[128], int nranks, int rank);
+/* All-gather count fp64 per rank (host in, host out: recv holds nranks*count). */
+int lfm_farm_allgather_f64(lfm_ctx* ctx, const double* send, int64_t count, double* recv);
+int lfm_farm_destroy(lfm_ctx* ctx);
+
+/* ------------------------------------------------------------ diagnostics */
+/* Throughput probe of v_mfma_f64_16x16x4_f64: *tflops over a grid of nblocks x 256. */
+int lfm_probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double* ms);
+/* Layout probe: D = A(16x4) * B(4x16) on one wave; A,B,D row-major host arrays. */
+int lfm_probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LFM_H */

@@ -1,0 +1,259 @@
+"""CPU oracle for the SIM latent-force-model MLL hot path — TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg
+may import this module, and only as the checker / the timed CPU baseline. The
+product path (``dis_project_amd``) never imports it and has no CPU fallback.
+
+What it restates (wejpurvis/DIS_project @ 2024-08-07):
+  * ``h``           src/model.py:315-365
+  * ``gamma``       src/model.py:367-369
+  * ``kernel_xx``   src/model.py:197-235
+  * ``kernel_xf``   src/model.py:237-282
+  * ``kernel_ff``   src/model.py:284-312 (divides by 2*l, kept)
+  * ``kernel``      src/model.py:152-195 (flag switches: all four branches are
+                    evaluated and multiplied by their integer switch, as the
+                    reference does under vmap)
+  * ``cross_covariance`` / ``gram``  src/model.py:372-414
+  * ``mean_function``                src/model.py:124-149 (block position, not x[:,1])
+  * ``mll``         src/objectives.py:21-78 -> gpjax 0.8.2 GaussianDistribution.log_prob:
+                    -1/2 (n log 2pi + logdet S + r^T S^{-1} r), logdet and solve through
+                    a Cholesky factor (cola Cholesky -> LAPACK potrf); a failed
+                    factorisation yields NaN (JAX semantics).
+  * ``dataset_3d``  src/dataset.py:358-399 (row layout of x / y)
+
+PARITY STATUS: **parity unpinned** by the reference itself. The reference is pure
+JAX/GPJax (jax 0.4.28, gpjax 0.8.2, cola-ml 0.0.5 pinned in environment.yml); none
+of them is installed in this image (ModuleNotFoundError, not a permission denial)
+and the reference ships no tests, fixtures or golden vectors.
+This restatement is instead pinned by:
+  * known-answer tests derived from the reference formulas (t = 0 rows vanish;
+    all-zero times give a diagonal Sigma with a closed-form log-density; exact
+    symmetry of kxx);
+  * 50-digit mpmath evaluation of ``h`` (``h_mpmath``);
+  * a scalar pure-Python restatement (``kernel_scalar``) that shares no code with
+    the vectorised one;
+  * an independent cross-read of the GPyTorch twin's ``h``
+    (src/gpytorch_alfi/model_alfi.py:343-378), which agrees term by term.
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import scipy.linalg
+import scipy.special
+
+SQRT_PI = math.sqrt(math.pi)
+LOG_2PI = math.log(2.0 * math.pi)
+
+
+# ------------------------------------------------------------------ indices
+def gene_index(g, G):
+    """int(x[1]) with JAX gather semantics: truncate, wrap negatives, clamp."""
+    g = np.trunc(np.asarray(g, dtype=np.float64))
+    g = np.where(g < 0, g + G, g)
+    g = np.where(np.isnan(g), 0, g)
+    return np.clip(g, 0, G - 1).astype(np.int64)
+
+
+def flag_int(f):
+    f = np.trunc(np.asarray(f, dtype=np.float64))
+    return np.where(np.isnan(f), 0, f).astype(np.int64)
+
+
+# --------------------------------------------------------------- kernel math
+def gamma(D, l, k):
+    """model.py:367-369."""
+    return (D[k] * l) / 2
+
+
+def h(D, l, j, k, t1, t2):
+    """model.py:315-365, vectorised over broadcastable j, k, t1, t2."""
+    t_dist = t2 - t1
+    gk = gamma(D, l, k)
+    multiplier = np.exp(gk**2) / (D[j] + D[k])
+    first_multiplier = np.exp(-D[k] * t_dist)
+    first_erf_terms = scipy.special.erf((t_dist / l) - gk) + scipy.special.erf(t1 / l + gk)
+    second_multiplier = np.exp(-(D[k] * t2 + D[j] * t1))
+    second_erf_terms = scipy.special.erf((t2 / l) - gk) + scipy.special.erf(gk)
+    return multiplier * (first_multiplier * first_erf_terms - second_multiplier * second_erf_terms)
+
+
+def kernel_xx(D, S, l, ta, ja, tb, jb):
+    """model.py:197-235; ja / jb are clamped integer gene indices."""
+    mult = S[ja] * S[jb] * l * SQRT_PI * 0.5
+    return mult * (h(D, l, jb, ja, tb, ta) + h(D, l, ja, jb, ta, tb))
+
+
+def kernel_xf(D, S, l, ta, ga, fa, tb, gb):
+    """model.py:237-282: the row whose flag (as float) is 0 is the latent row."""
+    a_lat = fa == 0
+    t_gene = np.where(a_lat, tb, ta)
+    g_gene = np.where(a_lat, gb, ga)
+    t_lat = np.where(a_lat, ta, tb)
+    j = gene_index(g_gene, D.shape[0])
+    t_dist = t_gene - t_lat
+    gj = gamma(D, l, j)
+    first_term = 0.5 * l * SQRT_PI * S[j]
+    first_expon_term = np.exp(gj**2)
+    second_expon_term = np.exp(-D[j] * t_dist)
+    erf_terms = scipy.special.erf((t_dist / l) - gj) + scipy.special.erf(t_lat / l + gj)
+    return first_term * first_expon_term * second_expon_term * erf_terms
+
+
+def kernel_ff(l, ta, tb):
+    """model.py:284-312."""
+    sq_dist = np.square(ta - tb)
+    sq_dist = sq_dist / (2 * l)
+    return np.exp(-sq_dist)
+
+
+def kernel_pairs(xa, xb, D, S, l):
+    """model.py:152-195 over broadcast rows xa[..., 3], xb[..., 3]."""
+    G = D.shape[0]
+    ta, ga, fa = xa[..., 0], xa[..., 1], xa[..., 2]
+    tb, gb, fb = xb[..., 0], xb[..., 1], xb[..., 2]
+    f1, f2 = flag_int(fa), flag_int(fb)
+    kxx_switch = f1 * f2
+    kff_switch = (1 - f1) * (1 - f2)
+    kxf_switch = f1 * (1 - f2)
+    kxf_t_switch = (1 - f1) * f2
+    with np.errstate(over="ignore", invalid="ignore"):
+        return (
+            kxx_switch * kernel_xx(D, S, l, ta, gene_index(ga, G), tb, gene_index(gb, G))
+            + kff_switch * kernel_ff(l, ta, tb)
+            + kxf_switch * kernel_xf(D, S, l, ta, ga, fa, tb, gb)
+            + kxf_t_switch * kernel_xf(D, S, l, tb, gb, fb, ta, ga)
+        )
+
+
+def cross_covariance(x, y, D, S, l, chunk=256):
+    """model.py:372-394 (vmap over rows of x, then rows of y), row-chunked."""
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64)
+    out = np.empty((x.shape[0], y.shape[0]))
+    for i0 in range(0, x.shape[0], chunk):
+        xa = x[i0:i0 + chunk, None, :]
+        out[i0:i0 + chunk] = kernel_pairs(xa, y[None, :, :], D, S, l)
+    return out
+
+
+def gram(x, D, S, l):
+    """model.py:396-414 (the dense matrix behind cola.PSD(Dense(.)))."""
+    return cross_covariance(x, x, D, S, l)
+
+
+def mean_function(x, D, B, num_genes):
+    """model.py:124-149: block position i // (N // G), times int(flag)."""
+    x = np.asarray(x, np.float64)
+    f = flag_int(x[:, 2:])
+    block_size = x.shape[0] // num_genes
+    mean = (B / D).reshape(-1, 1)
+    mean = np.repeat(mean, block_size, axis=0).reshape(-1, 1)
+    return mean * f
+
+
+# ----------------------------------------------------------------------- MLL
+def log_prob(loc, Sigma, y):
+    """gpjax 0.8.2 GaussianDistribution.log_prob with a Cholesky-backed PSD scale."""
+    n = loc.shape[-1]
+    diff = y - loc
+    try:
+        c = scipy.linalg.cho_factor(Sigma, lower=True, check_finite=False)
+    except (np.linalg.LinAlgError, scipy.linalg.LinAlgError):
+        return float("nan")
+    L = np.tril(c[0])
+    d = np.diag(L)
+    if not np.all(np.isfinite(d)) or np.any(d <= 0):
+        return float("nan")
+    logdet = 2.0 * np.sum(np.log(d))
+    quad = diff @ scipy.linalg.cho_solve(c, diff, check_finite=False)
+    return float(-0.5 * (n * LOG_2PI + logdet + quad))
+
+
+def sigma(x, D, S, l, obs_stddev, jitter):
+    """objectives.py:66-73: Sigma = (K + jitter I) + obs_stddev^2 I."""
+    n = x.shape[0]
+    K = gram(x, D, S, l)
+    K = K + np.eye(n) * jitter
+    return K + np.eye(n) * (obs_stddev**2)
+
+
+def mll(x, y, D, S, B, l, obs_stddev, jitter, negative=False):
+    """CustomConjMLL(negative).step (objectives.py:21-78)."""
+    D = np.asarray(D, np.float64)
+    S = np.asarray(S, np.float64)
+    B = np.asarray(B, np.float64)
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64).reshape(-1)
+    mx = mean_function(x, D, B, D.shape[0]).reshape(-1)
+    Sig = sigma(x, D, S, l, obs_stddev, jitter)
+    constant = -1.0 if negative else 1.0
+    return constant * log_prob(mx, Sig, y)
+
+
+# -------------------------------------------------- scalar restatement (math)
+def h_scalar(D, l, j, k, t1, t2):
+    t_dist = t2 - t1
+    gk = D[k] * l / 2
+    mult = math.exp(gk * gk) / (D[j] + D[k])
+    a = math.exp(-D[k] * t_dist) * (math.erf(t_dist / l - gk) + math.erf(t1 / l + gk))
+    b = math.exp(-(D[k] * t2 + D[j] * t1)) * (math.erf(t2 / l - gk) + math.erf(gk))
+    return mult * (a - b)
+
+
+def kernel_scalar(xa, xb, D, S, l):
+    """Pure-Python loop restatement of model.py:152-312 for one pair of rows."""
+    G = len(D)
+
+    def gi(g):
+        g = math.trunc(g)
+        if g < 0:
+            g += G
+        return int(min(max(g, 0), G - 1))
+
+    f1, f2 = math.trunc(xa[2]), math.trunc(xb[2])
+    val = 0.0
+    if f1 * f2:
+        j, k = gi(xa[1]), gi(xb[1])
+        mult = S[j] * S[k] * l * SQRT_PI * 0.5
+        val += f1 * f2 * mult * (h_scalar(D, l, k, j, xb[0], xa[0]) + h_scalar(D, l, j, k, xa[0], xb[0]))
+    if (1 - f1) * (1 - f2):
+        val += (1 - f1) * (1 - f2) * math.exp(-((xa[0] - xb[0]) ** 2) / (2 * l))
+    for sw, ra, rb in ((f1 * (1 - f2), xa, xb), ((1 - f1) * f2, xb, xa)):
+        if sw:
+            gene, lat = (rb, ra) if ra[2] == 0 else (ra, rb)
+            j = gi(gene[1])
+            td = gene[0] - lat[0]
+            gj = D[j] * l / 2
+            val += sw * (0.5 * l * SQRT_PI * S[j] * math.exp(gj * gj) * math.exp(-D[j] * td)
+                         * (math.erf(td / l - gj) + math.erf(lat[0] / l + gj)))
+    return val
+
+
+def h_mpmath(D, l, j, k, t1, t2, dps=50):
+    """50-digit evaluation of model.py:315-365 (pins the fp64 restatements)."""
+    import mpmath
+
+    with mpmath.workdps(dps):
+        Dj, Dk, L = mpmath.mpf(D[j]), mpmath.mpf(D[k]), mpmath.mpf(l)
+        T1, T2 = mpmath.mpf(t1), mpmath.mpf(t2)
+        gk = Dk * L / 2
+        td = T2 - T1
+        mult = mpmath.exp(gk**2) / (Dj + Dk)
+        a = mpmath.exp(-Dk * td) * (mpmath.erf(td / L - gk) + mpmath.erf(T1 / L + gk))
+        b = mpmath.exp(-(Dk * T2 + Dj * T1)) * (mpmath.erf(T2 / L - gk) + mpmath.erf(gk))
+        return float(mult * (a - b))
+
+
+# --------------------------------------------------------------- data layout
+def dataset_3d(gene_expressions, timepoints):
+    """src/dataset.py:358-399 for expressions shaped (R, G, T): rows r*G*T + g*T + tau."""
+    R, G, T = gene_expressions.shape
+    time_points_repeated = np.tile(np.asarray(timepoints, np.float64), R * G)
+    gene_indices = np.tile(np.repeat(np.arange(G), T), R)
+    ones = np.ones(G * T * R, dtype=np.int64)
+    x = np.stack((time_points_repeated, gene_indices, ones), axis=-1).astype(np.float64)
+    y = np.asarray(gene_expressions, np.float64).reshape(-1, 1)
+    return x, y

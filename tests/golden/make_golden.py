@@ -1,0 +1,125 @@
+"""Generate the golden fixtures in tests/golden/ from the CPU oracle (oracle/lfm_oracle.py).
+
+The reference (JAX / GPJax) cannot be imported in this image and ships no fixtures
+(SURVEY.md §8c), so these vectors come from the cited numpy/scipy restatement and
+are pinned by the known-answer and mpmath tests in tests/test_oracle.py.
+
+    python tests/golden/make_golden.py          # rewrites tests/golden/*.npz
+
+Each .npz holds inputs (x, y, D, S, B, l, obs_stddev, jitter) and oracle outputs
+(K = gram, m = mean_function, mll, neg_mll; plus extra arrays per case).
+"""
+
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import lfm_oracle as O  # noqa: E402
+
+
+def grid_x(G, T, R=1, t_max=12.0):
+    t = np.linspace(0, t_max, T)
+    return np.stack((np.tile(t, G * R), np.tile(np.repeat(np.arange(G), T), R),
+                     np.ones(G * T * R)), axis=-1)
+
+
+def case(name, x, y, D, S, B, l, sd, jit, extra=None, store_K=True):
+    D, S, B = (np.asarray(v, np.float64) for v in (D, S, B))
+    K = O.gram(x, D, S, l)
+    m = O.mean_function(x, D, B, D.shape[0]).reshape(-1)
+    val = O.mll(x, y, D, S, B, l, sd, jit, negative=False)
+    neg = O.mll(x, y, D, S, B, l, sd, jit, negative=True)
+    d = dict(x=x, y=np.asarray(y, np.float64).reshape(-1), D=D, S=S, B=B, l=np.float64(l),
+             obs_stddev=np.float64(sd), jitter=np.float64(jit), m=m, mll=np.float64(val),
+             neg_mll=np.float64(neg))
+    if store_K:
+        d["K"] = K
+    if extra:
+        d.update(extra)
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **d)
+    print(f"{name:28s} n={x.shape[0]:5d} mll={val:.12g}")
+
+
+def main():
+    # C1: p53 5 genes x 7 timepoints, reference init (model.py:99-114, main.py:41)
+    rng = np.random.default_rng(1)
+    x = grid_x(5, 7)
+    y = rng.normal(0.5, 0.5, 35)
+    case("c1_p53_n35", x, y, [0.4] * 5, [1.0] * 5, [0.05] * 5, 2.5, 1.0, 1e-4)
+
+    # C5-shaped: 3 replicates x leave-one-gene-out (N = 28 each)
+    for r, seed in enumerate((10, 11, 12)):
+        rng = np.random.default_rng(seed)
+        expr = rng.normal(0.5, 0.5, (5, 7))
+        vals, negs = [], []
+        for drop in range(5):
+            keep = [g for g in range(5) if g != drop]
+            xx = grid_x(4, 7)
+            yy = expr[keep].reshape(-1)
+            vals.append(O.mll(xx, yy, [0.4] * 4, [1.0] * 4, [0.05] * 4, 2.5, 1.0, 1e-4))
+            negs.append(-vals[-1])
+        np.savez_compressed(os.path.join(HERE, f"c5_rep{r}_loo.npz"), expr=expr,
+                            mll=np.array(vals), neg_mll=np.array(negs))
+        print(f"c5_rep{r}_loo                 5 problems mll[0]={vals[0]:.12g}")
+
+    # multi-replicate layout (replicate=None): exercises the mean-block quirk (model.py:145)
+    rng = np.random.default_rng(7)
+    x = grid_x(5, 7, R=3)
+    y = rng.normal(0.5, 0.5, 105)
+    case("p53_3rep_n105", x, y, [0.28, 0.37, 0.36, 0.8, 0.36], [0.9, 0.97, 0.98, 1.0, 0.97],
+         [0.065, 0.007, 0.018, 0.003, 0.087], 2.5, 0.8, 1e-4)
+
+    # random hyperparameters, uniform grid
+    rng = np.random.default_rng(64)
+    G, T = 4, 16
+    D = rng.uniform(0.2, 1.0, G); S = rng.uniform(0.5, 1.5, G); B = rng.uniform(0.01, 0.1, G)
+    x = grid_x(G, T)
+    y = np.repeat(B / D, T) + 0.5 * rng.standard_normal(G * T)
+    case("grid_n64", x, y, D, S, B, 1.7, 0.9, 1e-4)
+
+    rng = np.random.default_rng(512)
+    G, T = 8, 64
+    D = rng.uniform(0.2, 1.0, G); S = rng.uniform(0.5, 1.5, G); B = rng.uniform(0.01, 0.1, G)
+    x = grid_x(G, T)
+    y = np.repeat(B / D, T) + 0.5 * rng.standard_normal(G * T)
+    case("grid_n512", x, y, D, S, B, 2.5, 1.0, 1e-4)
+
+    # non-uniform, unsorted times and shuffled genes: the general (direct) gram path
+    rng = np.random.default_rng(200)
+    G, n = 5, 200
+    D = rng.uniform(0.2, 1.0, G); S = rng.uniform(0.5, 1.5, G); B = rng.uniform(0.01, 0.1, G)
+    x = np.stack((rng.uniform(0, 12, n), rng.integers(0, G, n).astype(np.float64), np.ones(n)), -1)
+    y = rng.normal(0.3, 0.5, n)
+    case("scattered_n200", x, y, D, S, B, 2.1, 1.1, 1e-4)
+
+    # mixed flags: gene rows (1) and latent-force rows (0) -> kxx / kff / kxf / kfx blocks
+    rng = np.random.default_rng(33)
+    G = 3
+    D = rng.uniform(0.2, 1.0, G); S = rng.uniform(0.5, 1.5, G)
+    xa = np.stack((rng.uniform(0, 12, 40), rng.integers(0, G, 40).astype(np.float64),
+                   rng.integers(0, 2, 40).astype(np.float64)), -1)
+    xb = np.stack((rng.uniform(0, 12, 30), rng.integers(-2, G + 2, 30).astype(np.float64),
+                   rng.integers(0, 2, 30).astype(np.float64)), -1)
+    Kab = O.cross_covariance(xa, xb, D, S, 2.3)
+    np.savez_compressed(os.path.join(HERE, "mixed_flags_cross.npz"), xa=xa, xb=xb, D=D, S=S,
+                        l=np.float64(2.3), K=Kab)
+    print("mixed_flags_cross            40 x 30")
+
+    # KAT: all-zero times -> Sigma = (jitter + sd^2) I, closed-form log-density
+    G, T = 4, 8
+    x = grid_x(G, T) * np.array([0.0, 1.0, 1.0])
+    rng = np.random.default_rng(0)
+    y = rng.normal(0.0, 1.0, G * T)
+    case("kat_zero_times_n32", x, y, [0.5, 0.6, 0.7, 0.8], [1.0, 1.1, 0.9, 1.2],
+         [0.05, 0.04, 0.03, 0.02], 2.5, 0.7, 1e-4)
+
+
+if __name__ == "__main__":
+    main()

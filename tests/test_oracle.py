@@ -1,0 +1,141 @@
+"""Pins the CPU oracle (oracle/lfm_oracle.py) before anything is checked against it.
+
+The reference ships no fixtures and cannot be imported here, so the
+oracle is pinned by: its committed golden vectors (regenerated and compared), known-
+answer tests derived from the reference formulas, an independent scalar restatement,
+50-digit mpmath values of h, and a cross-read of the GPyTorch twin's h.
+"""
+
+import math
+
+import numpy as np
+import pytest
+import scipy.special
+
+from oracle import lfm_oracle as O
+from tests.conftest import load_golden
+
+GOLDEN_CASES = ["c1_p53_n35", "p53_3rep_n105", "grid_n64", "grid_n512", "scattered_n200",
+                "kat_zero_times_n32"]
+
+
+@pytest.mark.parametrize("name", GOLDEN_CASES)
+def test_oracle_reproduces_golden(name):
+    g = load_golden(name)
+    K = O.gram(g["x"], g["D"], g["S"], float(g["l"]))
+    np.testing.assert_allclose(K, g["K"], rtol=0, atol=0)
+    m = O.mean_function(g["x"], g["D"], g["B"], g["D"].shape[0]).reshape(-1)
+    np.testing.assert_array_equal(m, g["m"])
+    v = O.mll(g["x"], g["y"], g["D"], g["S"], g["B"], float(g["l"]), float(g["obs_stddev"]),
+              float(g["jitter"]))
+    assert v == float(g["mll"])
+    assert float(g["neg_mll"]) == -float(g["mll"])
+
+
+def test_c5_golden_consistent():
+    for r in range(3):
+        g = load_golden(f"c5_rep{r}_loo")
+        for drop in range(5):
+            keep = [q for q in range(5) if q != drop]
+            x = np.stack((np.tile(np.linspace(0, 12, 7), 4), np.repeat(np.arange(4), 7),
+                          np.ones(28)), -1)
+            v = O.mll(x, g["expr"][keep].reshape(-1), [0.4] * 4, [1.0] * 4, [0.05] * 4, 2.5, 1.0,
+                      1e-4)
+            assert v == g["mll"][drop]
+
+
+def test_kat_t0_rows_vanish():
+    """h with t1 = 0 or t2 = 0: both erf sums cancel exactly (erf is odd), so kxx = 0."""
+    rng = np.random.default_rng(3)
+    D = rng.uniform(0.1, 2.0, 6)
+    S = rng.uniform(0.5, 1.5, 6)
+    t = np.concatenate(([0.0], rng.uniform(0, 12, 20)))
+    x = np.stack((np.tile(t, 6), np.repeat(np.arange(6), 21), np.ones(126)), -1)
+    K = O.gram(x, D, S, 2.5)
+    zero_rows = x[:, 0] == 0
+    assert np.all(K[zero_rows] == 0.0) and np.all(K[:, zero_rows] == 0.0)
+    # scipy's erf is exactly odd, which the KAT relies on
+    z = rng.uniform(-6, 6, 100000)
+    assert np.all(scipy.special.erf(-z) == -scipy.special.erf(z))
+
+
+def test_kat_all_zero_times_closed_form():
+    g = load_golden("kat_zero_times_n32")
+    n = g["x"].shape[0]
+    c = float(g["jitter"]) + float(g["obs_stddev"]) ** 2
+    r = g["y"] - g["m"]
+    closed = -0.5 * (n * math.log(2 * math.pi) + n * math.log(c) + r @ r / c)
+    assert abs(float(g["mll"]) - closed) <= 1e-12 * abs(closed)
+    assert np.all(g["K"] == 0.0)
+
+
+def test_kat_symmetry_bitwise():
+    g = load_golden("scattered_n200")
+    K = g["K"]
+    np.testing.assert_array_equal(K, K.T)
+
+
+def test_scalar_restatement_matches_vectorised():
+    g = load_golden("mixed_flags_cross")
+    D, S, l = g["D"], g["S"], float(g["l"])
+    for i in range(0, g["xa"].shape[0], 3):
+        for j in range(0, g["xb"].shape[0], 2):
+            ref = O.kernel_scalar(g["xa"][i], g["xb"][j], D, S, l)
+            assert abs(g["K"][i, j] - ref) <= 1e-13 * max(1.0, abs(ref)), (i, j)
+
+
+def test_h_against_mpmath():
+    rng = np.random.default_rng(11)
+    D = rng.uniform(0.2, 1.0, 5)
+    for _ in range(24):
+        j, k = rng.integers(0, 5, 2)
+        t1, t2 = rng.uniform(0, 12, 2)
+        l = rng.uniform(0.5, 3.5)
+        hv = float(O.h(D, l, np.int64(j), np.int64(k), t1, t2))
+        hm = O.h_mpmath(D, l, j, k, t1, t2)
+        assert abs(hv - hm) <= 1e-12 * max(1.0, abs(hm)), (j, k, t1, t2, l, hv, hm)
+
+
+def test_h_matches_gpytorch_twin_crossread():
+    """model_alfi.py:343-378 writes h(k, j, t2, t1) with gamma(k) and the same terms."""
+    rng = np.random.default_rng(5)
+    D = rng.uniform(0.2, 1.0, 4)
+    l = 2.2
+
+    def alfi_h(k, j, t2, t1):
+        t_dist = t2 - t1
+        gk = D[k] * l / 2
+        mult = np.exp(gk**2) / (D[j] + D[k])
+        first = scipy.special.erf(t_dist / l - gk) + scipy.special.erf(t1 / l + gk)
+        second = scipy.special.erf(t2 / l - gk) + scipy.special.erf(gk)
+        return mult * (np.exp(-D[k] * t_dist) * first - np.exp(-D[k] * t2 - D[j] * t1) * second)
+
+    for _ in range(50):
+        j, k = rng.integers(0, 4, 2)
+        t1, t2 = rng.uniform(0, 12, 2)
+        a = float(O.h(D, l, np.int64(j), np.int64(k), t1, t2))
+        b = float(alfi_h(k, j, t2, t1))
+        assert abs(a - b) <= 1e-14 * max(1.0, abs(a))
+
+
+def test_mean_function_block_quirk():
+    """model.py:145-149 uses the block position i // (N // G), not x[:, 1]."""
+    x = np.stack((np.zeros(12), np.array([2, 2, 2, 2, 0, 0, 0, 0, 1, 1, 1, 1.0]), np.ones(12)), -1)
+    D = np.array([1.0, 2.0, 4.0])
+    B = np.array([1.0, 1.0, 1.0])
+    m = O.mean_function(x, D, B, 3).reshape(-1)
+    np.testing.assert_array_equal(m, np.repeat(B / D, 4))
+
+
+def test_not_pd_gives_nan():
+    x = np.stack((np.linspace(0, 12, 8), np.zeros(8), np.ones(8)), -1)
+    v = O.mll(x, np.zeros(8), [0.4], [1.0], [0.05], 2.5, obs_stddev=0.0, jitter=-10.0)
+    assert math.isnan(v)
+
+
+def test_dataset_3d_layout():
+    expr = np.arange(2 * 3 * 4, dtype=np.float64).reshape(2, 3, 4)
+    x, y = O.dataset_3d(expr, np.linspace(0, 12, 4))
+    assert x.shape == (24, 3) and y.shape == (24, 1)
+    i = 1 * 12 + 2 * 4 + 3  # r=1, g=2, tau=3
+    assert x[i, 0] == 12.0 and x[i, 1] == 2 and x[i, 2] == 1 and y[i, 0] == expr[1, 2, 3]
