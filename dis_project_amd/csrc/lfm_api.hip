@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <climits>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "lfm_internal.h"
@@ -67,9 +68,20 @@ int ensure_pinned(lfm_ctx* ctx, size_t bytes) {
 }
 
 // ----------------------------------------------------------- profiling
-void prof_begin(lfm_ctx* ctx, int cls, hipEvent_t* a) {
+int ensure_events(lfm_ctx* ctx, size_t count) {
+  while (ctx->evs.size() < count) {
+    hipEvent_t e;
+    hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (r != hipSuccess) return hip_fail(ctx, r, "hipEventCreate");
+    ctx->evs.push_back(e);
+  }
+  return LFM_OK;
+}
+
+void prof_begin(lfm_ctx* ctx, int cls, hipEvent_t* a, hipStream_t st) {
   (void)cls;
   *a = nullptr;
+  if (!st) st = ctx->stream;
   if (!ctx->prof) return;
   if (ctx->pool.empty()) {
     hipEvent_t e;
@@ -78,11 +90,12 @@ void prof_begin(lfm_ctx* ctx, int cls, hipEvent_t* a) {
   }
   *a = ctx->pool.back();
   ctx->pool.pop_back();
-  hipEventRecord(*a, ctx->stream);
+  hipEventRecord(*a, st);
 }
 
-void prof_end(lfm_ctx* ctx, int cls, hipEvent_t a, double flops, double bytes) {
+void prof_end(lfm_ctx* ctx, int cls, hipEvent_t a, double flops, double bytes, hipStream_t st) {
   if (!ctx->prof || !a) return;
+  if (!st) st = ctx->stream;
   if (ctx->pool.empty()) {
     hipEvent_t e;
     hipEventCreate(&e);
@@ -90,7 +103,7 @@ void prof_end(lfm_ctx* ctx, int cls, hipEvent_t a, double flops, double bytes) {
   }
   hipEvent_t b = ctx->pool.back();
   ctx->pool.pop_back();
-  hipEventRecord(b, ctx->stream);
+  hipEventRecord(b, st);
   ctx->pending.push_back(ProfEvent{cls, a, b, flops, bytes});
 }
 
@@ -402,6 +415,33 @@ static int gram_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* h
   return finish(ctx);
 }
 
+namespace {
+// Main + side streams. LFM_SIDE_CUS=c (> 0) reserves c CUs for the side stream and keeps
+// the main stream off them (hipExtStreamCreateWithCUMask); 0 (default) shares every CU and
+// relies on the side stream's higher priority. LFM_LOOKAHEAD=0 serialises on one stream.
+hipError_t create_streams(lfm_ctx* ctx) {
+  const char* la = std::getenv("LFM_LOOKAHEAD");
+  ctx->lookahead = !(la && std::atoi(la) == 0);
+  int least = 0, greatest = 0;
+  hipDeviceGetStreamPriorityRange(&least, &greatest);
+  const char* sc = std::getenv("LFM_SIDE_CUS");
+  const int side_cus = sc ? std::atoi(sc) : 0;
+  hipDeviceProp_t prop;
+  hipGetDeviceProperties(&prop, ctx->device);
+  const int ncu = prop.multiProcessorCount;
+  if (side_cus > 0 && side_cus < ncu) {
+    std::vector<uint32_t> mside((ncu + 31) / 32, 0u), mmain((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; ++c) (c < side_cus ? mside : mmain)[c / 32] |= 1u << (c % 32);
+    hipError_t e = hipExtStreamCreateWithCUMask(&ctx->stream, (uint32_t)mmain.size(), mmain.data());
+    if (e != hipSuccess) return e;
+    return hipExtStreamCreateWithCUMask(&ctx->side, (uint32_t)mside.size(), mside.data());
+  }
+  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest);
+}
+}  // namespace
+
 // =================================================================== C ABI
 extern "C" {
 
@@ -428,7 +468,7 @@ int lfm_ctx_create(int device, lfm_ctx** out) {
   for (int i = 0; i < K_NCLASS; ++i)
     std::snprintf(ctx->stats[i].name, sizeof(ctx->stats[i].name), "%s", kClassName[i]);
   hipSetDevice(device);
-  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  hipError_t e = create_streams(ctx);
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->linvT, 128 * 128 * sizeof(double));
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->status, 64);
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->result, 64 * sizeof(double));
@@ -455,6 +495,11 @@ void lfm_ctx_destroy(lfm_ctx* ctx) {
     hipEventDestroy(p.b);
   }
   for (auto e : ctx->pool) hipEventDestroy(e);
+  for (auto e : ctx->evs) hipEventDestroy(e);
+  if (ctx->side) {
+    hipStreamSynchronize(ctx->side);
+    hipStreamDestroy(ctx->side);
+  }
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -850,6 +895,38 @@ int lfm_probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, dou
   if (!ctx || !tflops || !ms || nblocks < 1 || iters < 1) return LFM_E_ARG;
   DeviceGuard g(ctx->device);
   return probe_mfma_f64(ctx, nblocks, iters, tflops, ms);
+}
+
+int lfm_probe_mfma_f64_cycles(lfm_ctx* ctx, int nblocks, int iters, double* cyc_per_mfma,
+                              double* mhz) {
+  if (!ctx || !cyc_per_mfma || !mhz || nblocks < 1 || iters < 1) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_mfma_f64_cycles(ctx, nblocks, iters, cyc_per_mfma, mhz);
+}
+
+int lfm_probe_mfma4_layout(lfm_ctx* ctx, const double* a, const double* b, const double* c,
+                           double* d) {
+  if (!ctx || !a || !b || !c || !d) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_mfma4_layout(ctx, a, b, c, d);
+}
+
+int lfm_probe_rate(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflops) {
+  if (!ctx || !tflops || nblocks < 1 || iters < 1) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_rates(ctx, which, nblocks, iters, tflops);
+}
+
+int lfm_probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
+  if (!ctx || !us || T < 1 || reps < 1 || (kd != 128 && kd != 256)) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_syrk(ctx, T, kd, cio, reps, us);
+}
+
+int lfm_probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us) {
+  if (!ctx || !us || reps < 1) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_potrf(ctx, mask, reps, us);
 }
 
 int lfm_probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d) {

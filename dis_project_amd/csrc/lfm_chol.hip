@@ -11,12 +11,21 @@
 // row n: no separate triangular solve pass (quad = ||z||^2). Rows > n are identity.
 //
 // Per block column k (NB = 128):
-//   potrf_diag_kernel  one workgroup: L_kk (in LDS) + L_kk^{-1} (transposed, to linvT),
-//                      pivot check, logdet partial. Columns >= n take a unit pivot.
-//   trsm_kernel        rows below the block: X = A_ik * L_kk^{-T} as a GEMM on
-//                      v_mfma_f64_16x16x4_f64 against linvT.
-//   syrk_kernel        trailing lower triangle, 128x128 tiles: C -= P P^T on
-//                      v_mfma_f64_16x16x4_f64 (the only dense-flop kernel).
+//   potrf_diag_kernel  one workgroup factors the 128x128 diagonal block in LDS, 16 columns
+//                      at a time: the 16x16 diagonal sub-block is factored and inverted
+//                      in registers by every wave (cross-lane v_readlane broadcasts), the
+//                      rows below are solved against that inverse, and the rank-16 update
+//                      of the rest runs on v_mfma_f64_16x16x4_f64. It also writes the eight
+//                      16x16 diagonal inverses (dinv) for the panel solve, the logdet
+//                      partial and the first failing pivot. Columns >= n take a unit pivot.
+//   trsm_kernel        rows below the block: X = A_ik L_kk^{-T} by blocked substitution,
+//                      16 columns at a time, on fp64 MFMA (L_kk from L2, dinv blocks).
+//   syrk_kernel        trailing lower triangle, 128x128 tiles: C -= P P^T on fp64 MFMA —
+//                      the only O(n^3) kernel.
+// Look-ahead: the SYRK of block column k is split into the next block column (k+1) and
+// the rest. A high-priority side stream runs syrk(next) -> potrf(k+1) -> trsm(k+1) while
+// the main stream runs syrk(rest) of step k, so the latency-bound panel work of step k+1
+// hides behind the bulk of step k's trailing update.
 // finalize_kernel reduces logdet + ||z||^2 to the scalar MLL.
 #include <climits>
 
@@ -27,6 +36,7 @@ namespace lfm {
 typedef double double4v __attribute__((ext_vector_type(4)));
 
 static constexpr int NB = 128;       // panel width (block column)
+static constexpr int IB = 16;        // inner block of the diagonal factor / panel solve
 static constexpr int ST = 128;       // SYRK output tile edge
 static constexpr int KB = 16;        // SYRK K-step staged through LDS
 static constexpr int STATUS_NONE = INT_MAX;
@@ -35,120 +45,155 @@ __device__ __forceinline__ double4v mfma16(double a, double b, double4v c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// ---------------------------------------------------------------- potrf
-// One 1024-thread workgroup factors the NB x NB diagonal block held in LDS.
-// Right-looking, one barrier per column: in phase c every thread updates its
-// trailing elements with the (unscaled) column c and scales column c-1, which no
-// one reads in phase c.
-__global__ __launch_bounds__(1024) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
-                                                         int64_t kb, int64_t npiv,
-                                                         double* __restrict__ linvT,
-                                                         double* __restrict__ parts, int k,
-                                                         int* __restrict__ status) {
-  __shared__ double M[NB][NB + 1];
-  __shared__ double xd[NB];  // unscaled pivots during the factorisation, then diag(L^{-1})
-  const int tid = threadIdx.x;
+// Value of v held by `lane` (compile-time lane after unrolling), broadcast to the wave.
+__device__ __forceinline__ double rdl(double v, int lane) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffu), lane);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
 
-  for (int idx = tid; idx < NB * NB; idx += 1024) {
+// Orders one wave's LDS writes before its following LDS reads (and vice versa): LDS
+// operations of a wave complete in order; the asm keeps the compiler from reordering.
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// ---------------------------------------------------------------- potrf
+// One 256-thread workgroup, the 128x128 diagonal block in LDS, 16 columns per step:
+//  (1) wave 0 factors the 16x16 diagonal sub-block and inverts it in registers
+//      (lane = row for L, lane = column for X = L^{-1}; cross-lane values by v_readlane);
+//  (2) the rows below: P <- P X^T on fp64 MFMA, one 16-row block per wave;
+//  (3) the rank-16 update of the trailing lower triangle on fp64 MFMA.
+// Pivots are kept; logdet and the first failing pivot are reduced once at the end.
+// PH (diagnostics only, lfm_probe_potrf): bit 0 = phase 1, bit 1 = phase 2, bit 2 = phase 3,
+// bit 3 = global load / store of the block. The product path always runs PH = 15.
+template <int PH>
+__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
+                                                        int64_t kb, int64_t npiv,
+                                                        double* __restrict__ dinv,
+                                                        double* __restrict__ parts, int k,
+                                                        int* __restrict__ status) {
+  __shared__ double M[NB][NB + 1];
+  __shared__ double Xs[IB][IB + 1];
+  __shared__ double pvs[NB];
+  __shared__ double red[4];
+  __shared__ int redi[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+
+  for (int idx = tid; idx < NB * NB; idx += 256) {
     const int r = idx / NB, q = idx - r * NB;
-    M[r][q] = (q <= r) ? A[(kb + r) * lda + kb + q] : 0.0;
-  }
-  // this thread's lower-triangle elements (row-major enumeration of q <= r)
-  constexpr int NEL = NB * (NB + 1) / 2;
-  constexpr int SLOTS = (NEL + 1023) / 1024;
-  int er[SLOTS], eq[SLOTS];
-#pragma unroll
-  for (int s = 0; s < SLOTS; ++s) {
-    const int e = tid + 1024 * s;
-    if (e < NEL) {
-      int r = (int)((sqrt(8.0 * e + 1.0) - 1.0) * 0.5);
-      while ((r + 1) * (r + 2) / 2 <= e) ++r;
-      while (r * (r + 1) / 2 > e) --r;
-      er[s] = r;
-      eq[s] = e - r * (r + 1) / 2;
-    } else {
-      er[s] = -1;
-      eq[s] = NB;  // never active
-    }
+    if (PH & 8) M[r][q] = (q <= r) ? A[(kb + r) * lda + kb + q] : 0.0;
+    else M[r][q] = (q == r) ? 2.0 : 0.0;
   }
   __syncthreads();
 
-  double logacc = 0.0;  // thread 0 only
-  for (int c = 0; c <= NB; ++c) {
-    // scale column c-1 (finished in phase c-1)
-    if (c > 0) {
-      const int cp = c - 1;
-      const double dp = xd[cp];
-      const double piv = sqrt(dp);
-      const double inv = 1.0 / piv;
-      for (int r = cp + 1 + tid; r < NB; r += 1024) M[r][cp] *= inv;
-      if (tid == 0) {
-        M[cp][cp] = piv;
-        if (kb + cp < npiv) {
-          if (!(dp > 0.0)) atomicMin(status, (int)(kb + cp));
-          logacc += 0.5 * log(dp);
-        }
-      }
-    }
-    if (c < NB) {
-      const double d = (kb + c >= npiv) ? 1.0 : M[c][c];
-      if (tid == 0) xd[c] = d;  // read by everyone in phase c+1 only
-      const double invd = 1.0 / d;
+  for (int ib = 0; ib < NB / IB; ++ib) {
+    const int c0 = ib * IB;
+    if ((PH & 1) && w == 0) {
+      // (1) rows of the sub-block on lanes 0..15 (upper part of each row is scratch)
+      double d[IB], ip[IB], x[IB];
 #pragma unroll
-      for (int s = 0; s < SLOTS; ++s) {
-        const int r = er[s], q = eq[s];
-        if (q > c) M[r][q] -= M[r][c] * M[q][c] * invd;
+      for (int q = 0; q < IB; ++q) d[q] = (lane < IB && q <= lane) ? M[c0 + lane][c0 + q] : 0.0;
+#pragma unroll
+      for (int c = 0; c < IB; ++c) {
+        double dc = rdl(d[c], c);
+        if (kb + c0 + c >= npiv) dc = 1.0;
+        if (lane == 0) pvs[c0 + c] = dc;
+        const double piv = sqrt(dc);
+        ip[c] = 1.0 / piv;
+        d[c] = (lane == c) ? piv : d[c] * ip[c];
+#pragma unroll
+        for (int q = c + 1; q < IB; ++q) d[q] = fma(-d[c], rdl(d[c], q), d[q]);
+      }
+      // lane c: column c of X = L^{-1} (entries above the diagonal come out exactly 0)
+#pragma unroll
+      for (int r = 0; r < IB; ++r) {
+        double sacc = (lane == r) ? 1.0 : 0.0;
+#pragma unroll
+        for (int q = 0; q < r; ++q) sacc = fma(-rdl(d[q], r), x[q], sacc);
+        x[r] = sacc * ip[r];
+      }
+      if (lane < IB) {
+#pragma unroll
+        for (int q = 0; q < IB; ++q) {
+          if (q <= lane) M[c0 + lane][c0 + q] = d[q];
+          Xs[q][lane] = x[q];
+          dinv[(ib * IB + q) * IB + lane] = x[q];
+        }
       }
     }
     __syncthreads();
-  }
-  // write L (lower triangle incl. diagonal) back
-  for (int idx = tid; idx < NB * NB; idx += 1024) {
-    const int r = idx / NB, q = idx - r * NB;
-    if (q <= r) A[(kb + r) * lda + kb + q] = M[r][q];
-  }
-  if (tid == 0) parts[k] = logacc;
-
-  // X = L^{-1}: X^T is kept in the (zero) upper triangle of M, diag(X) in xd.
-  if (tid < NB) xd[tid] = 1.0 / M[tid][tid];
-  // clear the upper triangle (it held zeros already; keep explicit for clarity)
-  __syncthreads();
-  // row-by-row: X[i][j] = -(sum_{q=j}^{i-1} L[i][q] X[q][j]) / L[i][i], 8 lanes per j
-  {
-    const int j = tid >> 3, p = tid & 7;
-    for (int i = 1; i < NB; ++i) {
-      double sum = 0.0;
-      if (j < i) {
-        for (int q = j + p; q < i; q += 8) {
-          const double xqj = (q == j) ? xd[j] : M[j][q];
-          sum += M[i][q] * xqj;
-        }
-      }
-      sum += __shfl_xor(sum, 1);
-      sum += __shfl_xor(sum, 2);
-      sum += __shfl_xor(sum, 4);
-      if (j < i && p == 0) M[j][i] = -sum * xd[i];
-      __syncthreads();
+    // (2) P <- P X^T for the 16-row blocks below:  B[k][j] = X[j][k]
+    const int nrb = (NB - c0 - IB) / IB;
+    for (int rb = w; (PH & 2) && rb < nrb; rb += 4) {
+      const int r0 = c0 + IB + rb * IB;
+      double4v acc = {0, 0, 0, 0};
+#pragma unroll
+      for (int ks = 0; ks < IB / 4; ++ks)
+        acc = mfma16(M[r0 + li][c0 + ks * 4 + lk], Xs[li][ks * 4 + lk], acc);
+      wave_lds_fence();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) M[r0 + lk + 4 * r][c0 + li] = acc[r];
     }
+    __syncthreads();
+    // (3) rank-16 update of the trailing lower triangle, one 16x16 tile per wave at a time
+    const int ntiles = (PH & 4) ? nrb * (nrb + 1) / 2 : 0;
+    for (int t = w; t < ntiles; t += 4) {
+      int ti = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
+      while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+      while (ti * (ti + 1) / 2 > t) --ti;
+      const int tj = t - ti * (ti + 1) / 2;
+      const int i0 = c0 + IB + ti * IB, j0 = c0 + IB + tj * IB;
+      double4v acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = M[i0 + lk + 4 * r][j0 + li];
+#pragma unroll
+      for (int ks = 0; ks < IB / 4; ++ks)
+        acc = mfma16(-M[i0 + li][c0 + ks * 4 + lk], M[j0 + li][c0 + ks * 4 + lk], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) M[i0 + lk + 4 * r][j0 + li] = acc[r];
+    }
+    __syncthreads();
   }
-  // linvT[q][c] = X[c][q]: upper triangular, row-major NB x NB
-  for (int idx = tid; idx < NB * NB; idx += 1024) {
-    const int q = idx / NB, c = idx - q * NB;
-    double v = 0.0;
-    if (q < c) v = M[q][c];
-    else if (q == c) v = xd[c];
-    linvT[idx] = v;
+  for (int idx = tid; idx < NB * NB; idx += 256) {
+    const int r = idx / NB, q = idx - r * NB;
+    if ((PH & 8) && q <= r) A[(kb + r) * lda + kb + q] = M[r][q];
+  }
+  // logdet partial = 1/2 sum log(pivot) over real pivots; first non-positive pivot
+  double lg = 0.0;
+  int bad = STATUS_NONE;
+  if (tid < NB && kb + tid < npiv) {
+    const double dp = pvs[tid];
+    lg = 0.5 * log(dp);
+    if (!(dp > 0.0)) bad = (int)(kb + tid);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lg += __shfl_xor(lg, o);
+    bad = min(bad, __shfl_xor(bad, o));
+  }
+  if (lane == 0) {
+    red[w] = lg;
+    redi[w] = bad;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    parts[k] = red[0] + red[1] + red[2] + red[3];
+    const int b = min(min(redi[0], redi[1]), min(redi[2], redi[3]));
+    if (b != STATUS_NONE) atomicMin(status, b);
   }
 }
 
 // ----------------------------------------------------------------- trsm
-// Rows [s, Mp) of block column kb: X = A * L^{-T} = A * linvT (linvT upper triangular).
-// 64 rows per 256-thread workgroup; wave w owns 16-column blocks w and 7-w (balanced
-// because column block cb needs (cb+1)*4 MFMA k-steps).
+// Rows [s, Mp) of block column kb, 64 rows per workgroup, 16 rows per wave:
+//   X_cb = (A_cb - sum_{q < cb} X_q L_{cb,q}^T) * Dinv_cb^T,  cb = 0..7 (16 columns each).
+// The wave's rows live in LDS; the L_{cb,q} fragments (the factored diagonal block, shared
+// by every workgroup, L2-resident) for column block cb+1 are loaded while cb computes,
+// and the K chain is split over two accumulators.
 __global__ __launch_bounds__(256) void trsm_kernel(double* __restrict__ A, int64_t lda, int64_t s,
-                                                   int64_t kb, const double* __restrict__ linvT) {
+                                                   int64_t kb, const double* __restrict__ dinv) {
   __shared__ double sA[64][NB + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lk = lane >> 4;
   const int64_t r0 = s + (int64_t)blockIdx.x * 64;
   for (int idx = tid; idx < 64 * (NB / 2); idx += 256) {
     const int r = idx / (NB / 2), q2 = idx - r * (NB / 2);
@@ -156,119 +201,169 @@ __global__ __launch_bounds__(256) void trsm_kernel(double* __restrict__ A, int64
     sA[r][2 * q2] = v.x;
     sA[r][2 * q2 + 1] = v.y;
   }
+  const int wr = w * IB;
+  const double* Lrow = A + (kb + li) * lda + kb + lk;  // L[li][lk]
+  constexpr int NCB = NB / IB;
+  double bf[2][NB / 4];
+  double dv[2][IB / 4];
+#pragma unroll
+  for (int ks = 0; ks < IB / 4; ++ks) dv[0][ks] = dinv[li * IB + ks * 4 + lk];
   __syncthreads();
-  const int li = lane & 15, lk = lane >> 4;
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    const int cb = half == 0 ? w : (NB / 16 - 1 - w);
-    double4v acc[4];
+  for (int cb = 0; cb < NCB; ++cb) {
+    const int cur = cb & 1, nxt = cur ^ 1;
+    if (cb + 1 < NCB) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m) acc[m] = (double4v){0, 0, 0, 0};
-    const int qend = (cb + 1) * 16;
-    for (int q0 = 0; q0 < qend; q0 += 4) {
-      const double b = linvT[(q0 + lk) * NB + cb * 16 + li];
+      for (int st = 0; st < (cb + 1) * 4; ++st)
+        bf[nxt][st] = Lrow[(int64_t)(cb + 1) * IB * lda + st * 4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) acc[m] = mfma16(sA[m * 16 + li][q0 + lk], b, acc[m]);
+      for (int ks = 0; ks < IB / 4; ++ks)
+        dv[nxt][ks] = dinv[(cb + 1) * IB * IB + li * IB + ks * 4 + lk];
     }
+    double4v acc0, acc1 = {0, 0, 0, 0};
 #pragma unroll
-    for (int m = 0; m < 4; ++m)
+    for (int r = 0; r < 4; ++r) acc0[r] = sA[wr + lk + 4 * r][cb * IB + li];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m * 16 + lk + 4 * r;
-        A[(r0 + row) * lda + kb + cb * 16 + li] = acc[m][r];
-      }
+    for (int st = 0; st < cb * 4; ++st) {
+      if (st & 1) acc1 = mfma16(-sA[wr + li][st * 4 + lk], bf[cur][st], acc1);
+      else acc0 = mfma16(-sA[wr + li][st * 4 + lk], bf[cur][st], acc0);
+    }
+    acc0 += acc1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sA[wr + lk + 4 * r][cb * IB + li] = acc0[r];
+    wave_lds_fence();
+    double4v z = {0, 0, 0, 0};
+#pragma unroll
+    for (int ks = 0; ks < IB / 4; ++ks) z = mfma16(sA[wr + li][cb * IB + ks * 4 + lk], dv[cur][ks], z);
+    wave_lds_fence();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sA[wr + lk + 4 * r][cb * IB + li] = z[r];
+    wave_lds_fence();
+  }
+  // the wave's 16 rows back to HBM
+  for (int idx = lane; idx < IB * (NB / 2); idx += 64) {
+    const int r = idx / (NB / 2), q2 = idx - r * (NB / 2);
+    double2 v;
+    v.x = sA[wr + r][2 * q2];
+    v.y = sA[wr + r][2 * q2 + 1];
+    *reinterpret_cast<double2*>(&A[(r0 + wr + r) * lda + kb + 2 * q2]) = v;
   }
 }
 
 // ----------------------------------------------------------------- syrk
 // Trailing update of the lower triangle: for 128x128 tiles (ti >= tj) of rows/cols
 // starting at s:  C[i][j] -= sum_q P[i][q] P[j][q],  P = A[:, kb:kb+NB].
-// 4 waves as 2x2, each 64x64 = 4x4 MFMA tiles of 16x16 accumulated in registers.
+// 4 waves as 2x2, each a 64x64 block of C held in registers. The product runs on
+// v_mfma_f64_4x4x4_4b_f64 (72.7 TFLOP/s measured on MI355X, against 49 for
+// v_mfma_f64_16x16x4_f64; scripts/probe_mfma.py). Lane maps (scripts/probe_mfma4_layout.py),
+// with g = (lane >> 2) & 3 the block: A_g[i][k] at lane 16k + 4g + i, B_g[k][j] at lane
+// 16k + 4g + j, D_g[i][j] at lane 16i + 4g + j. A is replicated over the four blocks
+// (rows ir*4 + i) and each block owns 4 of 16 columns (jr*16 + 4g + j), so accumulator
+// acc[ir][jr] holds C[ir*4 + (lane >> 4)][jr*16 + (lane & 15)]: 16 consecutive columns per
+// 16 lanes, as the 16x16 layout. Per K step of 4: 16 A + 4 B fragments, 64 MFMAs.
 // The K dimension (NB) is staged KB columns at a time through LDS, the next stage
 // prefetched into registers while the current one feeds the MFMAs.
+__device__ __forceinline__ double mfma4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+// mode 0: every lower tile; 1: only tile column 0 (the next block column, look-ahead);
+// 2: every lower tile with tile column >= 1 (the rest).
+// KD: depth of the update (columns kb .. kb+KD of A). CIO = false (diagnostics only) skips
+// the C tile's HBM read and write.
+template <int KD, bool CIO>
 __global__ __launch_bounds__(256, 2) void syrk_kernel(double* __restrict__ A, int64_t lda,
-                                                      int64_t s, int64_t kb) {
+                                                      int64_t s, int64_t kb, int mode) {
   __shared__ double sP[2][ST][KB + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wr = w >> 1, wc = w & 1;
-  const int li = lane & 15, lk = lane >> 4;
+  const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
+  const int li = lane & 15, lk = lane >> 4, l3 = lane & 3;
 
   const int64_t b = blockIdx.x;
-  int ti = (int)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
-  while ((int64_t)(ti + 1) * (ti + 2) / 2 <= b) ++ti;
-  while ((int64_t)ti * (ti + 1) / 2 > b) --ti;
-  const int tj = (int)(b - (int64_t)ti * (ti + 1) / 2);
+  int ti, tj;
+  if (mode == 1) {
+    ti = (int)b;
+    tj = 0;
+  } else {
+    ti = (int)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
+    while ((int64_t)(ti + 1) * (ti + 2) / 2 <= b) ++ti;
+    while ((int64_t)ti * (ti + 1) / 2 > b) --ti;
+    tj = (int)(b - (int64_t)ti * (ti + 1) / 2);
+    if (mode == 2) {
+      ++ti;
+      ++tj;
+    }
+  }
   const int64_t i0 = s + (int64_t)ti * ST, j0 = s + (int64_t)tj * ST;
   const bool diag = (ti == tj);
+  double* Cb = A + (i0 + wr + lk) * lda + j0 + wc + li;  // C[wr + lk][wc + li]
+  const int ld4 = (int)(4 * lda);  // row-group stride (elements); 60 * ld4 < 2^31 for lda < 2^23
 
-  double4v acc[4][4];
+  double acc[16][4];
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
+  for (int ir = 0; ir < 16; ++ir)
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = i0 + wr * 64 + m * 16 + lk + 4 * r;
-        const int64_t col = j0 + wc * 64 + n * 16 + li;
-        acc[m][n][r] = A[row * lda + col];
-      }
+    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = CIO ? Cb[ir * ld4 + jr * 16] : 0.0;
 
-  // staging map: 2 panels x 128 rows x KB doubles = 8 double2 per thread
-  constexpr int CH = KB / 2;  // double2 chunks per row
+  // staging map: 2 panels x 128 rows x KB doubles = 8 double2 per thread; thread tid moves
+  // chunk (tid & 7) of rows (tid >> 3) + 32u of each panel
+  static_assert(KB == 16, "staging map assumes 8 double2 chunks per row");
+  const int srow = tid >> 3, sch = tid & 7;
+  const double* gi = A + (i0 + srow) * lda + kb + 2 * sch;
+  const double* gj = A + (j0 + srow) * lda + kb + 2 * sch;
+  const int ld32 = (int)(32 * lda);
   double2 pre[8];
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int idx = tid + 256 * u;  // 0..2047
-      const int p = idx >> 10;        // panel
-      const int rem = idx & 1023;
-      const int row = rem / CH, ch = rem - row * CH;
-      const int64_t grow = (p ? j0 : i0) + row;
-      pre[u] = *reinterpret_cast<const double2*>(&A[grow * lda + kb + k0 + 2 * ch]);
+    for (int u = 0; u < 4; ++u) {
+      pre[u] = *reinterpret_cast<const double2*>(gi + u * ld32 + k0);
+      pre[4 + u] = *reinterpret_cast<const double2*>(gj + u * ld32 + k0);
     }
   };
   auto lstore = [&]() {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const int idx = tid + 256 * u;
-      const int p = idx >> 10;
-      const int rem = idx & 1023;
-      const int row = rem / CH, ch = rem - row * CH;
-      sP[p][row][2 * ch] = pre[u].x;
-      sP[p][row][2 * ch + 1] = pre[u].y;
+      double* d = &sP[u >> 2][srow + 32 * (u & 3)][2 * sch];
+      d[0] = pre[u].x;
+      d[1] = pre[u].y;
     }
   };
 
   gload(0);
-  for (int k0 = 0; k0 < NB; k0 += KB) {
+  for (int k0 = 0; k0 < KD; k0 += KB) {
     __syncthreads();
     lstore();
     __syncthreads();
-    if (k0 + KB < NB) gload(k0 + KB);
-#pragma unroll
+    if (k0 + KB < KD) gload(k0 + KB);
+#pragma unroll 1
     for (int kk = 0; kk < KB; kk += 4) {
-      double a[4], bb[4];
+      double bb[4];
 #pragma unroll
-      for (int m = 0; m < 4; ++m) a[m] = -sP[0][wr * 64 + m * 16 + li][kk + lk];
+      for (int jr = 0; jr < 4; ++jr) bb[jr] = sP[1][wc + jr * 16 + li][kk + lk];
 #pragma unroll
-      for (int n = 0; n < 4; ++n) bb[n] = sP[1][wc * 64 + n * 16 + li][kk + lk];
+      for (int h = 0; h < 2; ++h) {
+        double a[8];
 #pragma unroll
-      for (int m = 0; m < 4; ++m)
+        for (int ir = 0; ir < 8; ++ir) a[ir] = -sP[0][wr + (h * 8 + ir) * 4 + l3][kk + lk];
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[m][n] = mfma16(a[m], bb[n], acc[m][n]);
+        for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+          for (int jr = 0; jr < 4; ++jr)
+            acc[h * 8 + ir][jr] = mfma4(a[ir], bb[jr], acc[h * 8 + ir][jr]);
+      }
     }
   }
 
+  int ld4s = ld4;
+  asm volatile("" : "+v"(ld4s));  // recompute store addresses instead of keeping 64 pointers live
 #pragma unroll
-  for (int m = 0; m < 4; ++m)
+  for (int ir = 0; ir < 16; ++ir)
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = i0 + wr * 64 + m * 16 + lk + 4 * r;
-        const int64_t col = j0 + wc * 64 + n * 16 + li;
-        if (!diag || col <= row) A[row * lda + col] = acc[m][n][r];
-      }
+    for (int jr = 0; jr < 4; ++jr) {
+      const int row = wr + ir * 4 + lk, col = wc + jr * 16 + li;
+      if (CIO && (!diag || col <= row)) Cb[ir * ld4s + jr * 16] = acc[ir][jr];
+      if (!CIO && acc[ir][jr] == 1.2345e300) Cb[0] = 0.0;  // keep the MFMAs live
+    }
 }
 
 // ------------------------------------------------------------- finalize
@@ -313,45 +408,158 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* __restrict
 
 __global__ void status_init_kernel(int* st) { st[0] = STATUS_NONE; }
 
+
+namespace {
+struct Launcher {
+  lfm_ctx* ctx;
+  double* A;
+  int64_t lda;
+  void potrf(hipStream_t st, int64_t k, int64_t n) {
+    hipEvent_t ev;
+    prof_begin(ctx, K_POTRF, &ev, st);
+    hipLaunchKernelGGL(potrf_diag_kernel<15>, dim3(1), dim3(256), 0, st, A, lda, k * NB, n,
+                       ctx->linvT, ctx->parts, (int)k, ctx->status);
+    prof_end(ctx, K_POTRF, ev, (double)NB * NB * NB / 3.0, 0, st);
+  }
+  void trsm(hipStream_t st, int64_t k, int64_t Mp) {
+    const int64_t s = (k + 1) * NB;
+    if (s >= Mp) return;
+    const int64_t rows = Mp - s;
+    hipEvent_t ev;
+    prof_begin(ctx, K_TRSM, &ev, st);
+    hipLaunchKernelGGL(trsm_kernel, dim3((unsigned)(rows / 64)), dim3(256), 0, st, A, lda, s,
+                       k * NB, ctx->linvT);
+    prof_end(ctx, K_TRSM, ev, (double)rows * NB * NB, 2.0 * rows * NB * 8, st);
+  }
+  // mode 0: all lower tiles of the trailing matrix after block column k; 1: next column; 2: rest
+  void syrk(hipStream_t st, int64_t k, int64_t Mp, int mode) {
+    const int64_t s = (k + 1) * NB;
+    const int64_t T = (Mp - s) / ST;
+    int64_t tiles = mode == 1 ? T : (mode == 2 ? (T - 1) * T / 2 : T * (T + 1) / 2);
+    if (tiles <= 0) return;
+    // algorithmic work of the updated lower elements (diagonal tiles count their lower half)
+    double elems;
+    const double t = (double)ST;
+    if (mode == 1) elems = (double)(T - 1) * t * t + t * (t + 1) / 2;
+    else if (mode == 2) elems = (double)(T - 1) * (T - 2) / 2 * t * t + (double)(T - 1) * t * (t + 1) / 2;
+    else elems = (double)(Mp - s) * (double)(Mp - s + 1) / 2;
+    hipEvent_t ev;
+    prof_begin(ctx, K_SYRK, &ev, st);
+    hipLaunchKernelGGL((syrk_kernel<NB, true>), dim3((unsigned)tiles), dim3(256), 0, st, A, lda, s,
+                       k * NB, mode);
+    prof_end(ctx, K_SYRK, ev, elems * 2.0 * NB, elems * 16.0, st);
+  }
+};
+}  // namespace
+
+// Diagnostic: average duration (us) of the diagonal-block kernel with phase mask `mask`
+// over `reps` launches on a 128 x 128 block of ctx->A (must hold >= 128*128 doubles).
+int probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us) {
+  int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)NB * NB * 8);
+  if (r) return r;
+  r = ensure(ctx, (void**)&ctx->parts, &ctx->parts_cap, 64);
+  if (r) return r;
+  hipStream_t st = ctx->stream;
+  auto launch = [&](int m) {
+    switch (m & 15) {
+#define LFM_PH(v) case v: hipLaunchKernelGGL(potrf_diag_kernel<v>, dim3(1), dim3(256), 0, st, \
+                                              ctx->A, (int64_t)NB, (int64_t)0, (int64_t)NB, ctx->linvT, ctx->parts, 0, ctx->status); break;
+      LFM_PH(0) LFM_PH(1) LFM_PH(2) LFM_PH(3) LFM_PH(4) LFM_PH(5) LFM_PH(6) LFM_PH(7)
+      LFM_PH(8) LFM_PH(9) LFM_PH(10) LFM_PH(11) LFM_PH(12) LFM_PH(13) LFM_PH(14) LFM_PH(15)
+#undef LFM_PH
+    }
+  };
+  launch(mask);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a, st);
+  for (int i = 0; i < reps; ++i) launch(mask);
+  hipEventRecord(b, st);
+  hipError_t e = hipStreamSynchronize(st);
+  float ms = 0;
+  hipEventElapsedTime(&ms, a, b);
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  *us = ms * 1e3 / reps;
+  return hip_fail(ctx, e, "probe_potrf");
+}
+
+// Diagnostic: average duration (us) of one full-lower-triangle SYRK launch over a T x T grid
+// of 128-tiles with update depth kd (128 or 256); cio = 0 skips the C tile I/O.
+int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
+  const int64_t n = (int64_t)T * ST + 256;
+  int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
+  if (r) return r;
+  hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8, ctx->stream);
+  const unsigned tiles = (unsigned)((int64_t)T * (T + 1) / 2);
+  hipStream_t st = ctx->stream;
+  auto go = [&]() {
+    if (kd == 256 && cio) hipLaunchKernelGGL((syrk_kernel<256, true>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
+    else if (kd == 256) hipLaunchKernelGGL((syrk_kernel<256, false>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
+    else if (cio) hipLaunchKernelGGL((syrk_kernel<128, true>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
+    else hipLaunchKernelGGL((syrk_kernel<128, false>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
+  };
+  go();
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a, st);
+  for (int i = 0; i < reps; ++i) go();
+  hipEventRecord(b, st);
+  hipError_t e = hipStreamSynchronize(st);
+  float ms = 0;
+  hipEventElapsedTime(&ms, a, b);
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  *us = ms * 1e3 / reps;
+  return hip_fail(ctx, e, "probe_syrk");
+}
+
 int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,
                       double* d_out) {
   const int64_t npb = (n + NB - 1) / NB;  // block columns that hold pivots
   int r = ensure(ctx, (void**)&ctx->parts, &ctx->parts_cap, (size_t)npb * sizeof(double));
   if (r) return r;
-  hipStream_t st = ctx->stream;
-  hipLaunchKernelGGL(status_init_kernel, dim3(1), dim3(1), 0, st, ctx->status);
-  for (int64_t k = 0; k < npb; ++k) {
-    const int64_t kb = k * NB;
-    hipEvent_t ev;
-    prof_begin(ctx, K_POTRF, &ev);
-    hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(1024), 0, st, A, lda, kb, n, ctx->linvT,
-                       ctx->parts, (int)k, ctx->status);
-    prof_end(ctx, K_POTRF, ev, (double)NB * NB * NB / 3.0 + (double)NB * NB * NB / 3.0, 0);
-    const int64_t s = kb + NB;
-    if (s < Mp) {
-      const int64_t rows = Mp - s;
-      prof_begin(ctx, K_TRSM, &ev);
-      hipLaunchKernelGGL(trsm_kernel, dim3((unsigned)(rows / 64)), dim3(256), 0, st, A, lda, s, kb,
-                         ctx->linvT);
-      prof_end(ctx, K_TRSM, ev, (double)rows * NB * NB, 2.0 * rows * NB * 8);
+  r = ensure_events(ctx, 2 * (size_t)npb + 2);
+  if (r) return r;
+  hipStream_t main = ctx->stream, side = ctx->side;
+  hipEvent_t* ev = ctx->evs.data();  // [0]: inputs ready; 1+2k: E1_k (trsm k); 2+2k: E2_k
+  Launcher L{ctx, A, lda};
+  hipLaunchKernelGGL(status_init_kernel, dim3(1), dim3(1), 0, main, ctx->status);
+  if (!ctx->lookahead) {
+    for (int64_t k = 0; k < npb; ++k) {
+      L.potrf(main, k, n);
+      L.trsm(main, k, Mp);
+      if (k + 1 < npb) L.syrk(main, k, Mp, 0);
     }
-    if (k + 1 < npb) {
-      const int64_t T = (Mp - s) / ST;
-      const int64_t tiles = T * (T + 1) / 2;
-      const double m = (double)(Mp - s);
-      prof_begin(ctx, K_SYRK, &ev);
-      hipLaunchKernelGGL(syrk_kernel, dim3((unsigned)tiles), dim3(256), 0, st, A, lda, s, kb);
-      // algorithmic: lower triangle m(m+1)/2 outputs x NB FMAs; bytes: C read+write
-      prof_end(ctx, K_SYRK, ev, m * (m + 1) * NB, m * (m + 1) / 2 * 16.0);
+  } else {
+    hipEventRecord(ev[0], main);
+    hipStreamWaitEvent(side, ev[0], 0);
+    L.potrf(side, 0, n);
+    L.trsm(side, 0, Mp);
+    hipEventRecord(ev[1], side);
+    for (int64_t k = 0; k + 1 < npb; ++k) {
+      // main: the bulk of step k's trailing update, once panel k is solved
+      hipStreamWaitEvent(main, ev[1 + 2 * k], 0);
+      L.syrk(main, k, Mp, 2);
+      hipEventRecord(ev[2 + 2 * k], main);
+      // side: block column k+1 first, then its factor and panel solve
+      if (k > 0) hipStreamWaitEvent(side, ev[2 + 2 * (k - 1)], 0);
+      L.syrk(side, k, Mp, 1);
+      L.potrf(side, k + 1, n);
+      L.trsm(side, k + 1, Mp);
+      hipEventRecord(ev[1 + 2 * (k + 1)], side);
     }
-    r = hip_fail(ctx, hipGetLastError(), "cholesky launch");
-    if (r) return r;
+    hipStreamWaitEvent(main, ev[1 + 2 * (npb - 1)], 0);
   }
-  hipEvent_t ev;
-  prof_begin(ctx, K_FINALIZE, &ev);
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, st, A, lda, n, ctx->parts, (int)npb,
-                     ctx->status, negative, d_out);
-  prof_end(ctx, K_FINALIZE, ev, 0, (double)n * 8);
+  r = hip_fail(ctx, hipGetLastError(), "cholesky launch");
+  if (r) return r;
+  hipEvent_t pe;
+  prof_begin(ctx, K_FINALIZE, &pe, main);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, main, A, lda, n, ctx->parts,
+                     (int)npb, ctx->status, negative, d_out);
+  prof_end(ctx, K_FINALIZE, pe, 0, (double)n * 8, main);
   return hip_fail(ctx, hipGetLastError(), "finalize_kernel");
 }
 
@@ -440,10 +648,10 @@ int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int ma
     attr_set = true;
   }
   hipEvent_t ev;
-  prof_begin(ctx, K_SMALL, &ev);
+  prof_begin(ctx, K_SMALL, &ev, ctx->stream);
   hipLaunchKernelGGL(small_mll_kernel, dim3(nprob), dim3(256), lds, ctx->stream,
                      d_probs, negative, d_out, d_status);
-  prof_end(ctx, K_SMALL, ev, 0, 0);
+  prof_end(ctx, K_SMALL, ev, 0, 0, ctx->stream);
   return hip_fail(ctx, hipGetLastError(), "small_mll_kernel");
 }
 

@@ -20,19 +20,30 @@
 namespace lfm {
 
 // ---------------------------------------------------------------- tables
-// Layout (doubles), W = 2T-1, d = tau' - tau in [-(T-1), T-1]:
-//   Wt[g][d] = e^{g^2} e^{-D_g d dt} erf(d dt / l - gam_g)      G*W
-//   Xt[g][d] = e^{g^2} e^{-D_g d dt}                            G*W
-//   Pt[g][tau] = erf(t_tau / l + gam_g)                         G*T
-//   Et[g][tau] = e^{-D_g t_tau}                                 G*T
-//   Qt[g][tau] = e^{g^2} (erf(t_tau / l - gam_g) + erf(gam_g))  G*T
-//   Cm[j][k]  = S_j S_k l sqrt(pi)/2 / (D_j + D_k)              G*G
-// so that kxx(j,tau; k,tau') = Cm[j][k] * ( Wt[k][d] + Wt[j][-d] + Xt[k][d] Pt[k][tau]
-//        + Xt[j][-d] Pt[j][tau'] - Et[k][tau'] Et[j][tau] (Qt[k][tau'] + Qt[j][tau]) ),
-// term-by-term the two h() calls of kernel_xx (model.py:231, 343-363).
+// The two h() calls of kernel_xx (model.py:231, 343-363) separate into per-gene tables.
+// Each erf sum of h is rewritten with exact complementary-error-function identities,
+//   erf(a - g) + erf(b + g) = erfc(g - a) - erfc(b + g),
+//   erf(t/l - g) + erf(g)   = erfc(g - t/l) - erfc(g),
+// so no table entry is the difference of two numbers near +-1 scaled by e^{g^2 - D*delta}
+// (the reference's own evaluation of those entries loses ~1e-16 * e^{g^2 + D*12}
+// absolutely; these tables do not, which also makes the fp32 gram usable).
+// Layout (doubles), W = 2T-1, d = tau' - tau in [-(T-1), T-1], delta = d * dt, g = D l / 2:
+//   Wt[g][d]   = e^{g^2 - D delta} erfc(g - delta/l)      G*W
+//   Xt[g][d]   = e^{g^2 - D delta}                        G*W
+//   Pt[g][tau] = erfc(t_tau / l + g)                      G*T
+//   Et[g][tau] = e^{-D t_tau}                             G*T
+//   Qt[g][tau] = e^{g^2} (erfc(g - t_tau/l) - erfc(g))    G*T
+//   Cm[j][k]   = S_j S_k l sqrt(pi)/2 / (D_j + D_k)       G*G
+// kxx(j,tau; k,tau') = Cm[j][k] * ( Wt[k][d] - Xt[k][d] Pt[k][tau] + Wt[j][-d]
+//        - Xt[j][-d] Pt[j][tau'] - Et[k][tau'] Et[j][tau] (Qt[k][tau'] + Qt[j][tau]) ).
 size_t tables_doubles(int G, int T) {
   const size_t W = 2 * (size_t)T - 1;
   return 2 * (size_t)G * W + 3 * (size_t)G * T + (size_t)G * G;
+}
+
+// e^{A} erfc(z) without overflow: erfcx(z) e^{A - z^2} once erfc(z) underflows towards 0.
+__device__ __forceinline__ double exp_erfc(double A, double z) {
+  return z > 0.0 ? erfcx(z) * exp(A - z * z) : exp(A) * erfc(z);
 }
 
 __global__ void tables_kernel(HypDev p, int T, double dt, const double* __restrict__ times,
@@ -51,8 +62,8 @@ __global__ void tables_kernel(HypDev p, int T, double dt, const double* __restri
       const int d = (int)(q - (int64_t)g * W) - (T - 1);
       const double gam = p.D[g] * l / 2.0;
       const double delta = (double)d * dt;
-      const double e = exp(gam * gam) * exp(-p.D[g] * delta);
-      v = idx < nW ? e * erf(delta / l - gam) : e;
+      const double A = gam * gam - p.D[g] * delta;
+      v = idx < nW ? exp_erfc(A, gam - delta / l) : exp(A);
     } else if (idx < 2 * nW + 3 * nT) {
       const int64_t q0 = idx - 2 * nW;
       const int which = (int)(q0 / nT);
@@ -60,9 +71,9 @@ __global__ void tables_kernel(HypDev p, int T, double dt, const double* __restri
       const int g = (int)(q / T);
       const double t = times[q - (int64_t)g * T];
       const double gam = p.D[g] * l / 2.0;
-      if (which == 0) v = erf(t / l + gam);
+      if (which == 0) v = erfc(t / l + gam);
       else if (which == 1) v = exp(-p.D[g] * t);
-      else v = exp(gam * gam) * (erf(t / l - gam) + erf(gam));
+      else v = exp_erfc(gam * gam, gam - t / l) - erfcx(gam);
     } else {
       const int64_t q = idx - 2 * nW - 3 * nT;
       const int j = (int)(q / G), k = (int)(q - (int64_t)j * G);
@@ -136,8 +147,8 @@ __global__ __launch_bounds__(256) void gram_grid_kernel(
     const T Qj = Qt[(int64_t)j * Tn + tau];
     const int d = tp - tau;
     T v = Wk[d] + Wj[-d];
-    v = fma(Xk[d], Pk[tau], v);
-    v = fma(Xj[-d], Pj_tp, v);
+    v = fma(-Xk[d], Pk[tau], v);
+    v = fma(-Xj[-d], Pj_tp, v);
     v = fma(-(Ek * Ej), Qk + Qj, v);
     v = Cjk * v;
     if (i == c) v = (v + da1) + da2;

@@ -51,7 +51,10 @@ struct ProfEvent {
 
 struct lfm_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // main stream: gram fill, bulk trailing updates, finalize
+  hipStream_t side = nullptr;    // high-priority look-ahead stream: panel factor + solve
+  bool lookahead = true;
+  std::vector<hipEvent_t> evs;   // cross-stream dependency events (timing disabled)
   std::string err;
   int nb = 128;  // Cholesky block size
 
@@ -61,7 +64,7 @@ struct lfm_ctx {
   float* tab32 = nullptr; size_t tab32_bytes = 0;// gene tables (fp32 copy)
   double* par = nullptr; size_t par_bytes = 0;   // packed hyperparameters + layout
   double* xin = nullptr; size_t xin_bytes = 0;   // staged x / y / loc inputs
-  double* linvT = nullptr;                       // NB x NB inverse of the diagonal block, transposed
+  double* linvT = nullptr;                       // 8 x 16x16 inverses of the diagonal sub-blocks
   double* parts = nullptr; size_t parts_cap = 0; // per-block logdet partials
   int* status = nullptr;                         // [0] first failing pivot (INT_MAX = none)
   double* result = nullptr;                      // [0..] scalar results
@@ -90,8 +93,10 @@ int ensure(lfm_ctx* ctx, void** p, size_t* cap, size_t bytes);
 int ensure_pinned(lfm_ctx* ctx, size_t bytes);
 
 // profiling hooks around a launch on ctx->stream
-void prof_begin(lfm_ctx* ctx, int cls, hipEvent_t* a);
-void prof_end(lfm_ctx* ctx, int cls, hipEvent_t a, double flops, double bytes);
+void prof_begin(lfm_ctx* ctx, int cls, hipEvent_t* a, hipStream_t st = nullptr);
+void prof_end(lfm_ctx* ctx, int cls, hipEvent_t a, double flops, double bytes,
+              hipStream_t st = nullptr);
+int ensure_events(lfm_ctx* ctx, size_t count);
 int prof_flush(lfm_ctx* ctx);
 
 GridLayout detect_grid(const double* x, int64_t n, int64_t G);
@@ -164,5 +169,12 @@ int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int ma
 // diagnostics (lfm_probe.hip)
 int probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double* ms);
 int probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d);
+int probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us);
+int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us);
+int probe_mfma4_layout(lfm_ctx* ctx, const double* a, const double* b, const double* c,
+                       double* d);
+int probe_rates(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflops);
+int probe_mfma_f64_cycles(lfm_ctx* ctx, int nblocks, int iters, double* cyc_per_mfma,
+                          double* mhz);
 
 }  // namespace lfm

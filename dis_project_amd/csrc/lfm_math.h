@@ -1,7 +1,11 @@
 // lfm_math.h — per-pair SIM kernel math (device), shared by the gram and small-N kernels.
-// Each function restates the reference expression it cites, in the same operation order.
+// Each function restates the reference expression it cites, in the same operation order,
+// with floating-point contraction off (no fused multiply-add): the reference's XLA-CPU
+// elementwise code rounds every product, and exact identities of the formula — e.g. the
+// t = 0 rows of h vanishing because erf is odd (SURVEY.md §4 KAT) — depend on it.
 #pragma once
 #include "lfm_internal.h"
+
 
 namespace lfm {
 
@@ -10,6 +14,7 @@ static constexpr double kSqrtPi = 1.7724538509055160273;
 // ------------------------------------------------------------- per-pair math
 // h(j,k,t1,t2), model.py:315-365.
 __device__ __forceinline__ double h_ref(const HypDev& p, int j, int k, double t1, double t2) {
+  #pragma clang fp contract(off)
   const double l = p.l;
   const double gk = p.D[k] * l / 2.0;                           // gamma(k), model.py:367-369
   const double tdist = t2 - t1;
@@ -23,6 +28,7 @@ __device__ __forceinline__ double h_ref(const HypDev& p, int j, int k, double t1
 
 // kernel_xx, model.py:197-235.
 __device__ __forceinline__ double kxx_ref(const HypDev& p, double ta, int j, double tb, int k) {
+  #pragma clang fp contract(off)
   const double mult = p.S[j] * p.S[k] * p.l * kSqrtPi * 0.5;
   return mult * (h_ref(p, k, j, tb, ta) + h_ref(p, j, k, ta, tb));
 }
@@ -30,6 +36,7 @@ __device__ __forceinline__ double kxx_ref(const HypDev& p, double ta, int j, dou
 // kernel_xf, model.py:237-282 (the row whose flag is non-zero is the gene row).
 __device__ __forceinline__ double kxf_ref(const HypDev& p, double ta, double ga, double fa,
                                           double tb, double gb) {
+  #pragma clang fp contract(off)
   const bool a_is_latent = (fa == 0.0);
   const double tg = a_is_latent ? tb : ta;
   const double gg = a_is_latent ? gb : ga;
@@ -47,6 +54,7 @@ __device__ __forceinline__ double kxf_ref(const HypDev& p, double ta, double ga,
 
 // kernel_ff, model.py:284-312 (divides by 2*l, not l^2: kept for parity).
 __device__ __forceinline__ double kff_ref(const HypDev& p, double ta, double tb) {
+  #pragma clang fp contract(off)
   const double d = ta - tb;
   return exp(-((d * d) / (2.0 * p.l)));
 }
@@ -55,6 +63,7 @@ __device__ __forceinline__ double kff_ref(const HypDev& p, double ta, double tb)
 // are not evaluated (the reference evaluates them and multiplies by 0).
 __device__ __forceinline__ double kernel_ref(const HypDev& p, double ta, double ga, double fa,
                                              double tb, double gb, double fb) {
+  #pragma clang fp contract(off)
   const long long f1 = flag_int(fa), f2 = flag_int(fb);
   const long long s_xx = f1 * f2, s_ff = (1 - f1) * (1 - f2);
   const long long s_xf = f1 * (1 - f2), s_fx = (1 - f1) * f2;
@@ -69,6 +78,7 @@ __device__ __forceinline__ double kernel_ref(const HypDev& p, double ta, double 
 // mean_function, model.py:143-149: m[i] = (B/D)[i / (n/G)] * int(x[i,2]).
 __device__ __forceinline__ double mean_at(const HypDev& p, const double* x, int64_t i,
                                           int64_t bs) {
+  #pragma clang fp contract(off)
   const int g = (int)(i / bs);
   return (p.B[g] / p.D[g]) * (double)flag_int(x[i * 3 + 2]);
 }

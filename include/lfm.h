@@ -161,6 +161,22 @@ int lfm_farm_destroy(lfm_ctx* ctx);
 /* ------------------------------------------------------------ diagnostics */
 /* Throughput probe of v_mfma_f64_16x16x4_f64: *tflops over a grid of nblocks x 256. */
 int lfm_probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double* ms);
+/* Shader cycles per v_mfma_f64_16x16x4_f64 per wave (8 chains) and the shader clock (MHz)
+ * seen by block 0 of an nblocks x 256 grid. */
+int lfm_probe_mfma_f64_cycles(lfm_ctx* ctx, int nblocks, int iters, double* cyc_per_mfma,
+                              double* mhz);
+/* v_mfma_f64_4x4x4_4b_f64 on one wave: per-lane a, b, c [64] -> d[5][64] for
+ * (CBSZ, ABID) = (0,0), (2,0), (2,1), (2,2), (2,3). */
+int lfm_probe_mfma4_layout(lfm_ctx* ctx, const double* a, const double* b, const double* c,
+                           double* d);
+/* fp64 rate probes: which = 0 VALU v_fma_f64, 1 v_mfma_f64_4x4x4_4b_f64 (TFLOP/s). */
+int lfm_probe_rate(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflops);
+/* Trailing-update kernel alone on a T x T grid of 128-tiles, depth kd (128 | 256),
+ * cio = 0 skips the C tile read/write: average us/launch. */
+int lfm_probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us);
+/* Diagonal-block factor kernel with phase mask (bit0 register factor, bit1 panel,
+ * bit2 trailing update, bit3 HBM load/store; 15 = product kernel): average us/launch. */
+int lfm_probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us);
 /* Layout probe: D = A(16x4) * B(4x16) on one wave; A,B,D row-major host arrays. */
 int lfm_probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d);
 

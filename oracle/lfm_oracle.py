@@ -139,6 +139,40 @@ def cross_covariance(x, y, D, S, l, chunk=256):
     return out
 
 
+def gram_error_scale(x, y, D, S, l, chunk=256):
+    """Per-element magnitude M of the intermediate terms of kernel() in the reference's
+    evaluation order: for gene/gene pairs S_j S_k l sqrt(pi)/2 times, for each h,
+    multiplier * (first_multiplier (|erf a| + |erf b|) + second_multiplier (|erf c| + |erf d|)).
+    An fp64 evaluation of the reference formula is accurate to ~eps * M, not eps * |K|
+    (the erf sums cancel and are then scaled by e^{gamma^2 - D delta}); tests compare two
+    evaluations with an absolute tolerance proportional to M."""
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64)
+    G = D.shape[0]
+    erf = scipy.special.erf
+
+    def habs(j, k, t1, t2):
+        td = t2 - t1
+        gk = gamma(D, l, k)
+        mult = np.exp(gk**2) / (D[j] + D[k])
+        a = np.exp(-D[k] * td) * (np.abs(erf(td / l - gk)) + np.abs(erf(t1 / l + gk)))
+        b = np.exp(-(D[k] * t2 + D[j] * t1)) * (np.abs(erf(t2 / l - gk)) + np.abs(erf(gk)))
+        return mult * (a + b)
+
+    out = np.empty((x.shape[0], y.shape[0]))
+    for i0 in range(0, x.shape[0], chunk):
+        xa = x[i0:i0 + chunk, None, :]
+        yb = y[None, :, :]
+        ta, tb = xa[..., 0], yb[..., 0]
+        ja, jb = gene_index(xa[..., 1], G), gene_index(yb[..., 1], G)
+        with np.errstate(over="ignore", invalid="ignore"):
+            mxx = (S[ja] * S[jb] * l * SQRT_PI * 0.5) * (habs(jb, ja, tb, ta) + habs(ja, jb, ta, tb))
+            kv = np.abs(kernel_pairs(xa, yb, D, S, l))
+        both = (flag_int(xa[..., 2]) * flag_int(yb[..., 2])) != 0
+        out[i0:i0 + chunk] = np.where(both, np.maximum(mxx, kv), kv + 1.0)
+    return out
+
+
 def gram(x, D, S, l):
     """model.py:396-414 (the dense matrix behind cola.PSD(Dense(.)))."""
     return cross_covariance(x, x, D, S, l)

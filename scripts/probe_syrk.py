@@ -1,0 +1,18 @@
+"""SYRK kernel alone: depth 128 vs 256, with and without the C tile HBM traffic."""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from dis_project_amd import _lib  # noqa: E402
+
+ctx = _lib.get_context(0)
+for T in (128, 64, 32):
+    for kd in (128, 256):
+        for cio in (1, 0):
+            us = _lib.c_double()
+            ctx.check(ctx.lib.lfm_probe_syrk(ctx.handle, T, kd, cio, 5, _lib.ctypes.byref(us)))
+            tiles = T * (T + 1) // 2
+            tf = tiles * 128 * 128 * kd * 2 / (us.value * 1e-6) / 1e12
+            print(json.dumps({"T": T, "kd": kd, "c_io": cio, "us": round(us.value, 1),
+                              "tflops_full_tiles": round(tf, 2)}), flush=True)
