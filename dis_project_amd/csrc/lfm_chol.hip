@@ -58,12 +58,22 @@ __device__ __forceinline__ double rdl(double v, int lane) {
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // ---------------------------------------------------------------- potrf
+// 1/sqrt(x) to ~1 ulp: v_rsq_f64 estimate + two Newton steps (a pivot and its inverse
+// come from one estimate instead of a correctly rounded sqrt followed by a divide).
+__device__ __forceinline__ double rsqrt_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = y * fma(-0.5 * x * y, y, 1.5);
+  y = y * fma(-0.5 * x * y, y, 1.5);
+  return y;
+}
+
 // One 256-thread workgroup, the 128x128 diagonal block in LDS, 16 columns per step:
-//  (1) wave 0 factors the 16x16 diagonal sub-block and inverts it in registers
-//      (lane = row for L, lane = column for X = L^{-1}; cross-lane values by v_readlane);
-//  (2) the rows below: P <- P X^T on fp64 MFMA, one 16-row block per wave;
+//  (1) wave 0 factors the 16x16 diagonal sub-block in registers (lane = row);
+//  (2) every wave solves rows below against it by substitution (lane = row; the L_D
+//      entries are wave-uniform LDS reads);
 //  (3) the rank-16 update of the trailing lower triangle on fp64 MFMA.
-// Pivots are kept; logdet and the first failing pivot are reduced once at the end.
+// After the loop the eight 16x16 diagonal inverses (dinv, for trsm_kernel) are built by
+// the four waves, and logdet / the first failing pivot are reduced.
 // PH (diagnostics only, lfm_probe_potrf): bit 0 = phase 1, bit 1 = phase 2, bit 2 = phase 3,
 // bit 3 = global load / store of the block. The product path always runs PH = 15.
 template <int PH>
@@ -73,91 +83,144 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
                                                         double* __restrict__ parts, int k,
                                                         int* __restrict__ status) {
   __shared__ double M[NB][NB + 1];
-  __shared__ double Xs[IB][IB + 1];
-  __shared__ double pvs[NB];
+  __shared__ double pvs[NB];  // unscaled pivots
+  __shared__ double ipv[NB];  // 1 / L_cc
   __shared__ double red[4];
   __shared__ int redi[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lk = lane >> 4;
 
-  for (int idx = tid; idx < NB * NB; idx += 256) {
-    const int r = idx / NB, q = idx - r * NB;
-    if (PH & 8) M[r][q] = (q <= r) ? A[(kb + r) * lda + kb + q] : 0.0;
-    else M[r][q] = (q == r) ? 2.0 : 0.0;
+  // block load: row r, 16-B chunks; all 32 loads of a thread issued before any LDS write
+  {
+    double2 v[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int idx = tid + 256 * u, r = idx >> 6, c2 = idx & 63;
+      v[u] = (PH & 8) ? *reinterpret_cast<const double2*>(&A[(kb + r) * lda + kb + 2 * c2])
+                      : double2{(r == 2 * c2) ? 2.0 : 0.0, (r == 2 * c2 + 1) ? 2.0 : 0.0};
+    }
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int idx = tid + 256 * u, r = idx >> 6, c2 = idx & 63;
+      M[r][2 * c2] = v[u].x;
+      M[r][2 * c2 + 1] = v[u].y;
+    }
   }
   __syncthreads();
 
   for (int ib = 0; ib < NB / IB; ++ib) {
     const int c0 = ib * IB;
     if ((PH & 1) && w == 0) {
-      // (1) rows of the sub-block on lanes 0..15 (upper part of each row is scratch)
-      double d[IB], ip[IB], x[IB];
+      double d[IB];
 #pragma unroll
       for (int q = 0; q < IB; ++q) d[q] = (lane < IB && q <= lane) ? M[c0 + lane][c0 + q] : 0.0;
 #pragma unroll
       for (int c = 0; c < IB; ++c) {
         double dc = rdl(d[c], c);
         if (kb + c0 + c >= npiv) dc = 1.0;
-        if (lane == 0) pvs[c0 + c] = dc;
-        const double piv = sqrt(dc);
-        ip[c] = 1.0 / piv;
-        d[c] = (lane == c) ? piv : d[c] * ip[c];
+        const double y = rsqrt_nr(dc);
+        if (lane == 0) {
+          pvs[c0 + c] = dc;
+          ipv[c0 + c] = y;
+        }
+        d[c] = (lane == c) ? dc * y : d[c] * y;
 #pragma unroll
         for (int q = c + 1; q < IB; ++q) d[q] = fma(-d[c], rdl(d[c], q), d[q]);
       }
-      // lane c: column c of X = L^{-1} (entries above the diagonal come out exactly 0)
-#pragma unroll
-      for (int r = 0; r < IB; ++r) {
-        double sacc = (lane == r) ? 1.0 : 0.0;
-#pragma unroll
-        for (int q = 0; q < r; ++q) sacc = fma(-rdl(d[q], r), x[q], sacc);
-        x[r] = sacc * ip[r];
-      }
       if (lane < IB) {
 #pragma unroll
-        for (int q = 0; q < IB; ++q) {
+        for (int q = 0; q < IB; ++q)
           if (q <= lane) M[c0 + lane][c0 + q] = d[q];
-          Xs[q][lane] = x[q];
-          dinv[(ib * IB + q) * IB + lane] = x[q];
-        }
       }
     }
     __syncthreads();
-    // (2) P <- P X^T for the 16-row blocks below:  B[k][j] = X[j][k]
-    const int nrb = (NB - c0 - IB) / IB;
-    for (int rb = w; (PH & 2) && rb < nrb; rb += 4) {
-      const int r0 = c0 + IB + rb * IB;
-      double4v acc = {0, 0, 0, 0};
+    // (2) rows below: x_c = (p_c - sum_{q<c} x_q L[c][q]) / L_cc
+    const int nr = NB - c0 - IB;
+    if ((PH & 2) && w * 64 < nr) {
+      const bool act = tid < nr;
+      const int row = c0 + IB + (act ? tid : 0);
+      double p[IB];
 #pragma unroll
-      for (int ks = 0; ks < IB / 4; ++ks)
-        acc = mfma16(M[r0 + li][c0 + ks * 4 + lk], Xs[li][ks * 4 + lk], acc);
-      wave_lds_fence();
+      for (int q = 0; q < IB; ++q) p[q] = M[row][c0 + q];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) M[r0 + lk + 4 * r][c0 + li] = acc[r];
+      for (int c = 0; c < IB; ++c) {
+        double sacc = p[c];
+#pragma unroll
+        for (int q = 0; q < c; ++q) sacc = fma(-p[q], M[c0 + c][c0 + q], sacc);
+        p[c] = sacc * ipv[c0 + c];
+      }
+      if (act) {
+#pragma unroll
+        for (int q = 0; q < IB; ++q) M[row][c0 + q] = p[q];
+      }
     }
     __syncthreads();
-    // (3) rank-16 update of the trailing lower triangle, one 16x16 tile per wave at a time
+    // (3) rank-16 update of the trailing lower triangle, two 16x16 tiles per wave at a time
+    const int nrb = nr / IB;
     const int ntiles = (PH & 4) ? nrb * (nrb + 1) / 2 : 0;
-    for (int t = w; t < ntiles; t += 4) {
-      int ti = (int)((sqrtf(8.0f * t + 1.0f) - 1.0f) * 0.5f);
-      while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-      while (ti * (ti + 1) / 2 > t) --ti;
-      const int tj = t - ti * (ti + 1) / 2;
-      const int i0 = c0 + IB + ti * IB, j0 = c0 + IB + tj * IB;
-      double4v acc;
+    for (int t = w; t < ntiles; t += 8) {
+      int i0[2], j0[2];
+      bool on[2];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r] = M[i0 + lk + 4 * r][j0 + li];
+      for (int u = 0; u < 2; ++u) {
+        const int tt = t + 4 * u;
+        on[u] = tt < ntiles;
+        const int tc = on[u] ? tt : t;
+        int ti = (int)((sqrtf(8.0f * tc + 1.0f) - 1.0f) * 0.5f);
+        while ((ti + 1) * (ti + 2) / 2 <= tc) ++ti;
+        while (ti * (ti + 1) / 2 > tc) --ti;
+        i0[u] = c0 + IB + ti * IB;
+        j0[u] = c0 + IB + (tc - ti * (ti + 1) / 2) * IB;
+      }
+      double4v acc[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[u][r] = M[i0[u] + lk + 4 * r][j0[u] + li];
 #pragma unroll
       for (int ks = 0; ks < IB / 4; ++ks)
-        acc = mfma16(-M[i0 + li][c0 + ks * 4 + lk], M[j0 + li][c0 + ks * 4 + lk], acc);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) M[i0 + lk + 4 * r][j0 + li] = acc[r];
+        for (int u = 0; u < 2; ++u)
+          acc[u] = mfma16(-M[i0[u] + li][c0 + ks * 4 + lk], M[j0[u] + li][c0 + ks * 4 + lk], acc[u]);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (on[u]) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) M[i0[u] + lk + 4 * r][j0[u] + li] = acc[u][r];
+        }
     }
     __syncthreads();
   }
-  for (int idx = tid; idx < NB * NB; idx += 256) {
-    const int r = idx / NB, q = idx - r * NB;
-    if ((PH & 8) && q <= r) A[(kb + r) * lda + kb + q] = M[r][q];
+  // inverses of the eight 16x16 diagonal blocks: wave w builds blocks w and w + 4,
+  // lane c (< 16) column c by forward substitution; dinv[ib][r][c] = X[r][c]
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int ib = w + 4 * h, c0 = ib * IB;
+    double x[IB];
+#pragma unroll
+    for (int r = 0; r < IB; ++r) {
+      double sacc = (li == r) ? 1.0 : 0.0;
+#pragma unroll
+      for (int q = 0; q < r; ++q) sacc = fma(-M[c0 + r][c0 + q], x[q], sacc);
+      x[r] = sacc * ipv[c0 + r];
+    }
+    if (lane < IB) {
+#pragma unroll
+      for (int r = 0; r < IB; ++r) dinv[(ib * IB + r) * IB + lane] = x[r];
+    }
+  }
+  // block store (lower triangle incl. diagonal)
+  if (PH & 8) {
+#pragma unroll 8
+    for (int u = 0; u < 32; ++u) {
+      const int idx = tid + 256 * u, r = idx >> 6, c2 = idx & 63;
+      if (2 * c2 <= r) {
+        double2 v;
+        v.x = M[r][2 * c2];
+        v.y = M[r][2 * c2 + 1];  // past the diagonal: scratch (the upper triangle is unused)
+        *reinterpret_cast<double2*>(&A[(kb + r) * lda + kb + 2 * c2]) = v;
+      }
+    }
   }
   // logdet partial = 1/2 sum log(pivot) over real pivots; first non-positive pivot
   double lg = 0.0;

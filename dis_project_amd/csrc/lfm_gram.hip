@@ -156,6 +156,65 @@ __global__ __launch_bounds__(256) void gram_grid_kernel(
   }
 }
 
+// Aligned variant: T % 256 == 0, so a 64-row x 256-column tile lies inside one (gene j,
+// gene k) block. The tile's Toeplitz windows of Wt/Xt (d = tau' - tau spans 319 values)
+// and its row tables are staged in LDS once; each element then costs 4 conflict-free LDS
+// reads (consecutive d across lanes), 3 wave-uniform ones and one coalesced store.
+template <typename T>
+__global__ __launch_bounds__(256) void gram_grid_aligned_kernel(
+    const T* __restrict__ tab, int G, int Tn, const int* __restrict__ bg, int64_t n, T da1, T da2,
+    int lower, T* __restrict__ out, int64_t ldo) {
+  constexpr int R = 64, C = 256, WIN = C + R - 1;
+  __shared__ T sWk[WIN], sXk[WIN], sWj[WIN], sXj[WIN];
+  __shared__ T sPk[R], sEj[R], sQj[R];
+  const int64_t c0 = (int64_t)blockIdx.x * C, r0 = (int64_t)blockIdx.y * R;
+  if (lower && c0 > r0 + R - 1) return;
+  const int tid = threadIdx.x;
+  const int W = 2 * Tn - 1;
+  const T* Wt = tab;
+  const T* Xt = Wt + (int64_t)G * W;
+  const T* Pt = Xt + (int64_t)G * W;
+  const T* Et = Pt + (int64_t)G * Tn;
+  const T* Qt = Et + (int64_t)G * Tn;
+  const T* Cm = Qt + (int64_t)G * Tn;
+  const int j = bg[r0 / Tn], k = bg[c0 / Tn];
+  const int tau0 = (int)(r0 % Tn), tp0 = (int)(c0 % Tn);
+  const int dmin = tp0 - tau0 - (R - 1);  // window index e = d - dmin
+  for (int e = tid; e < WIN; e += 256) {
+    const int d = dmin + e;
+    sWk[e] = Wt[(int64_t)k * W + (Tn - 1) + d];
+    sXk[e] = Xt[(int64_t)k * W + (Tn - 1) + d];
+    sWj[e] = Wt[(int64_t)j * W + (Tn - 1) - d];
+    sXj[e] = Xt[(int64_t)j * W + (Tn - 1) - d];
+  }
+  if (tid < R) {
+    sPk[tid] = Pt[(int64_t)k * Tn + tau0 + tid];
+    sEj[tid] = Et[(int64_t)j * Tn + tau0 + tid];
+    sQj[tid] = Qt[(int64_t)j * Tn + tau0 + tid];
+  }
+  const int tp = tp0 + tid;
+  const T Ek = Et[(int64_t)k * Tn + tp];
+  const T Qk = Qt[(int64_t)k * Tn + tp];
+  const T Pj = Pt[(int64_t)j * Tn + tp];
+  const T Cjk = Cm[(int64_t)j * G + k];
+  __syncthreads();
+  const int64_t c = c0 + tid;
+  T* op = out + r0 * ldo + c;
+#pragma unroll 4
+  for (int i = 0; i < R; ++i) {
+    const int64_t row = r0 + i;
+    if (lower && c > row) continue;
+    const int e = tid + (R - 1) - i;
+    T v = sWk[e] + sWj[e];
+    v = fma(-sXk[e], sPk[i], v);
+    v = fma(-sXj[e], Pj, v);
+    v = fma(-(Ek * sEj[i]), Qk + sQj[i], v);
+    v = Cjk * v;
+    if (row == c) v = (v + da1) + da2;
+    op[(int64_t)i * ldo] = v;
+  }
+}
+
 __global__ void f64_to_f32_kernel(const double* __restrict__ a, float* __restrict__ b, int64_t n) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * blockDim.x)
@@ -178,13 +237,19 @@ int launch_gram_grid(lfm_ctx* ctx, const HypDev& h, const GridLayout& lay, const
                        (int64_t)nt);
     tabT = ctx->tab32;
   }
-  dim3 grid((unsigned)((n + 255) / 256), (unsigned)((n + GR - 1) / GR));
   const int lower = uplo == LFM_UPLO_LOWER;
   const double elems = lower ? (double)n * (n + 1) / 2 : (double)n * n;
   hipEvent_t ev;
   prof_begin(ctx, K_GRAM_GRID, &ev);
-  hipLaunchKernelGGL((gram_grid_kernel<OutT, GR>), grid, dim3(256), 0, ctx->stream, tabT, h.G,
-                     lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out, ldo);
+  if (lay.T % 256 == 0) {
+    dim3 grid((unsigned)(n / 256), (unsigned)(n / 64));
+    hipLaunchKernelGGL((gram_grid_aligned_kernel<OutT>), grid, dim3(256), 0, ctx->stream, tabT,
+                       h.G, lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out, ldo);
+  } else {
+    dim3 grid((unsigned)((n + 255) / 256), (unsigned)((n + GR - 1) / GR));
+    hipLaunchKernelGGL((gram_grid_kernel<OutT, GR>), grid, dim3(256), 0, ctx->stream, tabT, h.G,
+                       lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out, ldo);
+  }
   prof_end(ctx, K_GRAM_GRID, ev, 0, elems * sizeof(OutT));
   return hip_fail(ctx, hipGetLastError(), "gram_grid_kernel");
 }

@@ -218,3 +218,47 @@ def test_structured_and_direct_paths_agree(lfm):
     K_dir = m.gram(m.kernel, g["x"][perm]).to_dense()
     assert_gram_close(K_grid[np.ix_(perm, perm)], K_dir, g["x"][perm], g["x"][perm], g["D"],
                       g["S"], float(g["l"]))
+
+
+def grid_problem(G, T, seed, l=2.5, sd=1.0, jitter=1e-4):
+    rng = np.random.default_rng(seed)
+    D = rng.uniform(0.2, 1.0, G)
+    S = rng.uniform(0.5, 1.5, G)
+    B = rng.uniform(0.01, 0.1, G)
+    x = np.stack((np.tile(np.linspace(0, 12, T), G), np.repeat(np.arange(G), T), np.ones(G * T)),
+                 -1)
+    y = np.repeat(B / D, T) + 0.5 * rng.standard_normal(G * T)
+    return x, y, D, S, B, l, sd, jitter
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_gram_aligned_T256(lfm, G):
+    """T = 256: the LDS-staged aligned grid kernel (configs 2-4 use it)."""
+    x, y, D, S, B, l, sd, jit = grid_problem(G, 256, 40 + G, l=1.8)
+    m = lfm.ExactLFM(jitter=jit, obs_stddev=sd, num_genes=G, true_d=D, true_s=S, true_b=B, l=l)
+    Kref = O.gram(x, D, S, l)
+    assert_gram_close(m.gram(m.kernel, x).to_dense(), Kref, x, x, D, S, l)
+    assert_gram_close(m.gram_f32(x).astype(np.float64), Kref, x, x, D, S, l, extra_rel=4e-6)
+
+
+def test_mll_aligned_T256_permuted_genes(lfm):
+    """Blocks in a shuffled gene order (an ablation-style layout) on the aligned path."""
+    x, y, D, S, B, l, sd, jit = grid_problem(4, 256, 77)
+    order = np.array([2, 0, 3, 1])
+    x2 = x.copy()
+    x2[:, 1] = np.repeat(order, 256)
+    ref = O.mll(x2, y, D, S, B, l, sd, jit)
+    m = lfm.ExactLFM(jitter=jit, obs_stddev=sd, num_genes=4, true_d=D, true_s=S, true_b=B, l=l)
+    v = lfm.CustomConjMLL()(m, lfm.Dataset(x2, y))
+    assert abs(v - ref) <= MLL_RTOL * abs(ref), (v, ref)
+
+
+@pytest.mark.slow
+def test_mll_n4096_vs_oracle(lfm):
+    """N = 4096 (16 genes x 256 timepoints): 32 block columns through the look-ahead
+    pipeline, compared with the scipy oracle. Tolerance: the north_star 1e-5, held to 1e-9."""
+    x, y, D, S, B, l, sd, jit = grid_problem(16, 256, 4096)
+    ref = O.mll(x, y, D, S, B, l, sd, jit, negative=True)
+    m = lfm.ExactLFM(jitter=jit, obs_stddev=sd, num_genes=16, true_d=D, true_s=S, true_b=B, l=l)
+    v = lfm.CustomConjMLL(negative=True)(m, lfm.Dataset(x, y))
+    assert abs(v - ref) <= MLL_RTOL * abs(ref), (v, ref)
