@@ -121,6 +121,7 @@ SIGNATURES = [
     ("lfm_probe_mfma_f64", c_int, [_c_ctx, c_int, c_int, _dptr, _dptr]),
     ("lfm_probe_mfma_f64_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr]),
     ("lfm_probe_potrf", c_int, [_c_ctx, c_int, c_int, _dptr]),
+    ("lfm_probe_trsm", c_int, [_c_ctx, c_int, c_int, c_int, _dptr]),
     ("lfm_probe_syrk", c_int, [_c_ctx, c_int, c_int, c_int, c_int, _dptr]),
     ("lfm_probe_rate", c_int, [_c_ctx, c_int, c_int, c_int, _dptr]),
     ("lfm_probe_mfma4_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr, _dptr]),

@@ -420,6 +420,8 @@ namespace {
 // the main stream off them (hipExtStreamCreateWithCUMask); 0 (default) shares every CU and
 // relies on the side stream's higher priority. LFM_LOOKAHEAD=0 serialises on one stream.
 hipError_t create_streams(lfm_ctx* ctx) {
+  const char* tv = std::getenv("LFM_TRSM");
+  if (tv) ctx->trsm_variant = std::atoi(tv);
   const char* la = std::getenv("LFM_LOOKAHEAD");
   ctx->lookahead = !(la && std::atoi(la) == 0);
   int least = 0, greatest = 0;
@@ -921,6 +923,12 @@ int lfm_probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   if (!ctx || !us || T < 1 || reps < 1 || (kd != 128 && kd != 256)) return LFM_E_ARG;
   DeviceGuard g(ctx->device);
   return probe_syrk(ctx, T, kd, cio, reps, us);
+}
+
+int lfm_probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us) {
+  if (!ctx || !us || rows < 64 || rows % 64 || reps < 1) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_trsm(ctx, variant, rows, reps, us);
 }
 
 int lfm_probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us) {

@@ -45,12 +45,50 @@ __device__ __forceinline__ double4v mfma16(double a, double b, double4v c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// v_mfma_f64_4x4x4_4b_f64: four independent 4x4x4 blocks, g = (lane >> 2) & 3; lane maps
+// (scripts/probe_mfma4_layout.py): A_g[i][k] at lane 16k + 4g + i, B_g[k][j] at lane
+// 16k + 4g + j, D_g[i][j] at lane 16i + 4g + j.
+__device__ __forceinline__ double mfma4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
 // Value of v held by `lane` (compile-time lane after unrolling), broadcast to the wave.
 __device__ __forceinline__ double rdl(double v, int lane) {
   const unsigned long long b = (unsigned long long)__double_as_longlong(v);
   const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffu), lane);
   const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Value of v held by lane `src` (0..15, compile-time) of each 16-lane row, broadcast to the
+// row: DPP row_newbcast (VGPR to VGPR; no SGPR round trip as with v_readlane).
+template <int SRC>
+__device__ __forceinline__ double row_bcast_t(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, 0x150 + SRC, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x150 + SRC, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// src folds to a constant in the fully unrolled callers
+__device__ __forceinline__ double row_bcast(double v, int src) {
+  switch (src) {
+    case 0: return row_bcast_t<0>(v);
+    case 1: return row_bcast_t<1>(v);
+    case 2: return row_bcast_t<2>(v);
+    case 3: return row_bcast_t<3>(v);
+    case 4: return row_bcast_t<4>(v);
+    case 5: return row_bcast_t<5>(v);
+    case 6: return row_bcast_t<6>(v);
+    case 7: return row_bcast_t<7>(v);
+    case 8: return row_bcast_t<8>(v);
+    case 9: return row_bcast_t<9>(v);
+    case 10: return row_bcast_t<10>(v);
+    case 11: return row_bcast_t<11>(v);
+    case 12: return row_bcast_t<12>(v);
+    case 13: return row_bcast_t<13>(v);
+    case 14: return row_bcast_t<14>(v);
+    default: return row_bcast_t<15>(v);
+  }
 }
 
 // Orders one wave's LDS writes before its following LDS reads (and vice versa): LDS
@@ -82,13 +120,17 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
                                                         double* __restrict__ dinv,
                                                         double* __restrict__ parts, int k,
                                                         int* __restrict__ status) {
-  __shared__ double M[NB][NB + 1];
+  // only the 36 lower 16x16 blocks of the 128x128 block, each 16 x 17 (padded) doubles:
+  // 78 KB, so the kernel fits on a CU beside one SYRK workgroup (look-ahead overlap)
+  __shared__ double Mb[(NB / IB) * (NB / IB + 1) / 2 * IB * (IB + 1)];
   __shared__ double pvs[NB];  // unscaled pivots
   __shared__ double ipv[NB];  // 1 / L_cc
   __shared__ double red[4];
   __shared__ int redi[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lk = lane >> 4;
+#define MS(r, q) Mb[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * (IB * (IB + 1)) + \
+                    ((r) & 15) * (IB + 1) + ((q) & 15)]
 
   // block load: row r, 16-B chunks; all 32 loads of a thread issued before any LDS write
   {
@@ -102,8 +144,10 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
 #pragma unroll
     for (int u = 0; u < 32; ++u) {
       const int idx = tid + 256 * u, r = idx >> 6, c2 = idx & 63;
-      M[r][2 * c2] = v[u].x;
-      M[r][2 * c2 + 1] = v[u].y;
+      if ((2 * c2) >> 4 <= r >> 4) {
+        MS(r, 2 * c2) = v[u].x;
+        MS(r, 2 * c2 + 1) = v[u].y;
+      }
     }
   }
   __syncthreads();
@@ -111,26 +155,31 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
   for (int ib = 0; ib < NB / IB; ++ib) {
     const int c0 = ib * IB;
     if ((PH & 1) && w == 0) {
-      double d[IB];
+      double d[IB], pv[IB], yv[IB];
 #pragma unroll
-      for (int q = 0; q < IB; ++q) d[q] = (lane < IB && q <= lane) ? M[c0 + lane][c0 + q] : 0.0;
+      for (int q = 0; q < IB; ++q) d[q] = (lane < IB && q <= lane) ? MS(c0 + li, c0 + q) : 0.0;
 #pragma unroll
       for (int c = 0; c < IB; ++c) {
-        double dc = rdl(d[c], c);
+        double dc = row_bcast(d[c], c);
         if (kb + c0 + c >= npiv) dc = 1.0;
         const double y = rsqrt_nr(dc);
-        if (lane == 0) {
-          pvs[c0 + c] = dc;
-          ipv[c0 + c] = y;
-        }
+        pv[c] = dc;
+        yv[c] = y;
         d[c] = (lane == c) ? dc * y : d[c] * y;
 #pragma unroll
-        for (int q = c + 1; q < IB; ++q) d[q] = fma(-d[c], rdl(d[c], q), d[q]);
+        for (int q = c + 1; q < IB; ++q) d[q] = fma(-d[c], row_bcast(d[c], q), d[q]);
       }
       if (lane < IB) {
 #pragma unroll
         for (int q = 0; q < IB; ++q)
-          if (q <= lane) M[c0 + lane][c0 + q] = d[q];
+          if (q <= lane) MS(c0 + lane, c0 + q) = d[q];
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int c = 0; c < IB; ++c) {
+          pvs[c0 + c] = pv[c];
+          ipv[c0 + c] = yv[c];
+        }
       }
     }
     __syncthreads();
@@ -141,17 +190,17 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
       const int row = c0 + IB + (act ? tid : 0);
       double p[IB];
 #pragma unroll
-      for (int q = 0; q < IB; ++q) p[q] = M[row][c0 + q];
+      for (int q = 0; q < IB; ++q) p[q] = MS(row, c0 + q);
 #pragma unroll
       for (int c = 0; c < IB; ++c) {
         double sacc = p[c];
 #pragma unroll
-        for (int q = 0; q < c; ++q) sacc = fma(-p[q], M[c0 + c][c0 + q], sacc);
+        for (int q = 0; q < c; ++q) sacc = fma(-p[q], MS(c0 + c, c0 + q), sacc);
         p[c] = sacc * ipv[c0 + c];
       }
       if (act) {
 #pragma unroll
-        for (int q = 0; q < IB; ++q) M[row][c0 + q] = p[q];
+        for (int q = 0; q < IB; ++q) MS(row, c0 + q) = p[q];
       }
     }
     __syncthreads();
@@ -176,17 +225,17 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) acc[u][r] = M[i0[u] + lk + 4 * r][j0[u] + li];
+        for (int r = 0; r < 4; ++r) acc[u][r] = MS(i0[u] + lk + 4 * r, j0[u] + li);
 #pragma unroll
       for (int ks = 0; ks < IB / 4; ++ks)
 #pragma unroll
         for (int u = 0; u < 2; ++u)
-          acc[u] = mfma16(-M[i0[u] + li][c0 + ks * 4 + lk], M[j0[u] + li][c0 + ks * 4 + lk], acc[u]);
+          acc[u] = mfma16(-MS(i0[u] + li, c0 + ks * 4 + lk), MS(j0[u] + li, c0 + ks * 4 + lk), acc[u]);
 #pragma unroll
       for (int u = 0; u < 2; ++u)
         if (on[u]) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) M[i0[u] + lk + 4 * r][j0[u] + li] = acc[u][r];
+          for (int r = 0; r < 4; ++r) MS(i0[u] + lk + 4 * r, j0[u] + li) = acc[u][r];
         }
     }
     __syncthreads();
@@ -201,7 +250,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
     for (int r = 0; r < IB; ++r) {
       double sacc = (li == r) ? 1.0 : 0.0;
 #pragma unroll
-      for (int q = 0; q < r; ++q) sacc = fma(-M[c0 + r][c0 + q], x[q], sacc);
+      for (int q = 0; q < r; ++q) sacc = fma(-MS(c0 + r, c0 + q), x[q], sacc);
       x[r] = sacc * ipv[c0 + r];
     }
     if (lane < IB) {
@@ -216,8 +265,8 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
       const int idx = tid + 256 * u, r = idx >> 6, c2 = idx & 63;
       if (2 * c2 <= r) {
         double2 v;
-        v.x = M[r][2 * c2];
-        v.y = M[r][2 * c2 + 1];  // past the diagonal: scratch (the upper triangle is unused)
+        v.x = MS(r, 2 * c2);
+        v.y = MS(r, 2 * c2 + 1);  // past the diagonal: scratch (the upper triangle is unused)
         *reinterpret_cast<double2*>(&A[(kb + r) * lda + kb + 2 * c2]) = v;
       }
     }
@@ -244,15 +293,111 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
     const int b = min(min(redi[0], redi[1]), min(redi[2], redi[3]));
     if (b != STATUS_NONE) atomicMin(status, b);
   }
+#undef MS
 }
 
 // ----------------------------------------------------------------- trsm
+// Rows [s, Mp) of block column kb, 32 rows per workgroup (2 waves x 16 rows):
+//   X_cb = (A_cb - sum_{q < cb} X_q L_{cb,q}^T) * Dinv_cb^T,  cb = 0..7 (16 columns each).
+// The factored diagonal block (its 36 lower 16x16 blocks) and the rows are staged in LDS
+// once (111 KB: fits beside one SYRK workgroup); the products run on
+// v_mfma_f64_4x4x4_4b_f64 with A replicated over the 4 blocks, so the 16x16 accumulator
+// acc[ir] holds X[ir*4 + (lane >> 4)][lane & 15] — the 16x16 MFMA layout — as four
+// independent chains.
+__global__ __launch_bounds__(128) void trsm_kernel_v3(double* __restrict__ A, int64_t lda, int64_t s,
+                                                   int64_t kb, const double* __restrict__ dinv) {
+  constexpr int RW = 32;                               // rows per workgroup
+  constexpr int BS = IB * (IB + 1);                    // one padded 16x16 block
+  __shared__ double sA[RW][NB + 1];
+  __shared__ double Lb[(NB / IB) * (NB / IB + 1) / 2 * BS];
+#define LS(r, q) Lb[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * BS + ((r) & 15) * (IB + 1) + ((q) & 15)]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lk = lane >> 4, l3 = lane & 3;
+  const int64_t r0 = s + (int64_t)blockIdx.x * RW;
+  // rows: 32 x 64 double2 = 16 per thread; diagonal block: the 36 lower 16x16 blocks
+  {
+    double2 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int idx = tid + 128 * u, r = idx >> 6, c2 = idx & 63;
+      v[u] = *reinterpret_cast<const double2*>(&A[(r0 + r) * lda + kb + 2 * c2]);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int idx = tid + 128 * u, r = idx >> 6, c2 = idx & 63;
+      sA[r][2 * c2] = v[u].x;
+      sA[r][2 * c2 + 1] = v[u].y;
+    }
+  }
+  for (int half = 0; half < 2; ++half) {
+    double2 v[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int idx = tid + 128 * (u + 32 * half), r = idx >> 6, c2 = idx & 63;
+      if ((2 * c2) >> 4 <= r >> 4) v[u] = *reinterpret_cast<const double2*>(&A[(kb + r) * lda + kb + 2 * c2]);
+    }
+#pragma unroll
+    for (int u = 0; u < 32; ++u) {
+      const int idx = tid + 128 * (u + 32 * half), r = idx >> 6, c2 = idx & 63;
+      if ((2 * c2) >> 4 <= r >> 4) {
+        LS(r, 2 * c2) = v[u].x;
+        LS(r, 2 * c2 + 1) = v[u].y;
+      }
+    }
+  }
+  // Dinv_cb fragments for the Z = acc Dinv^T step: B[k][j] = Dinv[j][k], lane: j = li, k = lk
+  double dv[NB / IB][IB / 4];
+#pragma unroll
+  for (int cb = 0; cb < NB / IB; ++cb)
+#pragma unroll
+    for (int ks = 0; ks < IB / 4; ++ks) dv[cb][ks] = dinv[cb * IB * IB + li * IB + ks * 4 + lk];
+  __syncthreads();
+
+  const int wr = w * IB;
+#pragma unroll
+  for (int cb = 0; cb < NB / IB; ++cb) {
+    double acc[4];
+#pragma unroll
+    for (int ir = 0; ir < 4; ++ir) acc[ir] = sA[wr + ir * 4 + lk][cb * IB + li];
+#pragma unroll 4
+    for (int q0 = 0; q0 < cb * IB; q0 += 4) {
+      const double b = LS(cb * IB + li, q0 + lk);
+#pragma unroll
+      for (int ir = 0; ir < 4; ++ir) acc[ir] = mfma4(-sA[wr + ir * 4 + l3][q0 + lk], b, acc[ir]);
+    }
+    // Z = acc * Dinv_cb^T: acc goes through the wave's own LDS rows to become the A operand
+#pragma unroll
+    for (int ir = 0; ir < 4; ++ir) sA[wr + ir * 4 + lk][cb * IB + li] = acc[ir];
+    wave_lds_fence();
+    double z[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int ks = 0; ks < IB / 4; ++ks)
+#pragma unroll
+      for (int ir = 0; ir < 4; ++ir)
+        z[ir] = mfma4(sA[wr + ir * 4 + l3][cb * IB + ks * 4 + lk], dv[cb][ks], z[ir]);
+    wave_lds_fence();
+#pragma unroll
+    for (int ir = 0; ir < 4; ++ir) sA[wr + ir * 4 + lk][cb * IB + li] = z[ir];
+    wave_lds_fence();
+  }
+  // the wave's 16 rows back to HBM
+  for (int idx = lane; idx < IB * (NB / 2); idx += 64) {
+    const int r = idx / (NB / 2), q2 = idx - r * (NB / 2);
+    double2 v;
+    v.x = sA[wr + r][2 * q2];
+    v.y = sA[wr + r][2 * q2 + 1];
+    *reinterpret_cast<double2*>(&A[(r0 + wr + r) * lda + kb + 2 * q2]) = v;
+  }
+#undef LS
+}
+
+// ------------------------------------------------------------ trsm (v2)
 // Rows [s, Mp) of block column kb, 64 rows per workgroup, 16 rows per wave:
 //   X_cb = (A_cb - sum_{q < cb} X_q L_{cb,q}^T) * Dinv_cb^T,  cb = 0..7 (16 columns each).
 // The wave's rows live in LDS; the L_{cb,q} fragments (the factored diagonal block, shared
 // by every workgroup, L2-resident) for column block cb+1 are loaded while cb computes,
 // and the K chain is split over two accumulators.
-__global__ __launch_bounds__(256) void trsm_kernel(double* __restrict__ A, int64_t lda, int64_t s,
+__global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, int64_t lda, int64_t s,
                                                    int64_t kb, const double* __restrict__ dinv) {
   __shared__ double sA[64][NB + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -326,20 +471,18 @@ __global__ __launch_bounds__(256) void trsm_kernel(double* __restrict__ A, int64
 // 16 lanes, as the 16x16 layout. Per K step of 4: 16 A + 4 B fragments, 64 MFMAs.
 // The K dimension (NB) is staged KB columns at a time through LDS, the next stage
 // prefetched into registers while the current one feeds the MFMAs.
-__device__ __forceinline__ double mfma4(double a, double b, double c) {
-  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
-}
-
 // mode 0: every lower tile; 1: only tile column 0 (the next block column, look-ahead);
 // 2: every lower tile with tile column >= 1 (the rest).
 // KD: depth of the update (columns kb .. kb+KD of A). CIO = false (diagnostics only) skips
 // the C tile's HBM read and write.
-template <int KD, bool CIO>
+template <int KD, bool CIO, int TR>
 __global__ __launch_bounds__(256, 2) void syrk_kernel(double* __restrict__ A, int64_t lda,
                                                       int64_t s, int64_t kb, int mode) {
+  // TR = tile rows (128, or 64 for the latency-critical look-ahead column); 128 columns.
+  constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
   __shared__ double sP[2][ST][KB + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wr = (w >> 1) * 64, wc = (w & 1) * 64;
+  const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
   const int li = lane & 15, lk = lane >> 4, l3 = lane & 3;
 
   const int64_t b = blockIdx.x;
@@ -357,36 +500,36 @@ __global__ __launch_bounds__(256, 2) void syrk_kernel(double* __restrict__ A, in
       ++tj;
     }
   }
-  const int64_t i0 = s + (int64_t)ti * ST, j0 = s + (int64_t)tj * ST;
-  const bool diag = (ti == tj);
+  const int64_t i0 = s + (int64_t)ti * TR, j0 = s + (int64_t)tj * ST;
+  const bool diag = i0 < j0 + ST;  // the tile reaches the diagonal: keep col <= row only
   double* Cb = A + (i0 + wr + lk) * lda + j0 + wc + li;  // C[wr + lk][wc + li]
   const int ld4 = (int)(4 * lda);  // row-group stride (elements); 60 * ld4 < 2^31 for lda < 2^23
 
-  double acc[16][4];
+  double acc[IRN][4];
 #pragma unroll
-  for (int ir = 0; ir < 16; ++ir)
+  for (int ir = 0; ir < IRN; ++ir)
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = CIO ? Cb[ir * ld4 + jr * 16] : 0.0;
 
-  // staging map: 2 panels x 128 rows x KB doubles = 8 double2 per thread; thread tid moves
-  // chunk (tid & 7) of rows (tid >> 3) + 32u of each panel
+  // staging: TR rows of panel i and 128 rows of panel j, KB doubles each; thread tid moves
+  // chunk (tid & 7) of rows (tid >> 3) + 32u
   static_assert(KB == 16, "staging map assumes 8 double2 chunks per row");
+  constexpr int NUI = TR / 32, NU = NUI + 4;
   const int srow = tid >> 3, sch = tid & 7;
   const double* gi = A + (i0 + srow) * lda + kb + 2 * sch;
   const double* gj = A + (j0 + srow) * lda + kb + 2 * sch;
   const int ld32 = (int)(32 * lda);
-  double2 pre[8];
+  double2 pre[NU];
   auto gload = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      pre[u] = *reinterpret_cast<const double2*>(gi + u * ld32 + k0);
-      pre[4 + u] = *reinterpret_cast<const double2*>(gj + u * ld32 + k0);
-    }
+    for (int u = 0; u < NUI; ++u) pre[u] = *reinterpret_cast<const double2*>(gi + u * ld32 + k0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pre[NUI + u] = *reinterpret_cast<const double2*>(gj + u * ld32 + k0);
   };
   auto lstore = [&]() {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      double* d = &sP[u >> 2][srow + 32 * (u & 3)][2 * sch];
+    for (int u = 0; u < NU; ++u) {
+      double* d = u < NUI ? &sP[0][srow + 32 * u][2 * sch] : &sP[1][srow + 32 * (u - NUI)][2 * sch];
       d[0] = pre[u].x;
       d[1] = pre[u].y;
     }
@@ -404,7 +547,7 @@ __global__ __launch_bounds__(256, 2) void syrk_kernel(double* __restrict__ A, in
 #pragma unroll
       for (int jr = 0; jr < 4; ++jr) bb[jr] = sP[1][wc + jr * 16 + li][kk + lk];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < IRN / 8; ++h) {
         double a[8];
 #pragma unroll
         for (int ir = 0; ir < 8; ++ir) a[ir] = -sP[0][wr + (h * 8 + ir) * 4 + l3][kk + lk];
@@ -420,10 +563,10 @@ __global__ __launch_bounds__(256, 2) void syrk_kernel(double* __restrict__ A, in
   int ld4s = ld4;
   asm volatile("" : "+v"(ld4s));  // recompute store addresses instead of keeping 64 pointers live
 #pragma unroll
-  for (int ir = 0; ir < 16; ++ir)
+  for (int ir = 0; ir < IRN; ++ir)
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) {
-      const int row = wr + ir * 4 + lk, col = wc + jr * 16 + li;
+      const int64_t row = i0 + wr + ir * 4 + lk, col = j0 + wc + jr * 16 + li;
       if (CIO && (!diag || col <= row)) Cb[ir * ld4s + jr * 16] = acc[ir][jr];
       if (!CIO && acc[ir][jr] == 1.2345e300) Cb[0] = 0.0;  // keep the MFMAs live
     }
@@ -490,15 +633,20 @@ struct Launcher {
     const int64_t rows = Mp - s;
     hipEvent_t ev;
     prof_begin(ctx, K_TRSM, &ev, st);
-    hipLaunchKernelGGL(trsm_kernel, dim3((unsigned)(rows / 64)), dim3(256), 0, st, A, lda, s,
-                       k * NB, ctx->linvT);
+    if (ctx->trsm_variant == 3)
+      hipLaunchKernelGGL(trsm_kernel_v3, dim3((unsigned)(rows / 32)), dim3(128), 0, st, A, lda, s,
+                         k * NB, ctx->linvT);
+    else
+      hipLaunchKernelGGL(trsm_kernel_v2, dim3((unsigned)(rows / 64)), dim3(256), 0, st, A, lda, s,
+                         k * NB, ctx->linvT);
     prof_end(ctx, K_TRSM, ev, (double)rows * NB * NB, 2.0 * rows * NB * 8, st);
   }
   // mode 0: all lower tiles of the trailing matrix after block column k; 1: next column; 2: rest
   void syrk(hipStream_t st, int64_t k, int64_t Mp, int mode) {
     const int64_t s = (k + 1) * NB;
     const int64_t T = (Mp - s) / ST;
-    int64_t tiles = mode == 1 ? T : (mode == 2 ? (T - 1) * T / 2 : T * (T + 1) / 2);
+    // the look-ahead column (mode 1) is on the critical path: 64-row tiles halve its latency
+    int64_t tiles = mode == 1 ? 2 * T : (mode == 2 ? (T - 1) * T / 2 : T * (T + 1) / 2);
     if (tiles <= 0) return;
     // algorithmic work of the updated lower elements (diagonal tiles count their lower half)
     double elems;
@@ -508,8 +656,12 @@ struct Launcher {
     else elems = (double)(Mp - s) * (double)(Mp - s + 1) / 2;
     hipEvent_t ev;
     prof_begin(ctx, K_SYRK, &ev, st);
-    hipLaunchKernelGGL((syrk_kernel<NB, true>), dim3((unsigned)tiles), dim3(256), 0, st, A, lda, s,
-                       k * NB, mode);
+    if (mode == 1)
+      hipLaunchKernelGGL((syrk_kernel<NB, true, 64>), dim3((unsigned)tiles), dim3(256), 0, st, A,
+                         lda, s, k * NB, mode);
+    else
+      hipLaunchKernelGGL((syrk_kernel<NB, true, 128>), dim3((unsigned)tiles), dim3(256), 0, st, A,
+                         lda, s, k * NB, mode);
     prof_end(ctx, K_SYRK, ev, elems * 2.0 * NB, elems * 16.0, st);
   }
 };
@@ -558,10 +710,10 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const unsigned tiles = (unsigned)((int64_t)T * (T + 1) / 2);
   hipStream_t st = ctx->stream;
   auto go = [&]() {
-    if (kd == 256 && cio) hipLaunchKernelGGL((syrk_kernel<256, true>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
-    else if (kd == 256) hipLaunchKernelGGL((syrk_kernel<256, false>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
-    else if (cio) hipLaunchKernelGGL((syrk_kernel<128, true>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
-    else hipLaunchKernelGGL((syrk_kernel<128, false>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
+    if (kd == 256 && cio) hipLaunchKernelGGL((syrk_kernel<256, true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
+    else if (kd == 256) hipLaunchKernelGGL((syrk_kernel<256, false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
+    else if (cio) hipLaunchKernelGGL((syrk_kernel<128, true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
+    else hipLaunchKernelGGL((syrk_kernel<128, false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
   };
   go();
   hipEvent_t a, b;
@@ -577,6 +729,35 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   hipEventDestroy(b);
   *us = ms * 1e3 / reps;
   return hip_fail(ctx, e, "probe_syrk");
+}
+
+// Diagnostic: average duration (us) of one panel solve over `rows` rows (multiple of 64)
+// below a unit diagonal block, variant 2 or 3.
+int probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us) {
+  const int64_t n = NB + rows;
+  int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
+  if (r) return r;
+  hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8, ctx->stream);
+  hipMemsetAsync(ctx->linvT, 0, NB * NB * 8, ctx->stream);
+  hipStream_t st = ctx->stream;
+  const int saved = ctx->trsm_variant;
+  ctx->trsm_variant = variant;
+  Launcher L{ctx, ctx->A, n};
+  L.trsm(st, 0, n);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a, st);
+  for (int i = 0; i < reps; ++i) L.trsm(st, 0, n);
+  hipEventRecord(b, st);
+  hipError_t e = hipStreamSynchronize(st);
+  ctx->trsm_variant = saved;
+  float ms = 0;
+  hipEventElapsedTime(&ms, a, b);
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  *us = ms * 1e3 / reps;
+  return hip_fail(ctx, e, "probe_trsm");
 }
 
 int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,

@@ -54,6 +54,7 @@ struct lfm_ctx {
   hipStream_t stream = nullptr;  // main stream: gram fill, bulk trailing updates, finalize
   hipStream_t side = nullptr;    // high-priority look-ahead stream: panel factor + solve
   bool lookahead = true;
+  int trsm_variant = 2;          // panel-solve kernel variant (LFM_TRSM=2|3)
   std::vector<hipEvent_t> evs;   // cross-stream dependency events (timing disabled)
   std::string err;
   int nb = 128;  // Cholesky block size
@@ -171,6 +172,7 @@ int probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double*
 int probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d);
 int probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us);
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us);
+int probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us);
 int probe_mfma4_layout(lfm_ctx* ctx, const double* a, const double* b, const double* c,
                        double* d);
 int probe_rates(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflops);

@@ -174,6 +174,8 @@ int lfm_probe_rate(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflo
 /* Trailing-update kernel alone on a T x T grid of 128-tiles, depth kd (128 | 256),
  * cio = 0 skips the C tile read/write: average us/launch. */
 int lfm_probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us);
+/* Panel-solve kernel alone (variant 2 | 3) over `rows` rows: average us/launch. */
+int lfm_probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us);
 /* Diagonal-block factor kernel with phase mask (bit0 register factor, bit1 panel,
  * bit2 trailing update, bit3 HBM load/store; 15 = product kernel): average us/launch. */
 int lfm_probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us);

@@ -1,0 +1,88 @@
+"""Turn one round's rocprofv3 output (gpurun_out/prof_trace, prof_fetch, prof_write) into the
+committed summaries under profiles/:
+
+  profiles/<round>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (as produced)
+  profiles/<round>_kernels.md         per-kernel table: calls, avg / total us, share
+  profiles/<round>_hbm.json           per-kernel FETCH_SIZE / WRITE_SIZE per launch
+  profiles/syrk_traffic.json          SYRK HBM bytes per launch (read by bench.py)
+
+HBM accounting follows MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB;
+FETCH_SIZE reads half of the bytes of a wide (16 B/lane) coalesced stream on gfx950, so
+the read side is reported raw and x2-corrected; WRITE_SIZE is exact for 16-B stores and
+uncalibrated for 8-B stores (the SYRK's C stores are 8 B/lane, 128-B rows per 16 lanes).
+
+    python scripts/summarize_profile.py r01 [bench_json]
+"""
+
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+PROF = os.path.join(ROOT, "profiles")
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("lfm::", "")
+
+
+def main():
+    rnd = sys.argv[1]
+    os.makedirs(PROF, exist_ok=True)
+    stats = os.path.join(OUT, "prof_trace", "run_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(PROF, f"{rnd}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats)))
+    lines = [f"# {rnd}: rocprofv3 --kernel-trace --stats, `bench.py --steps 3 --warmup 1` "
+             "(4 evaluations at N = 16384)", "",
+             "| kernel | calls | avg us | total ms | share % |", "|---|---|---|---|---|"]
+    for r in rows:
+        lines.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
+                     f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.2f} |")
+    hbm = defaultdict(lambda: {"launches": 0, "FETCH_SIZE_KiB": 0.0, "WRITE_SIZE_KiB": 0.0})
+    for counter, sub in (("FETCH_SIZE", "prof_fetch"), ("WRITE_SIZE", "prof_write")):
+        path = os.path.join(OUT, sub, "run_counter_collection.csv")
+        if not os.path.exists(path):
+            continue
+        seen = defaultdict(set)
+        for r in csv.DictReader(open(path)):
+            if r["Counter_Name"] != counter:
+                continue
+            k = short(r["Kernel_Name"])
+            hbm[k][counter + "_KiB"] += float(r["Counter_Value"])
+            seen[k].add(r["Dispatch_Id"])
+        for k, s in seen.items():
+            hbm[k]["launches"] = max(hbm[k]["launches"], len(s))
+    out = {}
+    for k, v in hbm.items():
+        n = max(1, v["launches"])
+        f = v["FETCH_SIZE_KiB"] * 1024 / n
+        w = v["WRITE_SIZE_KiB"] * 1024 / n
+        out[k] = {"launches": v["launches"], "fetch_bytes_per_launch_raw": f,
+                  "fetch_bytes_per_launch_x2": 2 * f, "write_bytes_per_launch": w,
+                  "hbm_bytes_per_launch": 2 * f + w}
+    json.dump(out, open(os.path.join(PROF, f"{rnd}_hbm.json"), "w"), indent=1)
+    if "syrk_kernel" in out:
+        s = out["syrk_kernel"]
+        json.dump({"round": rnd, "source": f"profiles/{rnd}_hbm.json (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                   "hbm_bytes_per_launch": s["hbm_bytes_per_launch"],
+                   "launches": s["launches"]},
+                  open(os.path.join(PROF, "syrk_traffic.json"), "w"), indent=1)
+    lines += ["", "HBM per launch (PMC, separate passes; read side x2 per MI355X_MICROARCH.md §HBM):",
+              "", "| kernel | launches | read B/launch (x2) | write B/launch |", "|---|---|---|---|"]
+    for k, v in sorted(out.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"]):
+        lines.append(f"| {k} | {v['launches']} | {v['fetch_bytes_per_launch_x2']:.3e} | "
+                     f"{v['write_bytes_per_launch']:.3e} |")
+    if len(sys.argv) > 2 and os.path.exists(sys.argv[2]):
+        b = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
+        shutil.copy(sys.argv[2], os.path.join(PROF, f"{rnd}_bench.json"))
+        lines += ["", f"bench.py: {b['value']:.3f} {b['unit']}, {b['ms_per_step']:.2f} ms/eval"]
+    open(os.path.join(PROF, f"{rnd}_kernels.md"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
