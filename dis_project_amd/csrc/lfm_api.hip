@@ -920,7 +920,7 @@ int lfm_probe_rate(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflo
 }
 
 int lfm_probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
-  if (!ctx || !us || T < 1 || reps < 1 || (kd != 128 && kd != 256)) return LFM_E_ARG;
+  if (!ctx || !us || T < 1 || reps < 1 || kd < 16 || kd > 512 || kd % 16) return LFM_E_ARG;
   DeviceGuard g(ctx->device);
   return probe_syrk(ctx, T, kd, cio, reps, us);
 }

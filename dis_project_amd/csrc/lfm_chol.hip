@@ -27,7 +27,10 @@
 // the main stream runs syrk(rest) of step k, so the latency-bound panel work of step k+1
 // hides behind the bulk of step k's trailing update.
 // finalize_kernel reduces logdet + ||z||^2 to the scalar MLL.
+#include <algorithm>
 #include <climits>
+#include <cstdlib>
+#include <utility>
 
 #include "lfm_math.h"
 
@@ -475,30 +478,37 @@ __global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, in
 // 2: every lower tile with tile column >= 1 (the rest).
 // KD: depth of the update (columns kb .. kb+KD of A). CIO = false (diagnostics only) skips
 // the C tile's HBM read and write.
-template <int KD, bool CIO, int TR>
+// Lower tiles (tile row ti >= tile column tj, 128-wide tile columns) of the trailing matrix
+// starting at row/column s, restricted to tile columns [tj_lo, tj_hi); T tile rows in all.
+// Bands of at most 8 columns (look-ahead / in-panel updates) are enumerated column by
+// column; otherwise tj_hi must be T and the band is a triangle. Update depth kd (multiple
+// of KB): columns kb .. kb + kd of A. TR = tile rows (128, or 64 for latency-critical bands).
+template <bool CIO, int TR>
 __global__ __launch_bounds__(256, 2) void syrk_kernel(double* __restrict__ A, int64_t lda,
-                                                      int64_t s, int64_t kb, int mode) {
-  // TR = tile rows (128, or 64 for the latency-critical look-ahead column); 128 columns.
+                                                      int64_t s, int64_t kb, int kd, int T,
+                                                      int tj_lo, int tj_hi) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
   __shared__ double sP[2][ST][KB + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
   const int li = lane & 15, lk = lane >> 4, l3 = lane & 3;
 
-  const int64_t b = blockIdx.x;
-  int ti, tj;
-  if (mode == 1) {
-    ti = (int)b;
-    tj = 0;
-  } else {
-    ti = (int)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
-    while ((int64_t)(ti + 1) * (ti + 2) / 2 <= b) ++ti;
-    while ((int64_t)ti * (ti + 1) / 2 > b) --ti;
-    tj = (int)(b - (int64_t)ti * (ti + 1) / 2);
-    if (mode == 2) {
-      ++ti;
+  constexpr int SUB = ST / TR;  // row tiles per 128 rows
+  int64_t b = blockIdx.x;
+  int ti, tj;  // ti in TR-row units
+  if (tj_hi - tj_lo <= 8) {
+    tj = tj_lo;
+    while (b >= (int64_t)SUB * (T - tj)) {
+      b -= (int64_t)SUB * (T - tj);
       ++tj;
     }
+    ti = SUB * tj + (int)b;
+  } else {
+    int a = (int)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
+    while ((int64_t)(a + 1) * (a + 2) / 2 <= b) ++a;
+    while ((int64_t)a * (a + 1) / 2 > b) --a;
+    tj = (int)(b - (int64_t)a * (a + 1) / 2) + tj_lo;
+    ti = SUB * (a + tj_lo);
   }
   const int64_t i0 = s + (int64_t)ti * TR, j0 = s + (int64_t)tj * ST;
   const bool diag = i0 < j0 + ST;  // the tile reaches the diagonal: keep col <= row only
@@ -536,11 +546,11 @@ __global__ __launch_bounds__(256, 2) void syrk_kernel(double* __restrict__ A, in
   };
 
   gload(0);
-  for (int k0 = 0; k0 < KD; k0 += KB) {
+  for (int k0 = 0; k0 < kd; k0 += KB) {
     __syncthreads();
     lstore();
     __syncthreads();
-    if (k0 + KB < KD) gload(k0 + KB);
+    if (k0 + KB < kd) gload(k0 + KB);
 #pragma unroll 1
     for (int kk = 0; kk < KB; kk += 4) {
       double bb[4];
@@ -641,30 +651,49 @@ struct Launcher {
                          k * NB, ctx->linvT);
     prof_end(ctx, K_TRSM, ev, (double)rows * NB * NB, 2.0 * rows * NB * 8, st);
   }
-  // mode 0: all lower tiles of the trailing matrix after block column k; 1: next column; 2: rest
-  void syrk(hipStream_t st, int64_t k, int64_t Mp, int mode) {
-    const int64_t s = (k + 1) * NB;
-    const int64_t T = (Mp - s) / ST;
-    // the look-ahead column (mode 1) is on the critical path: 64-row tiles halve its latency
-    int64_t tiles = mode == 1 ? 2 * T : (mode == 2 ? (T - 1) * T / 2 : T * (T + 1) / 2);
-    if (tiles <= 0) return;
-    // algorithmic work of the updated lower elements (diagonal tiles count their lower half)
-    double elems;
-    const double t = (double)ST;
-    if (mode == 1) elems = (double)(T - 1) * t * t + t * (t + 1) / 2;
-    else if (mode == 2) elems = (double)(T - 1) * (T - 2) / 2 * t * t + (double)(T - 1) * t * (t + 1) / 2;
-    else elems = (double)(Mp - s) * (double)(Mp - s + 1) / 2;
+  // Trailing update of tile columns [lo, hi) of the matrix starting at s0 (T = 128-tiles)
+  // with panel columns kb .. kb + kd. tr = 64 (latency-critical narrow bands) or 128.
+  void syrk(hipStream_t st, int64_t s0, int64_t kb, int kd, int64_t T, int lo, int hi, int tr) {
+    if (T <= 0 || hi <= lo) return;
+    hi = (int)std::min<int64_t>(hi, T);
+    const bool band = hi - lo <= 8;
+    if (!band && (hi != T || tr != 128)) { hi = (int)T; tr = 128; }
+    const int sub = ST / tr;
+    int64_t tiles = 0;
+    double elems = 0;
+    for (int tj = lo; tj < hi; ++tj) {
+      tiles += (int64_t)sub * (T - tj);
+      elems += (double)(T - tj - 1) * ST * ST + (double)ST * (ST + 1) / 2;
+    }
+    if (!band) tiles = (T - lo) * (T - lo + 1) / 2;
     hipEvent_t ev;
     prof_begin(ctx, K_SYRK, &ev, st);
-    if (mode == 1)
-      hipLaunchKernelGGL((syrk_kernel<NB, true, 64>), dim3((unsigned)tiles), dim3(256), 0, st, A,
-                         lda, s, k * NB, mode);
+    if (tr == 64)
+      hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3((unsigned)tiles), dim3(256), 0, st, A, lda,
+                         s0, kb, kd, (int)T, lo, hi);
     else
-      hipLaunchKernelGGL((syrk_kernel<NB, true, 128>), dim3((unsigned)tiles), dim3(256), 0, st, A,
-                         lda, s, k * NB, mode);
-    prof_end(ctx, K_SYRK, ev, elems * 2.0 * NB, elems * 16.0, st);
+      hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3((unsigned)tiles), dim3(256), 0, st, A,
+                         lda, s0, kb, kd, (int)T, lo, hi);
+    prof_end(ctx, K_SYRK, ev, elems * 2.0 * kd, elems * 16.0, st);
+  }
+  // Factor the super-panel of block columns [k, k + w): per column potrf + trsm, then the
+  // update of the super-panel's remaining columns with it (K = 128).
+  void superpanel(hipStream_t st, int64_t k, int w, int64_t n, int64_t Mp) {
+    for (int i = 0; i < w; ++i) {
+      potrf(st, k + i, n);
+      trsm(st, k + i, Mp);
+      if (i + 1 < w) {
+        const int64_t s0 = (k + i + 1) * NB;
+        syrk(st, s0, (k + i) * NB, NB, (Mp - s0) / ST, 0, w - 1 - i, 64);
+      }
+    }
   }
 };
+
+int env_int(const char* name, int def) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : def;
+}
 }  // namespace
 
 // Diagnostic: average duration (us) of the diagonal-block kernel with phase mask `mask`
@@ -703,17 +732,19 @@ int probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us) {
 // Diagnostic: average duration (us) of one full-lower-triangle SYRK launch over a T x T grid
 // of 128-tiles with update depth kd (128 or 256); cio = 0 skips the C tile I/O.
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
-  const int64_t n = (int64_t)T * ST + 256;
+  const int64_t n = (int64_t)T * ST + 512;
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
   if (r) return r;
   hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8, ctx->stream);
   const unsigned tiles = (unsigned)((int64_t)T * (T + 1) / 2);
   hipStream_t st = ctx->stream;
   auto go = [&]() {
-    if (kd == 256 && cio) hipLaunchKernelGGL((syrk_kernel<256, true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
-    else if (kd == 256) hipLaunchKernelGGL((syrk_kernel<256, false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
-    else if (cio) hipLaunchKernelGGL((syrk_kernel<128, true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
-    else hipLaunchKernelGGL((syrk_kernel<128, false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n, (int64_t)256, (int64_t)0, 0);
+    if (cio)
+      hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
+                         (int64_t)512, (int64_t)0, kd, T, 0, T);
+    else
+      hipLaunchKernelGGL((syrk_kernel<false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
+                         (int64_t)512, (int64_t)0, kd, T, 0, T);
   };
   go();
   hipEvent_t a, b;
@@ -765,37 +796,58 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   const int64_t npb = (n + NB - 1) / NB;  // block columns that hold pivots
   int r = ensure(ctx, (void**)&ctx->parts, &ctx->parts_cap, (size_t)npb * sizeof(double));
   if (r) return r;
-  r = ensure_events(ctx, 2 * (size_t)npb + 2);
+  // step plan: super-panels of w = 4, 2 or 1 block columns while the trailing matrix is
+  // large, so the bulk trailing update runs with depth 128 w (C traffic per flop / w)
+  const int64_t w4min = env_int("LFM_W4_MIN", 6144), w2min = env_int("LFM_W2_MIN", 4096);
+  std::vector<std::pair<int64_t, int>> steps;
+  for (int64_t k = 0; k < npb;) {
+    const int64_t m = Mp - k * NB;
+    int w = 1;
+    if (m >= w4min && k + 4 <= npb) w = 4;
+    else if (m >= w2min && k + 2 <= npb) w = 2;
+    steps.emplace_back(k, w);
+    k += w;
+  }
+  const int S = (int)steps.size();
+  r = ensure_events(ctx, 2 * (size_t)S + 2);
   if (r) return r;
   hipStream_t main = ctx->stream, side = ctx->side;
-  hipEvent_t* ev = ctx->evs.data();  // [0]: inputs ready; 1+2k: E1_k (trsm k); 2+2k: E2_k
+  hipEvent_t* ev = ctx->evs.data();  // [0]: inputs ready; E1_s = ev[1 + 2s]; E2_s = ev[2 + 2s]
   Launcher L{ctx, A, lda};
   hipLaunchKernelGGL(status_init_kernel, dim3(1), dim3(1), 0, main, ctx->status);
   if (!ctx->lookahead) {
-    for (int64_t k = 0; k < npb; ++k) {
-      L.potrf(main, k, n);
-      L.trsm(main, k, Mp);
-      if (k + 1 < npb) L.syrk(main, k, Mp, 0);
+    for (int s = 0; s < S; ++s) {
+      const int64_t k = steps[s].first;
+      const int w = steps[s].second;
+      L.superpanel(main, k, w, n, Mp);
+      const int64_t s0 = (k + w) * NB;
+      const int64_t T = (Mp - s0) / ST;
+      if (k + w < npb) L.syrk(main, s0, k * NB, NB * w, T, 0, (int)T, 128);
     }
   } else {
     hipEventRecord(ev[0], main);
     hipStreamWaitEvent(side, ev[0], 0);
-    L.potrf(side, 0, n);
-    L.trsm(side, 0, Mp);
+    L.superpanel(side, steps[0].first, steps[0].second, n, Mp);
     hipEventRecord(ev[1], side);
-    for (int64_t k = 0; k + 1 < npb; ++k) {
-      // main: the bulk of step k's trailing update, once panel k is solved
-      hipStreamWaitEvent(main, ev[1 + 2 * k], 0);
-      L.syrk(main, k, Mp, 2);
-      hipEventRecord(ev[2 + 2 * k], main);
-      // side: block column k+1 first, then its factor and panel solve
-      if (k > 0) hipStreamWaitEvent(side, ev[2 + 2 * (k - 1)], 0);
-      L.syrk(side, k, Mp, 1);
-      L.potrf(side, k + 1, n);
-      L.trsm(side, k + 1, Mp);
-      hipEventRecord(ev[1 + 2 * (k + 1)], side);
+    for (int s = 0; s < S; ++s) {
+      const int64_t k = steps[s].first;
+      const int w = steps[s].second;
+      const int wn = s + 1 < S ? steps[s + 1].second : 0;
+      const int64_t s0 = (k + w) * NB;
+      const int64_t T = (Mp - s0) / ST;
+      // main: the bulk of step s's trailing update (tile columns >= wn), depth 128 w
+      hipStreamWaitEvent(main, ev[1 + 2 * s], 0);
+      if (s + 1 < S) L.syrk(main, s0, k * NB, NB * w, T, wn, (int)T, 128);
+      hipEventRecord(ev[2 + 2 * s], main);
+      if (s + 1 < S) {
+        // side: the next super-panel's columns first (after main's previous bulk update),
+        // then its factorisation
+        if (s > 0) hipStreamWaitEvent(side, ev[2 + 2 * (s - 1)], 0);
+        L.syrk(side, s0, k * NB, NB * w, T, 0, wn, 64);
+        L.superpanel(side, steps[s + 1].first, steps[s + 1].second, n, Mp);
+        hipEventRecord(ev[1 + 2 * (s + 1)], side);
+      }
     }
-    hipStreamWaitEvent(main, ev[1 + 2 * (npb - 1)], 0);
   }
   r = hip_fail(ctx, hipGetLastError(), "cholesky launch");
   if (r) return r;

@@ -7,8 +7,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dis_project_amd import _lib  # noqa: E402
 
 ctx = _lib.get_context(0)
-for T in (128, 64, 32):
-    for kd in (128, 256):
+for T in (126, 64, 32):
+    for kd in (128, 256, 512):
         for cio in (1, 0):
             us = _lib.c_double()
             ctx.check(ctx.lib.lfm_probe_syrk(ctx.handle, T, kd, cio, 5, _lib.ctypes.byref(us)))
