@@ -21,7 +21,7 @@ namespace lfm {
 const char* const kClassName[K_NCLASS] = {"tables",   "gram_grid", "gram_direct",
                                           "augment",  "potrf",     "trsm",
                                           "syrk",     "finalize",  "small_mll",
-                                          "mean"};
+                                          "mean",     "grad"};
 
 int set_err(lfm_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;
@@ -642,6 +642,72 @@ int lfm_mll_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n, const
   hipMemcpyAsync(ctx->xin, x, n * 3 * 8, hipMemcpyHostToDevice, ctx->stream);
   hipMemcpyAsync(ctx->xin + 3 * n, y, n * 8, hipMemcpyHostToDevice, ctx->stream);
   return mll_blocked(ctx, st, ctx->xin, ctx->xin + 3 * n, nullptr, n, hyp, negative, out);
+}
+
+int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
+                     const lfm_hyp* hyp, int negative, double* value, double* grad) {
+  int r = validate_x(ctx, x, n);
+  if (r) return r;
+  if (!y || !value || !grad) return set_err(ctx, LFM_E_ARG, "y / value / grad is NULL");
+  r = check_hyp(ctx, hyp);
+  if (r) return r;
+  r = check_mean_shape(ctx, n, hyp);
+  if (r) return r;
+  DeviceGuard g(ctx->device);
+  Staged st;
+  r = stage_hyp(ctx, hyp, x, n, true, &st);
+  if (r) return r;
+  r = ensure(ctx, (void**)&ctx->xin, &ctx->xin_bytes, (size_t)n * 4 * 8);
+  if (r) return r;
+  const double* d_x = ctx->xin;
+  const double* d_y = ctx->xin + 3 * n;
+  hipMemcpyAsync(ctx->xin, x, n * 3 * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipMemcpyAsync(ctx->xin + 3 * n, y, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  // bordered 2Mp x 2Mp matrix [[S_aug, .], [I, 0]] (lfm_grad.hip)
+  const int64_t Mp = round_up(n + 1, 128), M2 = 2 * Mp;
+  r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)M2 * M2 * sizeof(double));
+  if (r) return r;
+  const int64_t G = hyp->num_genes;
+  r = ensure(ctx, (void**)&ctx->gacc, &ctx->gacc_bytes, (size_t)(5 * G + 3) * sizeof(double));
+  if (r) return r;
+  const double noise = hyp->obs_stddev * hyp->obs_stddev;  // objectives.py:66
+  if (st.lay.ok) {
+    r = ensure(ctx, (void**)&ctx->tab, &ctx->tab_bytes,
+               tables_doubles(st.h.G, st.lay.T) * sizeof(double));
+    if (r) return r;
+    r = launch_tables(ctx, st.h, st.lay, st.d_times, ctx->tab);
+    if (r) return r;
+    r = launch_gram_grid<double>(ctx, st.h, st.lay, ctx->tab, st.d_bg, n, hyp->jitter, noise,
+                                 LFM_UPLO_LOWER, ctx->A, M2);
+  } else {
+    r = launch_gram_direct<double>(ctx, st.h, d_x, n, d_x, n, hyp->jitter, noise,
+                                   LFM_UPLO_LOWER, ctx->A, M2);
+  }
+  if (r) return r;
+  r = launch_augment(ctx, st.h, d_x, d_y, nullptr, n, ctx->A, M2, Mp);
+  if (r) return r;
+  r = launch_border_init(ctx, ctx->A, M2, Mp);
+  if (r) return r;
+  r = chol_factor_solve(ctx, ctx->A, M2, n, Mp, negative, ctx->result, 1);
+  if (r) return r;
+  double* d_out = ctx->gacc + 2 * G + 1;
+  r = launch_grad(ctx, st.h, d_x, n, ctx->A, M2, Mp, hyp->obs_stddev, negative, ctx->gacc, d_out);
+  if (r) return r;
+  const size_t ng = (size_t)(3 * G + 2);
+  r = ensure_pinned(ctx, (ng + 16) * sizeof(double));
+  if (r) return r;
+  double* hres = ctx->hpin;
+  hipMemcpyAsync(hres, ctx->result, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+  hipMemcpyAsync(hres + 8, d_out, ng * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+  r = finish(ctx);
+  if (r) return r;
+  *value = hres[0];
+  std::memcpy(grad, hres + 8, ng * sizeof(double));
+  if ((int)hres[3] != INT_MAX)
+    return set_err(ctx, LFM_E_NOT_PD,
+                   "Cholesky failed: non-positive pivot at index " +
+                       std::to_string((long long)hres[3]));
+  return LFM_OK;
 }
 
 int lfm_mll_f64_dev(lfm_ctx* ctx, const double* d_x, const double* d_y, int64_t n,

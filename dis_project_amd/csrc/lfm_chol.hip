@@ -630,6 +630,9 @@ struct Launcher {
   lfm_ctx* ctx;
   double* A;
   int64_t lda;
+  int64_t Mp;   // rows of the (augmented) matrix being factored
+  int64_t win;  // 0: trailing rows run to Mp; > 0: rows [s, s + win) only (bordered inverse)
+  int64_t end(int64_t s) const { return win ? s + win : Mp; }
   void potrf(hipStream_t st, int64_t k, int64_t n) {
     hipEvent_t ev;
     prof_begin(ctx, K_POTRF, &ev, st);
@@ -637,10 +640,10 @@ struct Launcher {
                        ctx->linvT, ctx->parts, (int)k, ctx->status);
     prof_end(ctx, K_POTRF, ev, (double)NB * NB * NB / 3.0, 0, st);
   }
-  void trsm(hipStream_t st, int64_t k, int64_t Mp) {
+  void trsm(hipStream_t st, int64_t k) {
     const int64_t s = (k + 1) * NB;
-    if (s >= Mp) return;
-    const int64_t rows = Mp - s;
+    const int64_t rows = end(s) - s;
+    if (rows <= 0) return;
     hipEvent_t ev;
     prof_begin(ctx, K_TRSM, &ev, st);
     if (ctx->trsm_variant == 3)
@@ -676,15 +679,16 @@ struct Launcher {
                          lda, s0, kb, kd, (int)T, lo, hi);
     prof_end(ctx, K_SYRK, ev, elems * 2.0 * kd, elems * 16.0, st);
   }
+  int64_t tiles_from(int64_t s0) const { return (end(s0) - s0) / ST; }
   // Factor the super-panel of block columns [k, k + w): per column potrf + trsm, then the
   // update of the super-panel's remaining columns with it (K = 128).
-  void superpanel(hipStream_t st, int64_t k, int w, int64_t n, int64_t Mp) {
+  void superpanel(hipStream_t st, int64_t k, int w, int64_t n) {
     for (int i = 0; i < w; ++i) {
       potrf(st, k + i, n);
-      trsm(st, k + i, Mp);
+      trsm(st, k + i);
       if (i + 1 < w) {
         const int64_t s0 = (k + i + 1) * NB;
-        syrk(st, s0, (k + i) * NB, NB, (Mp - s0) / ST, 0, w - 1 - i, 64);
+        syrk(st, s0, (k + i) * NB, NB, tiles_from(s0), 0, w - 1 - i, 64);
       }
     }
   }
@@ -773,13 +777,13 @@ int probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us) {
   hipStream_t st = ctx->stream;
   const int saved = ctx->trsm_variant;
   ctx->trsm_variant = variant;
-  Launcher L{ctx, ctx->A, n};
-  L.trsm(st, 0, n);
+  Launcher L{ctx, ctx->A, n, n, 0};
+  L.trsm(st, 0);
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
   hipEventRecord(a, st);
-  for (int i = 0; i < reps; ++i) L.trsm(st, 0, n);
+  for (int i = 0; i < reps; ++i) L.trsm(st, 0);
   hipEventRecord(b, st);
   hipError_t e = hipStreamSynchronize(st);
   ctx->trsm_variant = saved;
@@ -792,19 +796,26 @@ int probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us) {
 }
 
 int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,
-                      double* d_out) {
+                      double* d_out, int64_t bordered) {
+  // bordered = 0: factor the Mp x Mp augmented matrix (block columns holding pivots only).
+  // bordered = 1: A is 2Mp x 2Mp, [[S_aug, .], [I, 0]]; all Mp/NB block columns of the top
+  // are eliminated with every trailing update restricted to the Mp-row window below the
+  // panel (the rows the identity border has reached), leaving -S_aug^{-1} in the bottom
+  // block: a Cholesky + triangular inverse + L^-T L^-1 product in N^3 flops on the same
+  // three kernels.
   const int64_t npb = (n + NB - 1) / NB;  // block columns that hold pivots
-  int r = ensure(ctx, (void**)&ctx->parts, &ctx->parts_cap, (size_t)npb * sizeof(double));
+  const int64_t nblk = bordered ? Mp / NB : npb;
+  int r = ensure(ctx, (void**)&ctx->parts, &ctx->parts_cap, (size_t)nblk * sizeof(double));
   if (r) return r;
   // step plan: super-panels of w = 4, 2 or 1 block columns while the trailing matrix is
   // large, so the bulk trailing update runs with depth 128 w (C traffic per flop / w)
   const int64_t w4min = env_int("LFM_W4_MIN", 6144), w2min = env_int("LFM_W2_MIN", 4096);
   std::vector<std::pair<int64_t, int>> steps;
-  for (int64_t k = 0; k < npb;) {
-    const int64_t m = Mp - k * NB;
+  for (int64_t k = 0; k < nblk;) {
+    const int64_t m = bordered ? Mp + NB : Mp - k * NB;
     int w = 1;
-    if (m >= w4min && k + 4 <= npb) w = 4;
-    else if (m >= w2min && k + 2 <= npb) w = 2;
+    if (m >= w4min && k + 4 <= nblk) w = 4;
+    else if (m >= w2min && k + 2 <= nblk) w = 2;
     steps.emplace_back(k, w);
     k += w;
   }
@@ -813,38 +824,39 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   if (r) return r;
   hipStream_t main = ctx->stream, side = ctx->side;
   hipEvent_t* ev = ctx->evs.data();  // [0]: inputs ready; E1_s = ev[1 + 2s]; E2_s = ev[2 + 2s]
-  Launcher L{ctx, A, lda};
+  Launcher L{ctx, A, lda, bordered ? 2 * Mp : Mp, bordered ? Mp : 0};
   hipLaunchKernelGGL(status_init_kernel, dim3(1), dim3(1), 0, main, ctx->status);
+  // the trailing update after the last super-panel matters only for the bordered rows
+  auto trailing = [&](int s) { return s + 1 < S || bordered; };
   if (!ctx->lookahead) {
     for (int s = 0; s < S; ++s) {
       const int64_t k = steps[s].first;
       const int w = steps[s].second;
-      L.superpanel(main, k, w, n, Mp);
+      L.superpanel(main, k, w, n);
       const int64_t s0 = (k + w) * NB;
-      const int64_t T = (Mp - s0) / ST;
-      if (k + w < npb) L.syrk(main, s0, k * NB, NB * w, T, 0, (int)T, 128);
+      if (trailing(s)) L.syrk(main, s0, k * NB, NB * w, L.tiles_from(s0), 0, INT_MAX, 128);
     }
   } else {
     hipEventRecord(ev[0], main);
     hipStreamWaitEvent(side, ev[0], 0);
-    L.superpanel(side, steps[0].first, steps[0].second, n, Mp);
+    L.superpanel(side, steps[0].first, steps[0].second, n);
     hipEventRecord(ev[1], side);
     for (int s = 0; s < S; ++s) {
       const int64_t k = steps[s].first;
       const int w = steps[s].second;
       const int wn = s + 1 < S ? steps[s + 1].second : 0;
       const int64_t s0 = (k + w) * NB;
-      const int64_t T = (Mp - s0) / ST;
+      const int64_t T = L.tiles_from(s0);
       // main: the bulk of step s's trailing update (tile columns >= wn), depth 128 w
       hipStreamWaitEvent(main, ev[1 + 2 * s], 0);
-      if (s + 1 < S) L.syrk(main, s0, k * NB, NB * w, T, wn, (int)T, 128);
+      if (trailing(s)) L.syrk(main, s0, k * NB, NB * w, T, wn, (int)T, 128);
       hipEventRecord(ev[2 + 2 * s], main);
       if (s + 1 < S) {
         // side: the next super-panel's columns first (after main's previous bulk update),
         // then its factorisation
         if (s > 0) hipStreamWaitEvent(side, ev[2 + 2 * (s - 1)], 0);
         L.syrk(side, s0, k * NB, NB * w, T, 0, wn, 64);
-        L.superpanel(side, steps[s + 1].first, steps[s + 1].second, n, Mp);
+        L.superpanel(side, steps[s + 1].first, steps[s + 1].second, n);
         hipEventRecord(ev[1 + 2 * (s + 1)], side);
       }
     }

@@ -1,0 +1,291 @@
+// lfm_grad.hip — gradient of the log marginal likelihood on gfx950.
+//
+// What jax.value_and_grad(loss) computes at src/trainer.py:126 for
+// CustomConjMLL.step (src/objectives.py:21-78), before the bijectors' chain rule:
+//     d log N(y; m, S) / d theta = 1/2 tr(W dS/dtheta) + a^T dm/dtheta,
+//     a = S^{-1} r,  W = a a^T - S^{-1},  r = y - m,
+// for theta in true_d, true_s, true_b [G], l and obs_stddev (jitter is static, model.py:64).
+//
+// S^{-1} comes from the bordered factorisation (lfm_chol.hip, chol_factor_solve with
+// bordered = 1): the 2Mp x 2Mp matrix [[S_aug, .], [I, 0]] is eliminated through its first
+// Mp columns, which leaves -(L_aug^{-T} L_aug^{-1}) in the bottom block. With the residual
+// row n of the augmented factor (z = L^{-1} r, unit pivot) that block is
+//     Bt[i][j] = -(S^{-1} + a a^T)[i][j]   (i, j < n),     Bt[n][j] = a_j,
+// so W = Bt + 2 a a^T and a needs no extra solve.
+//
+// grad_pairs_kernel: one thread per column c of a 256-column x GR-row tile of the lower
+//   triangle; per pair the kernel value and its derivatives in (D_row, D_col, l) are
+//   evaluated with forward-mode duals on the cancellation-free erfc form of h
+//   (model.py:315-365, the identities of lfm_gram.hip), weighted by W (x 1/2 on the
+//   diagonal), and summed into per-gene accumulators (row gene: wave-uniform, flushed on
+//   change; column gene: flushed at the end). Bound: VALU (erfc / exp), ~20 special
+//   functions per pair; W is read once (8 B per pair).
+// grad_finish_kernel: tr(W), the mean terms of m_i = (B/D)[i // (n/G)] flag_i
+//   (model.py:124-149), the sign of CustomConjMLL(negative) and NaN on a failed factor.
+#include "lfm_math.h"
+
+namespace lfm {
+
+// ---------------------------------------------------------------- duals
+// Value and derivatives with respect to (D_row_gene, D_col_gene, l).
+struct Dual3 {
+  double v, a, b, c;
+};
+__device__ __forceinline__ Dual3 dconst(double v) { return {v, 0.0, 0.0, 0.0}; }
+__device__ __forceinline__ Dual3 operator+(Dual3 x, Dual3 y) {
+  return {x.v + y.v, x.a + y.a, x.b + y.b, x.c + y.c};
+}
+__device__ __forceinline__ Dual3 operator-(Dual3 x, Dual3 y) {
+  return {x.v - y.v, x.a - y.a, x.b - y.b, x.c - y.c};
+}
+__device__ __forceinline__ Dual3 operator*(Dual3 x, Dual3 y) {
+  return {x.v * y.v, x.a * y.v + x.v * y.a, x.b * y.v + x.v * y.b, x.c * y.v + x.v * y.c};
+}
+__device__ __forceinline__ Dual3 operator*(double s, Dual3 x) {
+  return {s * x.v, s * x.a, s * x.b, s * x.c};
+}
+__device__ __forceinline__ Dual3 operator/(Dual3 x, Dual3 y) {
+  const double iv = 1.0 / y.v, q = x.v * iv;
+  return {q, (x.a - q * y.a) * iv, (x.b - q * y.b) * iv, (x.c - q * y.c) * iv};
+}
+__device__ __forceinline__ Dual3 dexp(Dual3 x) {
+  const double e = exp(x.v);
+  return {e, e * x.a, e * x.b, e * x.c};
+}
+// e^{A} erfc(z) and its derivative e^{A} erfc(z) dA - (2/sqrt(pi)) e^{A - z^2} dz.
+__device__ __forceinline__ Dual3 dexp_erfc(Dual3 A, Dual3 z) {
+  const double ez = exp(A.v - z.v * z.v);
+  const double f = z.v > 0.0 ? erfcx(z.v) * ez : exp(A.v) * erfc(z.v);
+  const double g = 1.1283791670955125739 * ez;  // 2 / sqrt(pi)
+  return {f, f * A.a - g * z.a, f * A.b - g * z.b, f * A.c - g * z.c};
+}
+
+// (D_j + D_k) h(j, k, t1, t2) of model.py:343-363 in the erfc form:
+//   e^{g^2 - Dk d} (erfc(g - d/l) - erfc(t1/l + g))
+//   - e^{-(Dk t2 + Dj t1)} e^{g^2} (erfc(g - t2/l) - erfc(g)),   g = Dk l / 2, d = t2 - t1.
+__device__ __forceinline__ Dual3 h_bracket(Dual3 Dj, Dual3 Dk, Dual3 l, double t1, double t2) {
+  const Dual3 g = 0.5 * (Dk * l);
+  const Dual3 g2 = g * g;
+  const double d = t2 - t1;
+  const Dual3 il = dconst(1.0) / l;
+  const Dual3 A1 = g2 - d * Dk;
+  const Dual3 first = dexp_erfc(A1, g - d * il) - dexp_erfc(A1, t1 * il + g);
+  const Dual3 E = dexp(dconst(0.0) - (t2 * Dk + t1 * Dj));
+  const Dual3 Q = dexp_erfc(g2, g - t2 * il) - dexp_erfc(g2, g);
+  return first - E * Q;
+}
+
+// Derivative contributions of one pair: K and dK/d{D_row, D_col, l}, dK/dS_row, dK/dS_col.
+struct PairGrad {
+  double dDr, dDc, dl, dSr, dSc;
+};
+
+// kernel_xx (model.py:197-235): K = S_j S_k l sqrt(pi)/2 (h(k,j,tb,ta) + h(j,k,ta,tb)).
+__device__ __forceinline__ void kxx_grad(const HypDev& p, double ta, int j, double tb, int k,
+                                         double wgt, PairGrad& o) {
+  const Dual3 Dj{p.D[j], 1.0, 0.0, 0.0}, Dk{p.D[k], 0.0, 1.0, 0.0}, L{p.l, 0.0, 0.0, 1.0};
+  const Dual3 hs = h_bracket(Dj, Dk, L, ta, tb) + h_bracket(Dk, Dj, L, tb, ta);
+  const Dual3 u = (0.5 * kSqrtPi) * (L * hs / (Dj + Dk));
+  const double ss = p.S[j] * p.S[k];
+  o.dDr += wgt * ss * u.a;
+  o.dDc += wgt * ss * u.b;
+  o.dl += wgt * ss * u.c;
+  o.dSr += wgt * p.S[k] * u.v;
+  o.dSc += wgt * p.S[j] * u.v;
+}
+
+// kernel_xf (model.py:237-282) with the gene row's time tg, gene gg and the latent time tl:
+//   K = l sqrt(pi)/2 S_g e^{g^2 - D delta} (erfc(g - delta/l) - erfc(tl/l + g)).
+// gene_is_row selects which accumulator (row or column gene) receives dD and dS.
+__device__ __forceinline__ void kxf_grad(const HypDev& p, double tg, int g, double tl,
+                                         bool gene_is_row, double wgt, PairGrad& o) {
+  const Dual3 Dg{p.D[g], 1.0, 0.0, 0.0}, L{p.l, 0.0, 0.0, 1.0};
+  const Dual3 gm = 0.5 * (Dg * L);
+  const double d = tg - tl;
+  const Dual3 il = dconst(1.0) / L;
+  const Dual3 A = gm * gm - d * Dg;
+  const Dual3 br = dexp_erfc(A, gm - d * il) - dexp_erfc(A, tl * il + gm);
+  const Dual3 u = (0.5 * kSqrtPi) * (L * br);
+  const double s = p.S[g];
+  if (gene_is_row) {
+    o.dDr += wgt * s * u.a;
+    o.dSr += wgt * u.v;
+  } else {
+    o.dDc += wgt * s * u.a;
+    o.dSc += wgt * u.v;
+  }
+  o.dl += wgt * s * u.c;
+}
+
+// Flag-switched kernel derivatives (model.py:152-195), same branch selection as kernel_ref.
+__device__ __forceinline__ void kernel_grad(const HypDev& p, double ta, double ga, double fa,
+                                            double tb, double gb, double fb, double wgt,
+                                            PairGrad& o) {
+  const long long f1 = flag_int(fa), f2 = flag_int(fb);
+  const long long s_xx = f1 * f2, s_ff = (1 - f1) * (1 - f2);
+  const long long s_xf = f1 * (1 - f2), s_fx = (1 - f1) * f2;
+  const int j = gene_index(ga, p.G), k = gene_index(gb, p.G);
+  if (s_xx) kxx_grad(p, ta, j, tb, k, wgt * (double)s_xx, o);
+  if (s_ff) {
+    const double d = ta - tb;
+    const double q = (d * d) / (2.0 * p.l);
+    o.dl += wgt * (double)s_ff * exp(-q) * q / p.l;
+  }
+  // kxf_ref(p, ta, ga, fa, tb, gb): the row whose flag is 0.0 is the latent one
+  if (s_xf) {
+    const bool a_lat = (fa == 0.0);
+    kxf_grad(p, a_lat ? tb : ta, a_lat ? k : j, a_lat ? ta : tb, !a_lat, wgt * (double)s_xf, o);
+  }
+  if (s_fx) {
+    const bool b_lat = (fb == 0.0);
+    kxf_grad(p, b_lat ? ta : tb, b_lat ? j : k, b_lat ? tb : ta, b_lat, wgt * (double)s_fx, o);
+  }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// ---------------------------------------------------------------- kernels
+// Bottom rows of the bordered matrix: row Mp + i = e_i in the first Mp columns, 0 after.
+__global__ void border_init_kernel(double* __restrict__ A, int64_t lda, int64_t Mp) {
+  const int64_t i = blockIdx.y;
+  double* row = A + (Mp + i) * lda;
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c <= Mp + i;
+       c += (int64_t)gridDim.x * blockDim.x)
+    row[c] = (c == i) ? 1.0 : 0.0;
+}
+
+// acc layout: [0,G) dD  [G,2G) dS  [2G] dl   (kernel terms of 1/2 tr(W dK))
+constexpr int GR = 32;
+__global__ __launch_bounds__(256) void grad_pairs_kernel(HypDev p, const double* __restrict__ x,
+                                                         int64_t n, const double* __restrict__ Bt,
+                                                         int64_t ldb, const double* __restrict__ al,
+                                                         double* __restrict__ acc) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.y * GR;
+  if ((int64_t)blockIdx.x * 256 > r0 + GR - 1) return;  // tile entirely above the diagonal
+  const int lane = threadIdx.x & 63;
+  const int G = p.G;
+  const bool cv = c < n;
+  const int64_t cc = cv ? c : n - 1;
+  const double tb = x[cc * 3], gb = x[cc * 3 + 1], fb = x[cc * 3 + 2];
+  const int k = gene_index(gb, G);
+  const double ac = al[cc];
+  double cD = 0.0, cS = 0.0, rD = 0.0, rS = 0.0, sl = 0.0;
+  int jcur = -1;
+  const int64_t rend = min(r0 + GR, n);
+  for (int64_t i = r0; i < rend; ++i) {
+    const double ta = x[i * 3], ga = x[i * 3 + 1], fa = x[i * 3 + 2];
+    const int j = gene_index(ga, G);  // wave-uniform
+    if (j != jcur) {
+      if (jcur >= 0) {
+        const double sD = wave_sum(rD), sS = wave_sum(rS);
+        if (lane == 0) {
+          unsafeAtomicAdd(acc + jcur, sD);
+          unsafeAtomicAdd(acc + G + jcur, sS);
+        }
+      }
+      rD = rS = 0.0;
+      jcur = j;
+    }
+    if (!cv || c > i) continue;
+    double wgt = Bt[i * ldb + c] + 2.0 * al[i] * ac;
+    if (c == i) wgt *= 0.5;
+    PairGrad o{0.0, 0.0, 0.0, 0.0, 0.0};
+    kernel_grad(p, ta, ga, fa, tb, gb, fb, wgt, o);
+    rD += o.dDr;
+    rS += o.dSr;
+    cD += o.dDc;
+    cS += o.dSc;
+    sl += o.dl;
+  }
+  if (jcur >= 0) {
+    const double sD = wave_sum(rD), sS = wave_sum(rS);
+    if (lane == 0) {
+      unsafeAtomicAdd(acc + jcur, sD);
+      unsafeAtomicAdd(acc + G + jcur, sS);
+    }
+  }
+  const double s_l = wave_sum(sl);
+  if (lane == 0) unsafeAtomicAdd(acc + 2 * G, s_l);
+  // column genes: one atomic per wave when the wave's columns share a gene
+  const int k0 = __shfl(k, 0);
+  if (__all(k == k0)) {
+    const double sD = wave_sum(cD), sS = wave_sum(cS);
+    if (lane == 0) {
+      unsafeAtomicAdd(acc + k0, sD);
+      unsafeAtomicAdd(acc + G + k0, sS);
+    }
+  } else if (cv) {
+    unsafeAtomicAdd(acc + k, cD);
+    unsafeAtomicAdd(acc + G + k, cS);
+  }
+}
+
+// One workgroup: tr(W), mean terms, sign, NaN on a failed factor.
+// out: [0,G) d  [G,2G) s  [2G,3G) b  [3G] l  [3G+1] obs_stddev.
+__global__ __launch_bounds__(1024) void grad_finish_kernel(
+    HypDev p, const double* __restrict__ x, int64_t n, const double* __restrict__ Bt, int64_t ldb,
+    const double* __restrict__ al, const double* __restrict__ acc, double obs_stddev,
+    const double* __restrict__ result, int negative, double* __restrict__ out) {
+  __shared__ double red[16];
+  const int tid = threadIdx.x, G = p.G;
+  const bool failed = (int)result[3] != INT_MAX;
+  const double sign = negative ? -1.0 : 1.0;
+  double tr = 0.0;
+  for (int64_t i = tid; i < n; i += 1024) tr += Bt[i * ldb + i] + 2.0 * al[i] * al[i];
+  tr = wave_sum(tr);
+  if ((tid & 63) == 0) red[tid >> 6] = tr;
+  const int64_t bs = n / G;
+  for (int g = tid; g < G; g += 1024) {
+    double af = 0.0;  // sum over mean block g of a_i flag_i (model.py:145-149)
+    for (int64_t i = (int64_t)g * bs; i < (int64_t)(g + 1) * bs; ++i)
+      af += al[i] * (double)flag_int(x[i * 3 + 2]);
+    const double D = p.D[g], B = p.B[g];
+    const double gd = acc[g] - B / (D * D) * af;
+    const double nan = __builtin_nan("");
+    out[g] = failed ? nan : sign * gd;
+    out[G + g] = failed ? nan : sign * acc[G + g];
+    out[2 * G + g] = failed ? nan : sign * (af / D);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double t = 0.0;
+    for (int w = 0; w < 16; ++w) t += red[w];
+    const double nan = __builtin_nan("");
+    out[3 * G] = failed ? nan : sign * acc[2 * G];
+    out[3 * G + 1] = failed ? nan : sign * obs_stddev * t;
+  }
+}
+
+int launch_border_init(lfm_ctx* ctx, double* A, int64_t lda, int64_t Mp) {
+  hipEvent_t ev;
+  prof_begin(ctx, K_AUGMENT, &ev);
+  dim3 grid((unsigned)std::min<int64_t>((2 * Mp + 255) / 256, 64), (unsigned)Mp);
+  hipLaunchKernelGGL(border_init_kernel, grid, dim3(256), 0, ctx->stream, A, lda, Mp);
+  prof_end(ctx, K_AUGMENT, ev, 0, (double)Mp * Mp * 1.5 * 8);
+  return hip_fail(ctx, hipGetLastError(), "border_init_kernel");
+}
+
+int launch_grad(lfm_ctx* ctx, const HypDev& h, const double* d_x, int64_t n, const double* A,
+                int64_t lda, int64_t Mp, double obs_stddev, int negative, double* acc,
+                double* d_out) {
+  const double* Bt = A + Mp * lda + Mp;
+  const double* al = Bt + n * lda;
+  hipMemsetAsync(acc, 0, (size_t)(2 * h.G + 1) * sizeof(double), ctx->stream);
+  hipEvent_t ev;
+  prof_begin(ctx, K_GRAD, &ev);
+  dim3 grid((unsigned)((n + 255) / 256), (unsigned)((n + GR - 1) / GR));
+  hipLaunchKernelGGL(grad_pairs_kernel, grid, dim3(256), 0, ctx->stream, h, d_x, n, Bt, lda, al,
+                     acc);
+  prof_end(ctx, K_GRAD, ev, 0, (double)n * (n + 1) / 2 * 8);
+  int r = hip_fail(ctx, hipGetLastError(), "grad_pairs_kernel");
+  if (r) return r;
+  hipLaunchKernelGGL(grad_finish_kernel, dim3(1), dim3(1024), 0, ctx->stream, h, d_x, n, Bt, lda,
+                     al, acc, obs_stddev, ctx->result, negative, d_out);
+  return hip_fail(ctx, hipGetLastError(), "grad_finish_kernel");
+}
+
+}  // namespace lfm

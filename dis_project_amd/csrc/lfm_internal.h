@@ -24,6 +24,7 @@ enum KClass {
   K_FINALIZE,     // logdet + quadratic form -> scalar
   K_SMALL,        // one-workgroup-per-problem fused small-N MLL
   K_MEAN,         // mean_function
+  K_GRAD,         // MLL gradient: W-weighted kernel-derivative reduction
   K_NCLASS
 };
 
@@ -69,6 +70,7 @@ struct lfm_ctx {
   double* parts = nullptr; size_t parts_cap = 0; // per-block logdet partials
   int* status = nullptr;                         // [0] first failing pivot (INT_MAX = none)
   double* result = nullptr;                      // [0..] scalar results
+  double* gacc = nullptr; size_t gacc_bytes = 0; // gradient accumulators + output
 
   // pinned host staging
   double* hpin = nullptr; size_t hpin_bytes = 0;
@@ -162,8 +164,14 @@ int launch_augment(lfm_ctx* ctx, const HypDev& h, const double* x, const double*
 
 // cholesky kernels (lfm_chol.hip)
 int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,
-                      double* d_out);
+                      double* d_out, int64_t bordered = 0);
 size_t tables_doubles(int G, int T);
+
+// gradient kernels (lfm_grad.hip)
+int launch_border_init(lfm_ctx* ctx, double* A, int64_t lda, int64_t Mp);
+int launch_grad(lfm_ctx* ctx, const HypDev& h, const double* d_x, int64_t n, const double* A,
+                int64_t lda, int64_t Mp, double obs_stddev, int negative, double* acc,
+                double* d_out);
 int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn,
                        int negative, double* d_out, int* d_status);
 

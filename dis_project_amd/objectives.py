@@ -49,6 +49,32 @@ class CustomConjMLL:
         ctx.check(rc, allow_not_pd=True)
         return float(out[0])
 
+    def value_and_grad(self, model: ExactLFM, train_data: Dataset):
+        """Value and gradient of ``step`` with respect to the constrained parameters —
+        what ``jax.value_and_grad(loss)`` differentiates at trainer.py:126 before the
+        bijectors' chain rule (trainer.py:103). One call into ``lfm_mll_grad_f64``.
+
+        Returns ``(value, grads)`` with ``grads = {"true_d": [G], "true_s": [G],
+        "true_b": [G], "l": float, "obs_stddev": float}`` (``jitter`` is static,
+        model.py:64). A Sigma that is not PD gives NaN everywhere, like JAX.
+        """
+        x = as_f64(train_data.X).reshape(-1, 3)
+        y = as_f64(train_data.y).reshape(-1)
+        if y.shape[0] != x.shape[0]:
+            raise ValueError("X and y must have the same number of rows")
+        G = int(model.num_genes)
+        val = np.empty(1)
+        g = np.empty(3 * G + 2)
+        hp = model.hyp()
+        ctx = model.ctx
+        rc = ctx.lib.lfm_mll_grad_f64(ctx.handle, dptr(x), dptr(y), x.shape[0], hp.ref,
+                                      int(self.negative), dptr(val), dptr(g))
+        ctx.check(rc, allow_not_pd=True)
+        grads = {"true_d": g[:G].copy(), "true_s": g[G:2 * G].copy(),
+                 "true_b": g[2 * G:3 * G].copy(), "l": float(g[3 * G]),
+                 "obs_stddev": float(g[3 * G + 1])}
+        return float(val[0]), grads
+
     def batch(self, models, datasets) -> np.ndarray:
         """Independent evaluations (restarts / ablations) in one call; NaN where not PD."""
         models = list(models)

@@ -125,6 +125,15 @@ int lfm_mll_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n, const
 int lfm_mll_batch_f64(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, int negative,
                       double* out, int* status);
 
+/* Value and gradient of CustomConjMLL(negative).step — what jax.value_and_grad(loss)
+ * differentiates at trainer.py:126, before the bijectors' chain rule (trainer.py:103) —
+ * with respect to the constrained parameters. grad[3G + 2]:
+ *   [0,G) true_d   [G,2G) true_s   [2G,3G) true_b   [3G] l   [3G+1] obs_stddev.
+ * jitter is a static field (model.py:64) and gets no gradient. Not PD: LFM_E_NOT_PD,
+ * value and grad NaN. */
+int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
+                     const lfm_hyp* hyp, int negative, double* value, double* grad);
+
 /* ------------------- GaussianDistribution(loc, scale).log_prob(y) (gpjax 0.8.2) */
 /* scale is a dense SPD n x n (row-major, leading dim lds; lower triangle read). */
 int lfm_log_prob_f64(lfm_ctx* ctx, const double* loc, const double* scale, int64_t n,

@@ -132,7 +132,9 @@ def cross_covariance(x, y, D, S, l, chunk=256):
     """model.py:372-394 (vmap over rows of x, then rows of y), row-chunked."""
     x = np.asarray(x, np.float64)
     y = np.asarray(y, np.float64)
-    out = np.empty((x.shape[0], y.shape[0]))
+    # complex D / S / l propagate (complex-step derivatives in mll_grad)
+    dt = np.result_type(np.asarray(D).dtype, np.asarray(S).dtype, np.asarray(l).dtype, np.float64)
+    out = np.empty((x.shape[0], y.shape[0]), dtype=dt)
     for i0 in range(0, x.shape[0], chunk):
         xa = x[i0:i0 + chunk, None, :]
         out[i0:i0 + chunk] = kernel_pairs(xa, y[None, :, :], D, S, l)
@@ -225,6 +227,82 @@ def mll(x, y, D, S, B, l, obs_stddev, jitter, negative=False):
     Sig = sigma(x, D, S, l, obs_stddev, jitter)
     constant = -1.0 if negative else 1.0
     return constant * log_prob(mx, Sig, y)
+
+
+def mll_grad(x, y, D, S, B, l, obs_stddev, jitter, negative=False, step=1e-30):
+    """Value and gradient of CustomConjMLL(negative).step with respect to the constrained
+    parameters (true_d, true_s, true_b, l, obs_stddev): the quantity
+    jax.value_and_grad(loss) differentiates before the bijectors' chain rule
+    (trainer.py:103, 126; jitter is a static field, model.py:64).
+
+        d log N / d theta = 1/2 tr((a a^T - Sigma^{-1}) dSigma/dtheta) + a^T dm/dtheta,
+        a = Sigma^{-1} (y - m),  dSigma/d obs_stddev = 2 obs_stddev I.
+
+    dK/dtheta of the reference kernel (model.py:152-369) is taken by complex step
+    (imag K(theta + i h) / h, exact to rounding: every operation of the kernel is analytic
+    and scipy's erf accepts complex arguments); dm/dtheta of mean_function
+    (model.py:124-149, block position i // (n // G)) is analytic.
+
+    Returns a dict: value, d, s, b (arrays [G]), l, obs_stddev, and the magnitudes
+    scale_{d,s,b,l,obs_stddev} of the summed terms (1/2 sum |W| |dSigma| + |a| |dm|) that
+    the tests scale their tolerance by.
+    """
+    D = np.asarray(D, np.float64)
+    S = np.asarray(S, np.float64)
+    B = np.asarray(B, np.float64)
+    x = np.asarray(x, np.float64)
+    y = np.asarray(y, np.float64).reshape(-1)
+    n, G = x.shape[0], D.shape[0]
+    sign = -1.0 if negative else 1.0
+    nanres = dict(value=float("nan"), d=np.full(G, np.nan), s=np.full(G, np.nan),
+                  b=np.full(G, np.nan), l=float("nan"), obs_stddev=float("nan"))
+    mx = mean_function(x, D, B, G).reshape(-1)
+    Sig = sigma(x, D, S, l, obs_stddev, jitter)
+    try:
+        c = scipy.linalg.cho_factor(Sig, lower=True, check_finite=False)
+    except (np.linalg.LinAlgError, scipy.linalg.LinAlgError):
+        return nanres
+    dg = np.diag(np.tril(c[0]))
+    if not np.all(np.isfinite(dg)) or np.any(dg <= 0):
+        return nanres
+    r = y - mx
+    a = scipy.linalg.cho_solve(c, r, check_finite=False)
+    Sinv = scipy.linalg.cho_solve(c, np.eye(n), check_finite=False)
+    W = np.outer(a, a) - Sinv
+    value = -0.5 * (n * LOG_2PI + 2.0 * np.sum(np.log(dg)) + r @ a)
+
+    def dgram(Dc, Sc, lc):
+        return np.imag(gram(x, Dc, Sc, lc)) / step
+
+    def contract(dK):
+        return 0.5 * np.sum(W * dK), 0.5 * np.sum(np.abs(W) * np.abs(dK))
+
+    out = dict(value=sign * value)
+    gd, gs, sd_, ss_ = np.zeros(G), np.zeros(G), np.zeros(G), np.zeros(G)
+    for g in range(G):
+        e = np.zeros(G, complex)
+        e[g] = 1j * step
+        gd[g], sd_[g] = contract(dgram(D + e, S, l))
+        gs[g], ss_[g] = contract(dgram(D, S + e, l))
+    gl, sl = contract(dgram(D, S, l + 1j * step))
+    # mean: m_i = (B/D)[i // bs] * flag_i
+    bs = n // G
+    f = flag_int(x[:, 2])
+    af = np.bincount(np.arange(n) // bs, weights=a * f, minlength=G)[:G]
+    aabs = np.bincount(np.arange(n) // bs, weights=np.abs(a * f), minlength=G)[:G]
+    gb = af / D
+    gd_mean = -B / D**2 * af
+    out["d"] = sign * (gd + gd_mean)
+    out["s"] = sign * gs
+    out["b"] = sign * gb
+    out["l"] = sign * gl
+    out["obs_stddev"] = sign * obs_stddev * np.trace(W)
+    out["scale_d"] = sd_ + np.abs(B / D**2) * aabs
+    out["scale_s"] = ss_
+    out["scale_b"] = aabs / np.abs(D)
+    out["scale_l"] = sl
+    out["scale_obs_stddev"] = abs(obs_stddev) * np.sum(np.abs(np.diag(W)))
+    return out
 
 
 # -------------------------------------------------- scalar restatement (math)

@@ -30,7 +30,7 @@ def grid_x(G, T, R=1, t_max=12.0):
                      np.ones(G * T * R)), axis=-1)
 
 
-def case(name, x, y, D, S, B, l, sd, jit, extra=None, store_K=True):
+def case(name, x, y, D, S, B, l, sd, jit, extra=None, store_K=True, grad=True):
     D, S, B = (np.asarray(v, np.float64) for v in (D, S, B))
     K = O.gram(x, D, S, l)
     m = O.mean_function(x, D, B, D.shape[0]).reshape(-1)
@@ -41,6 +41,11 @@ def case(name, x, y, D, S, B, l, sd, jit, extra=None, store_K=True):
              neg_mll=np.float64(neg))
     if store_K:
         d["K"] = K
+    if grad:  # gradient of +MLL w.r.t. the constrained parameters (oracle.mll_grad)
+        gr = O.mll_grad(x, y, D, S, B, l, sd, jit, negative=False)
+        for k in ("d", "s", "b", "l", "obs_stddev"):
+            d["grad_" + k] = np.asarray(gr[k], np.float64)
+            d["gscale_" + k] = np.asarray(gr["scale_" + k], np.float64)
     if extra:
         d.update(extra)
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **d)
@@ -111,6 +116,16 @@ def main():
     np.savez_compressed(os.path.join(HERE, "mixed_flags_cross.npz"), xa=xa, xb=xb, D=D, S=S,
                         l=np.float64(2.3), K=Kab)
     print("mixed_flags_cross            40 x 30")
+
+    # an MLL over mixed rows (gene rows and latent-force rows): all four kernel branches
+    # inside Sigma, for the gradient's kxf / kff terms
+    rng = np.random.default_rng(48)
+    G, n = 4, 48
+    D = rng.uniform(0.3, 1.0, G); S = rng.uniform(0.5, 1.5, G); B = rng.uniform(0.01, 0.1, G)
+    x = np.stack((rng.uniform(0, 12, n), rng.integers(0, G, n).astype(np.float64),
+                  (rng.uniform(size=n) < 0.75).astype(np.float64)), -1)
+    y = rng.normal(0.3, 0.5, n)
+    case("mixed_mll_n48", x, y, D, S, B, 1.9, 1.2, 1e-4)
 
     # KAT: all-zero times -> Sigma = (jitter + sd^2) I, closed-form log-density
     G, T = 4, 8

@@ -139,3 +139,38 @@ def test_dataset_3d_layout():
     assert x.shape == (24, 3) and y.shape == (24, 1)
     i = 1 * 12 + 2 * 4 + 3  # r=1, g=2, tau=3
     assert x[i, 0] == 12.0 and x[i, 1] == 2 and x[i, 2] == 1 and y[i, 0] == expr[1, 2, 3]
+
+
+@pytest.mark.parametrize("name", ["grid_n64", "mixed_mll_n48", "p53_3rep_n105"])
+def test_mll_grad_matches_central_differences(name):
+    """The complex-step gradient (oracle.mll_grad) against central differences of the
+    oracle MLL itself (h = 1e-6: truncation ~1e-9 relative)."""
+    g = load_golden(name)
+    x, y = g["x"], g["y"]
+    D, S, B = g["D"], g["S"], g["B"]
+    l, sd, jit = float(g["l"]), float(g["obs_stddev"]), float(g["jitter"])
+
+    def f(D=D, S=S, B=B, l=l, sd=sd):
+        return O.mll(x, y, D, S, B, l, sd, jit)
+
+    h = 1e-6
+    for key, arr in (("d", D), ("s", S), ("b", B)):
+        fd = []
+        for i in range(arr.size):
+            e = np.zeros(arr.size)
+            e[i] = h
+            fd.append((f(**{key.upper(): arr + e}) - f(**{key.upper(): arr - e})) / (2 * h))
+        np.testing.assert_allclose(g["grad_" + key], fd, rtol=2e-6,
+                                   atol=2e-7 * np.max(g["gscale_" + key]))
+    np.testing.assert_allclose(g["grad_l"], (f(l=l + h) - f(l=l - h)) / (2 * h), rtol=2e-6)
+    np.testing.assert_allclose(g["grad_obs_stddev"], (f(sd=sd + h) - f(sd=sd - h)) / (2 * h),
+                               rtol=2e-6)
+
+
+def test_mll_grad_golden_regenerates():
+    g = load_golden("grid_n64")
+    gr = O.mll_grad(g["x"], g["y"], g["D"], g["S"], g["B"], float(g["l"]),
+                    float(g["obs_stddev"]), float(g["jitter"]), negative=True)
+    for k in ("d", "s", "b", "l", "obs_stddev"):
+        np.testing.assert_allclose(gr[k], -g["grad_" + k], rtol=1e-12, atol=1e-12)
+    assert gr["value"] == pytest.approx(float(g["neg_mll"]), rel=1e-13)
