@@ -99,6 +99,9 @@ SIGNATURES = [
     ("lfm_mll_f64", c_int, [_c_ctx, _dptr, _dptr, c_int64, POINTER(LfmHyp), c_int, _dptr]),
     ("lfm_mll_grad_f64", c_int,
      [_c_ctx, _dptr, _dptr, c_int64, POINTER(LfmHyp), c_int, _dptr, _dptr]),
+    ("lfm_posterior_f64", c_int,
+     [_c_ctx, _dptr, _dptr, c_int64, _dptr, c_double, _dptr, c_int64, POINTER(LfmHyp), _dptr,
+      _dptr]),
     ("lfm_mll_batch_f64", c_int,
      [_c_ctx, c_int64, POINTER(LfmProblem), c_int, _dptr, POINTER(c_int)]),
     ("lfm_log_prob_f64", c_int, [_c_ctx, _dptr, _dptr, c_int64, c_int64, _dptr, _dptr]),

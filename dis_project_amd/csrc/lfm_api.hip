@@ -688,7 +688,7 @@ int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
   if (r) return r;
   r = launch_border_init(ctx, ctx->A, M2, Mp);
   if (r) return r;
-  r = chol_factor_solve(ctx, ctx->A, M2, n, Mp, negative, ctx->result, 1);
+  r = chol_factor_solve(ctx, ctx->A, M2, n, Mp, negative, ctx->result, CHOL_INVERSE);
   if (r) return r;
   double* d_out = ctx->gacc + 2 * G + 1;
   r = launch_grad(ctx, st.h, d_x, n, ctx->A, M2, Mp, hyp->obs_stddev, negative, ctx->gacc, d_out);
@@ -707,6 +707,61 @@ int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
     return set_err(ctx, LFM_E_NOT_PD,
                    "Cholesky failed: non-positive pivot at index " +
                        std::to_string((long long)hres[3]));
+  return LFM_OK;
+}
+
+int lfm_posterior_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
+                      const double* diag_vec, double diag_add, const double* t, int64_t m,
+                      const lfm_hyp* hyp, double* mean, double* cov) {
+  int r = validate_x(ctx, x, n);
+  if (r) return r;
+  r = validate_x(ctx, t, m);
+  if (r) return r;
+  if (!y || !mean || !cov) return set_err(ctx, LFM_E_ARG, "y / mean / cov is NULL");
+  r = check_hyp(ctx, hyp);
+  if (r) return r;
+  r = check_mean_shape(ctx, n, hyp);
+  if (r) return r;
+  r = check_mean_shape(ctx, m, hyp);
+  if (r) return r;
+  if ((n + m) > (int64_t)1 << 17) return set_err(ctx, LFM_E_ARG, "n + m too large");
+  DeviceGuard g(ctx->device);
+  Staged st;
+  r = stage_hyp(ctx, hyp, nullptr, 0, false, &st);
+  if (r) return r;
+  // xin: x (3n) y (n) v (n) t (3m) mean (m) cov (m*m)
+  const size_t nd = 5 * (size_t)n + 4 * (size_t)m + (size_t)m * m;
+  r = ensure(ctx, (void**)&ctx->xin, &ctx->xin_bytes, nd * 8);
+  if (r) return r;
+  double* d_x = ctx->xin;
+  double* d_y = d_x + 3 * n;
+  double* d_v = d_y + n;
+  double* d_t = d_v + n;
+  double* d_mean = d_t + 3 * m;
+  double* d_cov = d_mean + m;
+  hipMemcpyAsync(d_x, x, n * 3 * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipMemcpyAsync(d_y, y, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  if (diag_vec) hipMemcpyAsync(d_v, diag_vec, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipMemcpyAsync(d_t, t, m * 3 * 8, hipMemcpyHostToDevice, ctx->stream);
+  r = posterior_blocked(ctx, st.h, d_x, d_y, n, diag_vec ? d_v : nullptr, diag_add, d_t, m,
+                        d_mean, d_cov);
+  if (r) return r;
+  r = ensure_pinned(ctx, 64 * sizeof(double));
+  if (r) return r;
+  double* hres = ctx->hpin;
+  hipMemcpyAsync(hres, ctx->result, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+  hipMemcpyAsync(mean, d_mean, m * 8, hipMemcpyDeviceToHost, ctx->stream);
+  hipMemcpyAsync(cov, d_cov, (size_t)m * m * 8, hipMemcpyDeviceToHost, ctx->stream);
+  r = finish(ctx);
+  if (r) return r;
+  if ((int)hres[3] != INT_MAX) {
+    const double nan = std::nan("");
+    for (int64_t i = 0; i < m; ++i) mean[i] = nan;
+    for (int64_t i = 0; i < m * m; ++i) cov[i] = nan;
+    return set_err(ctx, LFM_E_NOT_PD,
+                   "Cholesky failed: non-positive pivot at index " +
+                       std::to_string((long long)hres[3]));
+  }
   return LFM_OK;
 }
 

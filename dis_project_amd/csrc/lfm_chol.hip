@@ -796,13 +796,17 @@ int probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us) {
 }
 
 int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,
-                      double* d_out, int64_t bordered) {
-  // bordered = 0: factor the Mp x Mp augmented matrix (block columns holding pivots only).
-  // bordered = 1: A is 2Mp x 2Mp, [[S_aug, .], [I, 0]]; all Mp/NB block columns of the top
-  // are eliminated with every trailing update restricted to the Mp-row window below the
-  // panel (the rows the identity border has reached), leaving -S_aug^{-1} in the bottom
-  // block: a Cholesky + triangular inverse + L^-T L^-1 product in N^3 flops on the same
-  // three kernels.
+                      double* d_out, int mode) {
+  // CHOL_MLL: factor the Mp x Mp augmented matrix (block columns holding pivots only).
+  // CHOL_INVERSE: A is 2Mp x 2Mp, [[S_aug, .], [I, 0]]; all Mp/NB block columns of the top
+  //   are eliminated with every trailing update restricted to the Mp-row window below the
+  //   panel (the rows the identity border has reached), leaving -S_aug^{-1} in the bottom
+  //   block: a Cholesky + triangular inverse + L^-T L^-1 product in N^3 flops on the same
+  //   three kernels.
+  // CHOL_SCHUR: eliminate the block columns holding the n pivots of an Mp x Mp matrix and
+  //   apply every trailing update, so rows >= round_up(n, NB) end up holding the Schur
+  //   complement (posterior covariance / mean correction, lfm_predict.hip).
+  const bool bordered = mode == CHOL_INVERSE;
   const int64_t npb = (n + NB - 1) / NB;  // block columns that hold pivots
   const int64_t nblk = bordered ? Mp / NB : npb;
   int r = ensure(ctx, (void**)&ctx->parts, &ctx->parts_cap, (size_t)nblk * sizeof(double));
@@ -827,7 +831,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   Launcher L{ctx, A, lda, bordered ? 2 * Mp : Mp, bordered ? Mp : 0};
   hipLaunchKernelGGL(status_init_kernel, dim3(1), dim3(1), 0, main, ctx->status);
   // the trailing update after the last super-panel matters only for the bordered rows
-  auto trailing = [&](int s) { return s + 1 < S || bordered; };
+  auto trailing = [&](int s) { return s + 1 < S || mode != CHOL_MLL; };
   if (!ctx->lookahead) {
     for (int s = 0; s < S; ++s) {
       const int64_t k = steps[s].first;

@@ -163,12 +163,16 @@ int launch_augment(lfm_ctx* ctx, const HypDev& h, const double* x, const double*
                    const double* loc, int64_t n, double* A, int64_t lda, int64_t Mp);
 
 // cholesky kernels (lfm_chol.hip)
+enum CholMode { CHOL_MLL = 0, CHOL_INVERSE = 1, CHOL_SCHUR = 2 };
 int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,
-                      double* d_out, int64_t bordered = 0);
+                      double* d_out, int mode = CHOL_MLL);
 size_t tables_doubles(int G, int T);
 
 // gradient kernels (lfm_grad.hip)
 int launch_border_init(lfm_ctx* ctx, double* A, int64_t lda, int64_t Mp);
+int posterior_blocked(lfm_ctx* ctx, const HypDev& h, const double* d_x, const double* d_y,
+                      int64_t n, const double* d_dv, double diag_add, const double* d_t, int64_t m,
+                      double* d_mean, double* d_cov);
 int launch_grad(lfm_ctx* ctx, const HypDev& h, const double* d_x, int64_t n, const double* A,
                 int64_t lda, int64_t Mp, double obs_stddev, int negative, double* acc,
                 double* d_out);

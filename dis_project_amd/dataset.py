@@ -128,3 +128,21 @@ def grid_inputs(num_genes: int, num_timepoints: int, replicates: int = 1, t_max:
                   np.tile(np.repeat(np.arange(num_genes), num_timepoints), replicates),
                   np.ones(num_genes * num_timepoints * replicates)), axis=-1)
     return x.astype(np.float64)
+
+
+def generate_test_times(t: int = 100) -> np.ndarray:
+    """utils.py:268-287: latent-force test inputs (linspace(0, 13, t), gene -1, flag 0).
+    Gene -1 wraps to the last gene under JAX gather semantics; with flag 0 only the
+    kff / kxf branches read it."""
+    times = np.linspace(0, 13, t)
+    return np.stack((times, np.repeat(-1.0, t), np.repeat(0.0, t)), axis=-1)
+
+
+def generate_test_times_pred(t: int = 100, num_genes: int = 5) -> np.ndarray:
+    """utils.py:290-314 (and GeneExpressionPredictor.generate_test_times_pred, utils.py:81-98):
+    gene-expression test inputs with 1-based gene indices 1..num_genes and flag 1. Index
+    num_genes is out of range and clamps to the last gene (JAX gather), a reference quirk
+    kept for parity."""
+    times = np.linspace(0, 13, t)
+    return np.stack((np.tile(times, num_genes), np.repeat(np.arange(1, num_genes + 1), t),
+                     np.ones(t * num_genes)), axis=1).astype(np.float64)

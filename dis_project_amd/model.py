@@ -202,6 +202,46 @@ class ExactLFM:
         """model.py:367-369: D_k * l / 2."""
         return (self.true_d[k] * self.l) / 2
 
+    # ----------------------------------------------------------- predictors
+    def _posterior(self, t, train_data, diag_add):
+        from .dataset import dataset_3d
+
+        x, y, variances = dataset_3d(train_data)
+        x = as_f64(x).reshape(-1, 3)
+        y = as_f64(y).reshape(-1)
+        v = as_f64(variances).reshape(-1)
+        t = as_f64(t).reshape(-1, 3)
+        m = t.shape[0]
+        mean = np.empty(m)
+        cov = np.empty((m, m))
+        hp = self.hyp()
+        ctx = self.ctx
+        rc = ctx.lib.lfm_posterior_f64(ctx.handle, dptr(x), dptr(y), x.shape[0], dptr(v),
+                                       float(diag_add), dptr(t), m, hp.ref, dptr(mean), dptr(cov))
+        ctx.check(rc, allow_not_pd=True)
+        return mean, cov
+
+    def latent_predict(self, test_inputs, train_data):
+        """model.py:420-465: S = K(x,x) + diag(variances) + jitter I (no observation noise);
+        mean = m(t) + K(t,x) S^{-1} (y - m(x)); var = diag(diag(K(t,t) + jitter I - K(t,x)
+        S^{-1} K(x,t))) + jitter I. One lfm_posterior_f64 call (Schur complement on the
+        Cholesky kernels; the reference's explicit cola.inv is the same operator)."""
+        from .distributions import GaussianDistribution
+
+        mean, cov = self._posterior(test_inputs, train_data, self.jitter)
+        var = np.diag(np.diag(cov) + self.jitter) + np.eye(mean.shape[0]) * self.jitter
+        return GaussianDistribution(np.atleast_1d(mean.squeeze()), var, device=self.device)
+
+    def multi_gene_predict(self, test_inputs, train_data):
+        """model.py:467-514: S = K(x,x) + diag(variances) + obs_stddev^2 I;
+        mean = m(t) + K(t,x) S^{-1} (y - m(x)); var = K(t,t) - K(t,x) S^{-1} K(x,t)
+        + jitter I. (The reference's ``t2`` with flags set to 1 is computed and unused.)"""
+        from .distributions import GaussianDistribution
+
+        mean, cov = self._posterior(test_inputs, train_data, self.obs_stddev**2)
+        var = cov + np.eye(mean.shape[0]) * self.jitter
+        return GaussianDistribution(np.atleast_1d(mean.squeeze()), var, device=self.device)
+
     def _check_kernel(self, kernel):
         # The reference passes ``model.kernel`` (objectives.py:70); any other kernel
         # object is not part of this hot path.

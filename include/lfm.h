@@ -134,6 +134,15 @@ int lfm_mll_batch_f64(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, int
 int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
                      const lfm_hyp* hyp, int negative, double* value, double* grad);
 
+/* ------------- posterior at test inputs (latent_predict / multi_gene_predict) */
+/* mean[m] = m(t) + K(t,x) S^{-1} (y - m(x)),  cov[m x m] = K(t,t) - K(t,x) S^{-1} K(x,t),
+ * S = K(x,x) + diag(diag_vec) + diag_add I (diag_vec [n] may be NULL); model.py:420-514.
+ * n and m must be multiples of num_genes (mean_function, model.py:145-149). The callers'
+ * jitter / diagonalisation is applied by the shim. Not PD: LFM_E_NOT_PD, outputs NaN. */
+int lfm_posterior_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
+                      const double* diag_vec, double diag_add, const double* t, int64_t m,
+                      const lfm_hyp* hyp, double* mean, double* cov);
+
 /* ------------------- GaussianDistribution(loc, scale).log_prob(y) (gpjax 0.8.2) */
 /* scale is a dense SPD n x n (row-major, leading dim lds; lower triangle read). */
 int lfm_log_prob_f64(lfm_ctx* ctx, const double* loc, const double* scale, int64_t n,

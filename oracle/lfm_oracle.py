@@ -305,6 +305,47 @@ def mll_grad(x, y, D, S, B, l, obs_stddev, jitter, negative=False, step=1e-30):
     return out
 
 
+# ---------------------------------------------------------------- predictors
+def latent_predict(x, y, variances, t, D, S, B, l, jitter):
+    """model.py:420-465 (cola.inv -> an explicit inverse here too).
+    Returns (mean [m], var [m, m] diagonal)."""
+    D, S, B = (np.asarray(v, np.float64) for v in (D, S, B))
+    y = np.asarray(y, np.float64).reshape(-1, 1)
+    G = D.shape[0]
+    mean_x = mean_function(x, D, B, G)
+    mean_t = mean_function(t, D, B, G)
+    Kxx = gram(x, D, S, l) + np.diag(np.asarray(variances, np.float64).reshape(-1))
+    Kxx = Kxx + np.eye(Kxx.shape[0]) * jitter
+    K_inv = np.linalg.inv(Kxx)
+    Kxf = cross_covariance(x, t, D, S, l)
+    KfxKxx = Kxf.T @ K_inv
+    mean = mean_t + KfxKxx @ (y - mean_x)
+    Kff = gram(t, D, S, l) + np.eye(t.shape[0]) * jitter
+    var = Kff - KfxKxx @ Kxf
+    var = np.diag(np.diag(var)) + np.eye(t.shape[0]) * jitter
+    return np.atleast_1d(mean.squeeze()), var
+
+
+def multi_gene_predict(x, y, variances, t, D, S, B, l, obs_stddev, jitter):
+    """model.py:467-514 (cola.solve on a PSD operator -> Cholesky solve).
+    Returns (mean [m], var [m, m])."""
+    D, S, B = (np.asarray(v, np.float64) for v in (D, S, B))
+    y = np.asarray(y, np.float64).reshape(-1, 1)
+    G = D.shape[0]
+    mean_x = mean_function(x, D, B, G)
+    Kxx = gram(x, D, S, l)
+    Sigma = Kxx + np.diag(np.asarray(variances, np.float64).reshape(-1))
+    Sigma = Sigma + np.eye(Sigma.shape[0]) * obs_stddev**2
+    mean_t = mean_function(t, D, B, G)
+    Ktt = gram(t, D, S, l)
+    Kxt = cross_covariance(x, t, D, S, l)
+    c = scipy.linalg.cho_factor(Sigma, lower=True)
+    Sigma_inv_Kxt = scipy.linalg.cho_solve(c, Kxt)
+    mean = mean_t + Sigma_inv_Kxt.T @ (y - mean_x)
+    var = Ktt - Kxt.T @ Sigma_inv_Kxt + np.eye(t.shape[0]) * jitter
+    return np.atleast_1d(mean.squeeze()), var
+
+
 # -------------------------------------------------- scalar restatement (math)
 def h_scalar(D, l, j, k, t1, t2):
     t_dist = t2 - t1

@@ -127,6 +127,26 @@ def main():
     y = rng.normal(0.3, 0.5, n)
     case("mixed_mll_n48", x, y, D, S, B, 1.9, 1.2, 1e-4)
 
+    # posterior predictors (model.py:420-514) on p53-shaped synthetic data: one replicate
+    # and all three (replicate-major layout), trained-looking hyperparameters
+    from dis_project_amd.dataset import (SyntheticP53Data, dataset_3d, generate_test_times,
+                                         generate_test_times_pred)
+    D = np.array([0.28, 0.37, 0.36, 0.8, 0.36]); S = np.array([0.9, 0.97, 0.98, 1.0, 0.97])
+    B = np.array([0.065, 0.007, 0.018, 0.003, 0.087])
+    for tag, rep in (("rep0", 0), ("all", None)):
+        data = SyntheticP53Data(replicate=rep, seed=5)
+        xx, yy, vv = dataset_3d(data)
+        t_lat = generate_test_times(100)
+        t_gene = generate_test_times_pred(40, 5)
+        lm, lv = O.latent_predict(xx, yy, vv, t_lat, D, S, B, 2.2, 1e-4)
+        gm, gv = O.multi_gene_predict(xx, yy, vv, t_gene, D, S, B, 2.2, 0.85, 1e-4)
+        np.savez_compressed(os.path.join(HERE, f"predict_p53_{tag}.npz"), x=xx,
+                            y=yy.reshape(-1), v=vv.reshape(-1), t_lat=t_lat, t_gene=t_gene, D=D,
+                            S=S, B=B, l=np.float64(2.2), obs_stddev=np.float64(0.85),
+                            jitter=np.float64(1e-4), lat_mean=lm, lat_var=lv, gene_mean=gm,
+                            gene_var=gv)
+        print(f"predict_p53_{tag:17s} n={xx.shape[0]:5d} m_lat=100 m_gene=200")
+
     # KAT: all-zero times -> Sigma = (jitter + sd^2) I, closed-form log-density
     G, T = 4, 8
     x = grid_x(G, T) * np.array([0.0, 1.0, 1.0])

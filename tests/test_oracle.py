@@ -174,3 +174,21 @@ def test_mll_grad_golden_regenerates():
     for k in ("d", "s", "b", "l", "obs_stddev"):
         np.testing.assert_allclose(gr[k], -g["grad_" + k], rtol=1e-12, atol=1e-12)
     assert gr["value"] == pytest.approx(float(g["neg_mll"]), rel=1e-13)
+
+
+def test_predictor_oracle_identities():
+    """latent_predict's explicit inverse and multi_gene_predict's Cholesky solve agree when
+    their Sigma coincide; test inputs equal to training rows reproduce the smoother."""
+    g = load_golden("predict_p53_rep0")
+    x, y, v = g["x"], g["y"], g["v"]
+    D, S, B, l = g["D"], g["S"], g["B"], float(g["l"])
+    jit = 1e-3
+    t = x[:35]
+    lm, lv = O.latent_predict(x, y, v, t, D, S, B, l, jit)
+    gm, gv = O.multi_gene_predict(x, y, v, t, D, S, B, l, np.sqrt(jit), jit)
+    np.testing.assert_allclose(lm, gm, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(np.diag(lv), np.diag(gv) + jit, rtol=1e-9, atol=1e-12)
+    # regenerate the stored fixture exactly
+    lm2, lv2 = O.latent_predict(x, y, v, g["t_lat"], D, S, B, l, float(g["jitter"]))
+    np.testing.assert_array_equal(lm2, g["lat_mean"])
+    np.testing.assert_array_equal(lv2, g["lat_var"])
