@@ -146,3 +146,103 @@ def generate_test_times_pred(t: int = 100, num_genes: int = 5) -> np.ndarray:
     times = np.linspace(0, 13, t)
     return np.stack((np.tile(times, num_genes), np.repeat(np.arange(1, num_genes + 1), t),
                      np.ones(t * num_genes)), axis=1).astype(np.float64)
+
+
+# ------------------------------------------------------------ Barenco CSV loader
+# dataset.py:213-321. The CSVs themselves are not distributed with the reference
+# (data/README.md); the format is: a probe-ID index column, then columns
+# cARP{r}-{t}hrs.CEL (r = 1..3, t = 0, 2, ..., 12), PUMA log-expressions in
+# barencoPUMA_exprs.csv and their standard errors in barencoPUMA_se.csv.
+BARENCO_PROBES = {
+    "203409_at": "DDB2",
+    "202284_s_at": "p21",
+    "218346_s_at": "SESN1",
+    "205780_at": "BIK",
+    "209295_at": "DR5",
+    "211300_s_at": "p53",
+}
+BARENCO_ORDER = ["DDB2", "BIK", "DR5", "p21", "SESN1", "p53"]
+BARENCO_COLUMNS = [f"cARP{r}-{t}hrs.CEL" for r in range(1, 4) for t in np.arange(7) * 2]
+
+
+def load_barenco_data(dir_path):
+    """dataset.py:213-321: read the two CSVs, keep the six known probes in the order
+    DDB2, BIK, DR5, p21, SESN1, p53, log-normal transform (mean e^{mu + s^2/2}, variance
+    (e^{s^2} - 1) e^{2 mu + s^2}) and rescale each gene by the ddof=1 standard deviation of
+    its first replicate. Falls back to ../data like the reference."""
+    import os
+
+    import pandas as pd
+
+    def read(name):
+        try:
+            with open(os.path.join(dir_path, name)) as f:
+                return pd.read_csv(f, index_col=0)
+        except FileNotFoundError:
+            with open(os.path.join("../data", name)) as f:
+                return pd.read_csv(f, index_col=0)
+
+    exprs = read("barencoPUMA_exprs.csv")
+    se = read("barencoPUMA_se.csv")
+    genes = exprs[exprs.index.isin(list(BARENCO_PROBES))][BARENCO_COLUMNS]
+    genes_se = se[se.index.isin(list(BARENCO_PROBES))][BARENCO_COLUMNS]
+    genes = genes.rename(index=BARENCO_PROBES).reindex(BARENCO_ORDER)
+    genes_se = genes_se.rename(index=BARENCO_PROBES).reindex(BARENCO_ORDER)
+
+    mu = genes.values  # [6, 21]
+    var = genes_se.values ** 2
+    full = np.exp(mu + var / 2)
+    var_full = (np.exp(var) - 1) * np.exp(2 * mu + var)
+    scale = np.sqrt(np.var(full[:, :7], axis=1, ddof=1))[:, None]  # first replicate, per gene
+    expr = full / scale
+    varr = var_full / scale**2
+    return {
+        "gene_names": list(genes.index[:-1]),
+        "gene_expressions": np.float64(expr[:-1]).reshape((5, 3, 7)).swapaxes(0, 1),
+        "gene_variances": np.float64(varr[:-1]).reshape((5, 3, 7)).swapaxes(0, 1),
+        "p53_expressions": np.float64(expr[-1:]).reshape((3, 1, 7)),
+        "p53_variances": np.float64(varr[-1:]).reshape((3, 1, 7)),
+    }
+
+
+class JaxP53Data(SyntheticP53Data):
+    """dataset.py:21-210: the Barenco data from CSV (load_barenco_data), with the same
+    replicate / gene selection and layout as the synthetic stand-in."""
+
+    def __init__(self, replicate=None, data_dir="data", selected_genes=None):
+        d = load_barenco_data(data_dir)
+        if replicate is not None and not (0 <= replicate < 3):
+            raise AssertionError("Invalid replicate number")  # dataset.py:62
+        super().__init__(replicate=replicate, selected_genes=selected_genes, num_genes=5,
+                         num_timepoints=7, num_replicates=3,
+                         expressions=d["gene_expressions"], variances=d["gene_variances"])
+
+    def params_ground_truth(self):
+        """dataset.py:194-210: Barenco et al. (2006) measured B, S, D, filtered by the
+        selected genes."""
+        B = np.array([0.0649, 0.0069, 0.0181, 0.0033, 0.0869])
+        D = np.array([0.2829, 0.3720, 0.3617, 0.8000, 0.3573])
+        S = np.array([0.9075, 0.9748, 0.9785, 1.0000, 0.9680])
+        idx = self.selected_indices
+        return B[idx], S[idx], D[idx]
+
+
+def write_barenco_csv(dir_path, log_expr, se, extra_probes=2, seed=0):
+    """Write log-expressions [6, 21] and standard errors [6, 21] (rows in BARENCO_ORDER) as
+    the two Barenco CSVs, probes shuffled among `extra_probes` unrelated rows and extra
+    columns — the on-disk format load_barenco_data reads (tests / synthetic runs)."""
+    import os
+
+    import pandas as pd
+
+    rng = np.random.default_rng(seed)
+    inv = {v: k for k, v in BARENCO_PROBES.items()}
+    probes = [inv[g] for g in BARENCO_ORDER] + [f"9999{i}_at" for i in range(extra_probes)]
+    cols = BARENCO_COLUMNS + ["cMOCK1-0hrs.CEL"]
+    order = rng.permutation(len(probes))
+    for name, arr in (("barencoPUMA_exprs.csv", log_expr), ("barencoPUMA_se.csv", se)):
+        full = np.concatenate([np.asarray(arr, np.float64),
+                               rng.normal(5, 1, (extra_probes, 21))], 0)
+        full = np.concatenate([full, rng.normal(5, 1, (len(probes), 1))], 1)
+        df = pd.DataFrame(full[order], index=[probes[i] for i in order], columns=cols)
+        df.to_csv(os.path.join(dir_path, name))

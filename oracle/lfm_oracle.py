@@ -305,6 +305,30 @@ def mll_grad(x, y, D, S, B, l, obs_stddev, jitter, negative=False, step=1e-30):
     return out
 
 
+# ------------------------------------------------------------- Barenco loader
+def barenco_transform(log_expr, se):
+    """dataset.py:268-313 element by element: rows DDB2, BIK, DR5, p21, SESN1, p53; columns
+    replicate-major (r, t). Returns gene_expressions / gene_variances [3, 5, 7] and
+    p53_expressions / p53_variances [3, 1, 7]."""
+    log_expr = np.asarray(log_expr, np.float64)
+    var = np.asarray(se, np.float64) ** 2
+    out_e = np.empty((3, 6, 7))
+    out_v = np.empty((3, 6, 7))
+    for g in range(6):
+        full = [math.exp(log_expr[g, c] + var[g, c] / 2) for c in range(21)]
+        vfull = [(math.exp(var[g, c]) - 1) * math.exp(2 * log_expr[g, c] + var[g, c])
+                 for c in range(21)]
+        first = full[:7]
+        mean = sum(first) / 7
+        scale = math.sqrt(sum((f - mean) ** 2 for f in first) / 6)  # ddof = 1, replicate 1
+        for r in range(3):
+            for t in range(7):
+                out_e[r, g, t] = full[7 * r + t] / scale
+                out_v[r, g, t] = vfull[7 * r + t] / scale**2
+    return {"gene_expressions": out_e[:, :5], "gene_variances": out_v[:, :5],
+            "p53_expressions": out_e[:, 5:], "p53_variances": out_v[:, 5:]}
+
+
 # ---------------------------------------------------------------- predictors
 def latent_predict(x, y, variances, t, D, S, B, l, jitter):
     """model.py:420-465 (cola.inv -> an explicit inverse here too).
