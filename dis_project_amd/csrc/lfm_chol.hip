@@ -814,11 +814,13 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   // step plan: super-panels of w = 4, 2 or 1 block columns while the trailing matrix is
   // large, so the bulk trailing update runs with depth 128 w (C traffic per flop / w)
   const int64_t w4min = env_int("LFM_W4_MIN", 6144), w2min = env_int("LFM_W2_MIN", 4096);
+  const int64_t w8min = env_int("LFM_W8_MIN", 1 << 30);
   std::vector<std::pair<int64_t, int>> steps;
   for (int64_t k = 0; k < nblk;) {
     const int64_t m = bordered ? Mp + NB : Mp - k * NB;
     int w = 1;
-    if (m >= w4min && k + 4 <= nblk) w = 4;
+    if (m >= w8min && k + 8 <= nblk) w = 8;
+    else if (m >= w4min && k + 4 <= nblk) w = 4;
     else if (m >= w2min && k + 2 <= nblk) w = 2;
     steps.emplace_back(k, w);
     k += w;
