@@ -65,11 +65,15 @@ def main():
                   "fetch_bytes_per_launch_x2": 2 * f, "write_bytes_per_launch": w,
                   "hbm_bytes_per_launch": 2 * f + w}
     json.dump(out, open(os.path.join(PROF, f"{rnd}_hbm.json"), "w"), indent=1)
-    if "syrk_kernel" in out:
-        s = out["syrk_kernel"]
+    # every SYRK instantiation (128-row bulk tiles, 64-row look-ahead bands) together: the
+    # same population bench.py's roofline averages over
+    syrk = [(k, v) for k, v in out.items() if k.startswith("syrk_kernel")]
+    if syrk:
+        launches = sum(v["launches"] for _, v in syrk)
+        total = sum(v["hbm_bytes_per_launch"] * v["launches"] for _, v in syrk)
         json.dump({"round": rnd, "source": f"profiles/{rnd}_hbm.json (PMC FETCH_SIZE x2 + WRITE_SIZE)",
-                   "hbm_bytes_per_launch": s["hbm_bytes_per_launch"],
-                   "launches": s["launches"]},
+                   "kernels": [k for k, _ in syrk],
+                   "hbm_bytes_per_launch": total / max(1, launches), "launches": launches},
                   open(os.path.join(PROF, "syrk_traffic.json"), "w"), indent=1)
     lines += ["", "HBM per launch (PMC, separate passes; read side x2 per MI355X_MICROARCH.md §HBM):",
               "", "| kernel | launches | read B/launch (x2) | write B/launch |", "|---|---|---|---|"]
