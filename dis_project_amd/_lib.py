@@ -117,6 +117,7 @@ SIGNATURES = [
     ("lfm_gram_f32_dev", c_int,
      [_c_ctx, c_void_p, c_int64, POINTER(LfmHyp), c_double, c_int, c_void_p, c_int64]),
     ("lfm_profile_enable", c_int, [_c_ctx, c_int]),
+    ("lfm_profile_classes", c_int, [_c_ctx, ctypes.c_uint]),
     ("lfm_profile_reset", c_int, [_c_ctx]),
     ("lfm_profile_read", c_int, [_c_ctx, POINTER(LfmKstat), c_int, POINTER(c_int)]),
     ("lfm_farm_unique_id", c_int, [_c_ctx, POINTER(ctypes.c_ubyte)]),
@@ -132,6 +133,10 @@ SIGNATURES = [
     ("lfm_probe_mfma4_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr, _dptr]),
     ("lfm_probe_mfma_f64_cycles", c_int, [_c_ctx, c_int, c_int, _dptr, _dptr]),
 ]
+
+# kernel classes in lfm_profile_read order (lfm_internal.h KClass)
+KCLASSES = ["tables", "gram_grid", "gram_direct", "augment", "potrf", "trsm", "syrk",
+            "finalize", "small_mll", "mean", "grad"]
 
 _lib = None
 _lib_lock = threading.Lock()
@@ -226,7 +231,15 @@ class Context:
             pass
 
     # -- profiling
-    def profile(self, on: bool = True):
+    def profile(self, on: bool = True, classes=None):
+        """Event-time kernel launches; `classes` (names from profile_read) limits which."""
+        if classes is not None:
+            mask = 0
+            for c in classes:
+                mask |= 1 << KCLASSES.index(c)
+            self.check(self.lib.lfm_profile_classes(self.handle, mask))
+        else:
+            self.check(self.lib.lfm_profile_classes(self.handle, 0xFFFFFFFF))
         self.check(self.lib.lfm_profile_enable(self.handle, int(on)))
 
     def profile_reset(self):

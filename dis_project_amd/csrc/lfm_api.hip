@@ -79,10 +79,9 @@ int ensure_events(lfm_ctx* ctx, size_t count) {
 }
 
 void prof_begin(lfm_ctx* ctx, int cls, hipEvent_t* a, hipStream_t st) {
-  (void)cls;
   *a = nullptr;
   if (!st) st = ctx->stream;
-  if (!ctx->prof) return;
+  if (!ctx->prof || !((ctx->prof_mask >> cls) & 1u)) return;
   if (ctx->pool.empty()) {
     hipEvent_t e;
     hipEventCreate(&e);
@@ -895,6 +894,12 @@ int lfm_memcpy_d2h(lfm_ctx* ctx, void* dst, const void* src, size_t bytes) {
 int lfm_profile_enable(lfm_ctx* ctx, int on) {
   if (!ctx) return LFM_E_ARG;
   ctx->prof = on != 0;
+  return LFM_OK;
+}
+
+int lfm_profile_classes(lfm_ctx* ctx, unsigned mask) {
+  if (!ctx) return LFM_E_ARG;
+  ctx->prof_mask = mask;
   return LFM_OK;
 }
 

@@ -834,37 +834,41 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   hipLaunchKernelGGL(status_init_kernel, dim3(1), dim3(1), 0, main, ctx->status);
   // the trailing update after the last super-panel matters only for the bordered rows
   auto trailing = [&](int s) { return s + 1 < S || mode != CHOL_MLL; };
-  if (!ctx->lookahead) {
-    for (int s = 0; s < S; ++s) {
-      const int64_t k = steps[s].first;
-      const int w = steps[s].second;
-      L.superpanel(main, k, w, n);
-      const int64_t s0 = (k + w) * NB;
-      if (trailing(s)) L.syrk(main, s0, k * NB, NB * w, L.tiles_from(s0), 0, INT_MAX, 128);
-    }
-  } else {
+  // Super-panel s is prepared ahead on the side stream while the trailing matrix is large
+  // enough for the main stream's bulk update to hide it; below LFM_SERIAL_BELOW rows the
+  // steps run back to back on the main stream (no cross-stream event hops in the tail).
+  const int64_t serial_below = env_int("LFM_SERIAL_BELOW", 0);
+  auto ahead = [&](int s) {
+    if (!ctx->lookahead) return false;
+    const int64_t m = bordered ? Mp + NB : Mp - steps[s].first * NB;
+    return m >= serial_below;
+  };
+  if (ahead(0)) {
     hipEventRecord(ev[0], main);
     hipStreamWaitEvent(side, ev[0], 0);
     L.superpanel(side, steps[0].first, steps[0].second, n);
     hipEventRecord(ev[1], side);
-    for (int s = 0; s < S; ++s) {
-      const int64_t k = steps[s].first;
-      const int w = steps[s].second;
-      const int wn = s + 1 < S ? steps[s + 1].second : 0;
-      const int64_t s0 = (k + w) * NB;
-      const int64_t T = L.tiles_from(s0);
-      // main: the bulk of step s's trailing update (tile columns >= wn), depth 128 w
-      hipStreamWaitEvent(main, ev[1 + 2 * s], 0);
-      if (trailing(s)) L.syrk(main, s0, k * NB, NB * w, T, wn, (int)T, 128);
-      hipEventRecord(ev[2 + 2 * s], main);
-      if (s + 1 < S) {
-        // side: the next super-panel's columns first (after main's previous bulk update),
-        // then its factorisation
-        if (s > 0) hipStreamWaitEvent(side, ev[2 + 2 * (s - 1)], 0);
-        L.syrk(side, s0, k * NB, NB * w, T, 0, wn, 64);
-        L.superpanel(side, steps[s + 1].first, steps[s + 1].second, n);
-        hipEventRecord(ev[1 + 2 * (s + 1)], side);
-      }
+  }
+  for (int s = 0; s < S; ++s) {
+    const int64_t k = steps[s].first;
+    const int w = steps[s].second;
+    const int64_t s0 = (k + w) * NB;
+    const int64_t T = L.tiles_from(s0);
+    if (ahead(s)) hipStreamWaitEvent(main, ev[1 + 2 * s], 0);
+    else L.superpanel(main, k, w, n);
+    // ahead(s + 1) implies ahead(s): the trailing matrix only shrinks
+    const bool nxt = s + 1 < S && ahead(s + 1);
+    const int wn = nxt ? steps[s + 1].second : 0;
+    // main: the bulk of step s's trailing update (tile columns >= wn), depth 128 w
+    if (trailing(s)) L.syrk(main, s0, k * NB, NB * w, T, wn, (int)T, 128);
+    hipEventRecord(ev[2 + 2 * s], main);
+    if (nxt) {
+      // side: the next super-panel's columns first (after main's previous bulk update,
+      // which wrote the same tiles), then its factorisation
+      if (s > 0) hipStreamWaitEvent(side, ev[2 + 2 * (s - 1)], 0);
+      L.syrk(side, s0, k * NB, NB * w, T, 0, wn, 64);
+      L.superpanel(side, steps[s + 1].first, steps[s + 1].second, n);
+      hipEventRecord(ev[1 + 2 * (s + 1)], side);
     }
   }
   r = hip_fail(ctx, hipGetLastError(), "cholesky launch");

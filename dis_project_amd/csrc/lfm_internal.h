@@ -77,6 +77,7 @@ struct lfm_ctx {
 
   // profiling
   bool prof = false;
+  unsigned prof_mask = ~0u;  // kernel classes timed while prof is on
   std::vector<lfm::ProfEvent> pending;
   std::vector<hipEvent_t> pool;
   lfm_kstat stats[lfm::K_NCLASS];

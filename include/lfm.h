@@ -164,6 +164,9 @@ int lfm_gram_f32_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* 
 
 /* ------------------------------------------------------------- profiling */
 int lfm_profile_enable(lfm_ctx* ctx, int on);
+/* Restrict event timing to kernel classes whose bit is set (bit i = entry i of
+ * lfm_profile_read's list; default all): fewer events inside a timed region. */
+int lfm_profile_classes(lfm_ctx* ctx, unsigned mask);
 int lfm_profile_reset(lfm_ctx* ctx);
 /* Copies up to max entries; *count = number of kernel classes seen. */
 int lfm_profile_read(lfm_ctx* ctx, lfm_kstat* stats, int max, int* count);

@@ -15,7 +15,7 @@ T = int(os.environ.get("SWEEP_T", "256"))
 work = configs.grid_workload("sweep", G, T, seed_params=2, seed_y=3)
 x = np.ascontiguousarray(work.data.X)
 y = np.ascontiguousarray(work.data.y.reshape(-1))
-# setting = lookahead,side_cus[,w4_min,w2_min[,w8_min]]
+# setting = lookahead,side_cus[,w4_min,w2_min[,w8_min[,serial_below]]]
 settings = [("1", "0"), ("0", "0"), ("1", "8"), ("1", "16"), ("1", "32")]
 if len(sys.argv) > 1:
     settings = [tuple(s.split(",")) for s in sys.argv[1:]]
@@ -25,6 +25,7 @@ for st in settings:
     if len(st) > 2:
         os.environ["LFM_W4_MIN"], os.environ["LFM_W2_MIN"] = st[2], st[3]
     os.environ["LFM_W8_MIN"] = st[4] if len(st) > 4 else "1073741824"
+    os.environ["LFM_SERIAL_BELOW"] = st[5] if len(st) > 5 else "0"
     ctx = _lib.Context(0)
     lib, h = ctx.lib, ctx.handle
     dx, dy = _lib.c_void_p(), _lib.c_void_p()
@@ -46,7 +47,8 @@ for st in settings:
     ctx.profile(False)
     print(json.dumps({"lookahead": la, "side_cus": cus, "w4_min": os.environ.get("LFM_W4_MIN"),
                       "w2_min": os.environ.get("LFM_W2_MIN"),
-                      "w8_min": os.environ.get("LFM_W8_MIN"), "n": int(x.shape[0]),
+                      "w8_min": os.environ.get("LFM_W8_MIN"),
+                      "serial_below": os.environ.get("LFM_SERIAL_BELOW"), "n": int(x.shape[0]),
                       "ms_median": float(np.median(ts[1:])), "ms_min": float(min(ts[1:])),
                       "mll": float(out[0]), "kernel_ms_sum": st}), flush=True)
     lib.lfm_dev_free(h, dx)
