@@ -419,6 +419,8 @@ namespace {
 // the main stream off them (hipExtStreamCreateWithCUMask); 0 (default) shares every CU and
 // relies on the side stream's higher priority. LFM_LOOKAHEAD=0 serialises on one stream.
 hipError_t create_streams(lfm_ctx* ctx) {
+  const char* dbv = std::getenv("LFM_SYRK_DB");
+  ctx->syrk_db = dbv ? std::atoi(dbv) : 0;
   const char* tv = std::getenv("LFM_TRSM");
   if (tv) ctx->trsm_variant = std::atoi(tv);
   const char* la = std::getenv("LFM_LOOKAHEAD");
@@ -1046,7 +1048,7 @@ int lfm_probe_rate(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflo
 }
 
 int lfm_probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
-  if (!ctx || !us || T < 1 || reps < 1 || kd < 16 || kd > 512 || kd % 16) return LFM_E_ARG;
+  if (!ctx || !us || T < 1 || reps < 1 || kd < 16 || kd > 2048 || kd % 16) return LFM_E_ARG;
   DeviceGuard g(ctx->device);
   return probe_syrk(ctx, T, kd, cio, reps, us);
 }

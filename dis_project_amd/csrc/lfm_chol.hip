@@ -483,12 +483,14 @@ __global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, in
 // Bands of at most 8 columns (look-ahead / in-panel updates) are enumerated column by
 // column; otherwise tj_hi must be T and the band is a triangle. Update depth kd (multiple
 // of KB): columns kb .. kb + kd of A. TR = tile rows (128, or 64 for latency-critical bands).
-template <bool CIO, int TR>
+// DB: double-buffered LDS stages (one barrier per K step instead of two).
+template <bool CIO, int TR, bool DB = false>
 __global__ __launch_bounds__(256, 2) void syrk_kernel(double* __restrict__ A, int64_t lda,
                                                       int64_t s, int64_t kb, int kd, int T,
                                                       int tj_lo, int tj_hi) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
-  __shared__ double sP[2][ST][KB + 1];
+  constexpr int NBUF = DB ? 2 : 1;
+  __shared__ double sPb[NBUF][2][ST][KB + 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
   const int li = lane & 15, lk = lane >> 4, l3 = lane & 3;
@@ -536,37 +538,54 @@ __global__ __launch_bounds__(256, 2) void syrk_kernel(double* __restrict__ A, in
 #pragma unroll
     for (int u = 0; u < 4; ++u) pre[NUI + u] = *reinterpret_cast<const double2*>(gj + u * ld32 + k0);
   };
-  auto lstore = [&]() {
+  auto lstore = [&](int b) {
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-      double* d = u < NUI ? &sP[0][srow + 32 * u][2 * sch] : &sP[1][srow + 32 * (u - NUI)][2 * sch];
+      double* d = u < NUI ? &sPb[b][0][srow + 32 * u][2 * sch]
+                          : &sPb[b][1][srow + 32 * (u - NUI)][2 * sch];
       d[0] = pre[u].x;
       d[1] = pre[u].y;
     }
   };
-
-  gload(0);
-  for (int k0 = 0; k0 < kd; k0 += KB) {
-    __syncthreads();
-    lstore();
-    __syncthreads();
-    if (k0 + KB < kd) gload(k0 + KB);
+  auto compute = [&](int b) {
 #pragma unroll 1
     for (int kk = 0; kk < KB; kk += 4) {
       double bb[4];
 #pragma unroll
-      for (int jr = 0; jr < 4; ++jr) bb[jr] = sP[1][wc + jr * 16 + li][kk + lk];
+      for (int jr = 0; jr < 4; ++jr) bb[jr] = sPb[b][1][wc + jr * 16 + li][kk + lk];
 #pragma unroll
       for (int h = 0; h < IRN / 8; ++h) {
         double a[8];
 #pragma unroll
-        for (int ir = 0; ir < 8; ++ir) a[ir] = -sP[0][wr + (h * 8 + ir) * 4 + l3][kk + lk];
+        for (int ir = 0; ir < 8; ++ir) a[ir] = -sPb[b][0][wr + (h * 8 + ir) * 4 + l3][kk + lk];
 #pragma unroll
         for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
           for (int jr = 0; jr < 4; ++jr)
             acc[h * 8 + ir][jr] = mfma4(a[ir], bb[jr], acc[h * 8 + ir][jr]);
       }
+    }
+  };
+
+  gload(0);
+  if (!DB) {
+    for (int k0 = 0; k0 < kd; k0 += KB) {
+      __syncthreads();
+      lstore(0);
+      __syncthreads();
+      if (k0 + KB < kd) gload(k0 + KB);
+      compute(0);
+    }
+  } else {
+    // stage k lives in buffer k & 1; the global loads run one stage ahead in registers
+    lstore(0);
+    if (KB < kd) gload(KB);
+    __syncthreads();
+    for (int k0 = 0, b = 0; k0 < kd; k0 += KB, b ^= 1) {
+      if (k0 + KB < kd) lstore(b ^ 1);
+      if (k0 + 2 * KB < kd) gload(k0 + 2 * KB);
+      compute(b);
+      __syncthreads();
     }
   }
 
@@ -674,6 +693,9 @@ struct Launcher {
     if (tr == 64)
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3((unsigned)tiles), dim3(256), 0, st, A, lda,
                          s0, kb, kd, (int)T, lo, hi);
+    else if (ctx->syrk_db)
+      hipLaunchKernelGGL((syrk_kernel<true, 128, true>), dim3((unsigned)tiles), dim3(256), 0, st,
+                         A, lda, s0, kb, kd, (int)T, lo, hi);
     else
       hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3((unsigned)tiles), dim3(256), 0, st, A,
                          lda, s0, kb, kd, (int)T, lo, hi);
@@ -734,7 +756,7 @@ int probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us) {
 }
 
 // Diagnostic: average duration (us) of one full-lower-triangle SYRK launch over a T x T grid
-// of 128-tiles with update depth kd (128 or 256); cio = 0 skips the C tile I/O.
+// of 128-tiles with update depth kd; cio bit 0 = C tile I/O, bit 1 = double-buffered stages.
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const int64_t n = (int64_t)T * ST + 512;
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
@@ -743,12 +765,23 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const unsigned tiles = (unsigned)((int64_t)T * (T + 1) / 2);
   hipStream_t st = ctx->stream;
   auto go = [&]() {
-    if (cio)
-      hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T);
-    else
-      hipLaunchKernelGGL((syrk_kernel<false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T);
+    switch (cio & 3) {
+      case 1:
+        hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
+                           (int64_t)512, (int64_t)0, kd, T, 0, T);
+        break;
+      case 0:
+        hipLaunchKernelGGL((syrk_kernel<false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
+                           (int64_t)512, (int64_t)0, kd, T, 0, T);
+        break;
+      case 3:
+        hipLaunchKernelGGL((syrk_kernel<true, 128, true>), dim3(tiles), dim3(256), 0, st, ctx->A,
+                           n, (int64_t)512, (int64_t)0, kd, T, 0, T);
+        break;
+      default:
+        hipLaunchKernelGGL((syrk_kernel<false, 128, true>), dim3(tiles), dim3(256), 0, st,
+                           ctx->A, n, (int64_t)512, (int64_t)0, kd, T, 0, T);
+    }
   };
   go();
   hipEvent_t a, b;

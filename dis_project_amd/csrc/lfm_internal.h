@@ -56,6 +56,7 @@ struct lfm_ctx {
   hipStream_t side = nullptr;    // high-priority look-ahead stream: panel factor + solve
   bool lookahead = true;
   int trsm_variant = 2;          // panel-solve kernel variant (LFM_TRSM=2|3)
+  int syrk_db = 0;               // double-buffered SYRK stages (LFM_SYRK_DB=1)
   std::vector<hipEvent_t> evs;   // cross-stream dependency events (timing disabled)
   std::string err;
   int nb = 128;  // Cholesky block size

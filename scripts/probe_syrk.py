@@ -7,9 +7,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dis_project_amd import _lib  # noqa: E402
 
 ctx = _lib.get_context(0)
-for T in (126, 64, 32):
-    for kd in (128, 256, 512):
-        for cio in (1, 0):
+# cio: bit 0 = C tile I/O, bit 1 = double-buffered LDS stages
+TS = [int(v) for v in os.environ.get("PROBE_T", "126,64,32").split(",")]
+KDS = [int(v) for v in os.environ.get("PROBE_KD", "128,256,512").split(",")]
+CIOS = [int(v) for v in os.environ.get("PROBE_CIO", "1,0,3,2").split(",")]
+for T in TS:
+    for kd in KDS:
+        for cio in CIOS:
             us = _lib.c_double()
             ctx.check(ctx.lib.lfm_probe_syrk(ctx.handle, T, kd, cio, 5, _lib.ctypes.byref(us)))
             tiles = T * (T + 1) // 2
