@@ -419,6 +419,15 @@ namespace {
 // the main stream off them (hipExtStreamCreateWithCUMask); 0 (default) shares every CU and
 // relies on the side stream's higher priority. LFM_LOOKAHEAD=0 serialises on one stream.
 hipError_t create_streams(lfm_ctx* ctx) {
+  const char* trv = std::getenv("LFM_SYRK_TR");
+  ctx->syrk_tr = trv ? std::atoi(trv) : 0;
+  if (ctx->syrk_tr != 64 && ctx->syrk_tr != 128) ctx->syrk_tr = 0;
+  const char* scv = std::getenv("LFM_SLAB_COST");
+  if (scv) ctx->slab_cost = std::atof(scv);
+  int ncu = 0;
+  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) ==
+          hipSuccess && ncu > 0)
+    ctx->cus = ncu;
   const char* dbv = std::getenv("LFM_SYRK_DB");
   ctx->syrk_db = dbv ? std::atoi(dbv) : 0;
   const char* tv = std::getenv("LFM_TRSM");

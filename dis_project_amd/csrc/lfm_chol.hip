@@ -506,11 +506,14 @@ __global__ __launch_bounds__(256, 2) void syrk_kernel(double* __restrict__ A, in
     }
     ti = SUB * tj + (int)b;
   } else {
+    // triangle of 128-tiles over tile columns [tj_lo, T), SUB row slabs of TR rows per tile
+    const int sub = (int)(b % SUB);
+    b /= SUB;
     int a = (int)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
     while ((int64_t)(a + 1) * (a + 2) / 2 <= b) ++a;
     while ((int64_t)a * (a + 1) / 2 > b) --a;
     tj = (int)(b - (int64_t)a * (a + 1) / 2) + tj_lo;
-    ti = SUB * (a + tj_lo);
+    ti = SUB * (a + tj_lo) + sub;
   }
   const int64_t i0 = s + (int64_t)ti * TR, j0 = s + (int64_t)tj * ST;
   const bool diag = i0 < j0 + ST;  // the tile reaches the diagonal: keep col <= row only
@@ -679,7 +682,10 @@ struct Launcher {
     if (T <= 0 || hi <= lo) return;
     hi = (int)std::min<int64_t>(hi, T);
     const bool band = hi - lo <= 8;
-    if (!band && (hi != T || tr != 128)) { hi = (int)T; tr = 128; }
+    if (!band) {
+      hi = (int)T;
+      tr = tile_rows(T - lo);
+    }
     const int sub = ST / tr;
     int64_t tiles = 0;
     double elems = 0;
@@ -687,7 +693,6 @@ struct Launcher {
       tiles += (int64_t)sub * (T - tj);
       elems += (double)(T - tj - 1) * ST * ST + (double)ST * (ST + 1) / 2;
     }
-    if (!band) tiles = (T - lo) * (T - lo + 1) / 2;
     hipEvent_t ev;
     prof_begin(ctx, K_SYRK, &ev, st);
     if (tr == 64)
@@ -702,6 +707,17 @@ struct Launcher {
     prof_end(ctx, K_SYRK, ev, elems * 2.0 * kd, elems * 16.0, st);
   }
   int64_t tiles_from(int64_t s0) const { return (end(s0) - s0) / ST; }
+  // Row height of the triangle's work units: 128-row tiles run 2 per CU, 64-row slabs 3 per
+  // CU (fewer VGPRs); pick the one with fewer (cost-weighted) rounds of workgroups over the
+  // chip, so a triangle just past a multiple of 512 tiles does not leave a mostly idle
+  // last round. LFM_SYRK_TR=64|128 forces one.
+  int tile_rows(int64_t Tt) const {
+    if (ctx->syrk_tr) return ctx->syrk_tr;
+    const int64_t tiles = Tt * (Tt + 1) / 2;
+    const double r128 = (double)((tiles + 2 * ctx->cus - 1) / (2 * ctx->cus));
+    const double r64 = (double)((2 * tiles + 3 * ctx->cus - 1) / (3 * ctx->cus));
+    return r64 * ctx->slab_cost < r128 ? 64 : 128;
+  }
   // Factor the super-panel of block columns [k, k + w): per column potrf + trsm, then the
   // update of the super-panel's remaining columns with it (K = 128).
   void superpanel(hipStream_t st, int64_t k, int w, int64_t n) {
@@ -756,7 +772,8 @@ int probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us) {
 }
 
 // Diagnostic: average duration (us) of one full-lower-triangle SYRK launch over a T x T grid
-// of 128-tiles with update depth kd; cio bit 0 = C tile I/O, bit 1 = double-buffered stages.
+// of 128-tiles with update depth kd; cio bit 0 = C tile I/O, bit 1 = double-buffered stages,
+// bit 2 = 64-row slabs (with C I/O).
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const int64_t n = (int64_t)T * ST + 512;
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
@@ -765,6 +782,11 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const unsigned tiles = (unsigned)((int64_t)T * (T + 1) / 2);
   hipStream_t st = ctx->stream;
   auto go = [&]() {
+    if (cio & 4) {  // 64-row slabs, C I/O
+      hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(2 * tiles), dim3(256), 0, st, ctx->A, n,
+                         (int64_t)512, (int64_t)0, kd, T, 0, T);
+      return;
+    }
     switch (cio & 3) {
       case 1:
         hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,

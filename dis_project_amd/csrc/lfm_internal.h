@@ -57,6 +57,9 @@ struct lfm_ctx {
   bool lookahead = true;
   int trsm_variant = 2;          // panel-solve kernel variant (LFM_TRSM=2|3)
   int syrk_db = 0;               // double-buffered SYRK stages (LFM_SYRK_DB=1)
+  int syrk_tr = 0;               // force SYRK triangle work-unit rows (LFM_SYRK_TR=64|128)
+  int cus = 256;                 // compute units of the device
+  double slab_cost = 0.75;       // time of a round of 64-row slabs / a round of 128-tiles
   std::vector<hipEvent_t> evs;   // cross-stream dependency events (timing disabled)
   std::string err;
   int nb = 128;  // Cholesky block size
