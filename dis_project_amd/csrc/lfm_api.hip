@@ -424,10 +424,6 @@ hipError_t create_streams(lfm_ctx* ctx) {
   if (ctx->syrk_tr != 64 && ctx->syrk_tr != 128) ctx->syrk_tr = 0;
   const char* scv = std::getenv("LFM_SLAB_COST");
   if (scv) ctx->slab_cost = std::atof(scv);
-  int ncu = 0;
-  if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device) ==
-          hipSuccess && ncu > 0)
-    ctx->cus = ncu;
   const char* dbv = std::getenv("LFM_SYRK_DB");
   ctx->syrk_db = dbv ? std::atoi(dbv) : 0;
   const char* tv = std::getenv("LFM_TRSM");
@@ -441,6 +437,7 @@ hipError_t create_streams(lfm_ctx* ctx) {
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, ctx->device);
   const int ncu = prop.multiProcessorCount;
+  if (ncu > 0) ctx->cus = ncu;
   if (side_cus > 0 && side_cus < ncu) {
     std::vector<uint32_t> mside((ncu + 31) / 32, 0u), mmain((ncu + 31) / 32, 0u);
     for (int c = 0; c < ncu; ++c) (c < side_cus ? mside : mmain)[c / 32] |= 1u << (c % 32);
