@@ -420,8 +420,9 @@ namespace {
 // relies on the side stream's higher priority. LFM_LOOKAHEAD=0 serialises on one stream.
 hipError_t create_streams(lfm_ctx* ctx) {
   const char* trv = std::getenv("LFM_SYRK_TR");
+  // LFM_SYRK_TR: 64 / 128 force the triangle's row height, -1 = choose by round count
   ctx->syrk_tr = trv ? std::atoi(trv) : 0;
-  if (ctx->syrk_tr != 64 && ctx->syrk_tr != 128) ctx->syrk_tr = 0;
+  if (ctx->syrk_tr != 64 && ctx->syrk_tr != 128 && ctx->syrk_tr != -1) ctx->syrk_tr = 0;
   const char* scv = std::getenv("LFM_SLAB_COST");
   if (scv) ctx->slab_cost = std::atof(scv);
   const char* dbv = std::getenv("LFM_SYRK_DB");

@@ -484,8 +484,11 @@ __global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, in
 // column; otherwise tj_hi must be T and the band is a triangle. Update depth kd (multiple
 // of KB): columns kb .. kb + kd of A. TR = tile rows (128, or 64 for latency-critical bands).
 // DB: double-buffered LDS stages (one barrier per K step instead of two).
+#ifndef LFM_SLAB_WGS
+#define LFM_SLAB_WGS 3
+#endif
 template <bool CIO, int TR, bool DB = false>
-__global__ __launch_bounds__(256, 2) void syrk_kernel(double* __restrict__ A, int64_t lda,
+__global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(double* __restrict__ A, int64_t lda,
                                                       int64_t s, int64_t kb, int kd, int T,
                                                       int tj_lo, int tj_hi) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
@@ -712,7 +715,8 @@ struct Launcher {
   // chip, so a triangle just past a multiple of 512 tiles does not leave a mostly idle
   // last round. LFM_SYRK_TR=64|128 forces one.
   int tile_rows(int64_t Tt) const {
-    if (ctx->syrk_tr) return ctx->syrk_tr;
+    if (ctx->syrk_tr > 0) return ctx->syrk_tr;
+    if (ctx->syrk_tr == 0) return 64;  // measured faster at every size (scripts/probe_syrk.py)
     const int64_t tiles = Tt * (Tt + 1) / 2;
     const double r128 = (double)((tiles + 2 * ctx->cus - 1) / (2 * ctx->cus));
     const double r64 = (double)((2 * tiles + 3 * ctx->cus - 1) / (3 * ctx->cus));
