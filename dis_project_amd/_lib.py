@@ -136,7 +136,7 @@ SIGNATURES = [
 
 # kernel classes in lfm_profile_read order (lfm_internal.h KClass)
 KCLASSES = ["tables", "gram_grid", "gram_direct", "augment", "potrf", "trsm", "syrk",
-            "finalize", "small_mll", "mean", "grad"]
+            "finalize", "small_mll", "mean", "grad", "panel"]
 
 _lib = None
 _lib_lock = threading.Lock()

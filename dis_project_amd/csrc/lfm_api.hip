@@ -21,7 +21,7 @@ namespace lfm {
 const char* const kClassName[K_NCLASS] = {"tables",   "gram_grid", "gram_direct",
                                           "augment",  "potrf",     "trsm",
                                           "syrk",     "finalize",  "small_mll",
-                                          "mean",     "grad"};
+                                          "mean",     "grad",      "panel"};
 
 int set_err(lfm_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;
@@ -419,14 +419,14 @@ namespace {
 // the main stream off them (hipExtStreamCreateWithCUMask); 0 (default) shares every CU and
 // relies on the side stream's higher priority. LFM_LOOKAHEAD=0 serialises on one stream.
 hipError_t create_streams(lfm_ctx* ctx) {
+  const char* fv = std::getenv("LFM_FUSED");
+  ctx->fused = fv ? std::atoi(fv) : 1;
   const char* trv = std::getenv("LFM_SYRK_TR");
   // LFM_SYRK_TR: 64 / 128 force the triangle's row height, -1 = choose by round count
   ctx->syrk_tr = trv ? std::atoi(trv) : 0;
   if (ctx->syrk_tr != 64 && ctx->syrk_tr != 128 && ctx->syrk_tr != -1) ctx->syrk_tr = 0;
   const char* scv = std::getenv("LFM_SLAB_COST");
   if (scv) ctx->slab_cost = std::atof(scv);
-  const char* dbv = std::getenv("LFM_SYRK_DB");
-  ctx->syrk_db = dbv ? std::atoi(dbv) : 0;
   const char* tv = std::getenv("LFM_TRSM");
   if (tv) ctx->trsm_variant = std::atoi(tv);
   const char* la = std::getenv("LFM_LOOKAHEAD");
@@ -482,6 +482,8 @@ int lfm_ctx_create(int device, lfm_ctx** out) {
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->linvT, 128 * 128 * sizeof(double));
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->status, 64);
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->result, 64 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&ctx->psync, 64);
+  if (e == hipSuccess) e = hipMemset(ctx->psync, 0, 64);
   if (e != hipSuccess) {
     lfm_ctx_destroy(ctx);
     return LFM_E_HIP;
@@ -497,7 +499,8 @@ void lfm_ctx_destroy(lfm_ctx* ctx) {
   lfm_farm_destroy(ctx);
   for (void* p : {(void*)ctx->A, (void*)ctx->tab, (void*)ctx->tab32, (void*)ctx->par,
                   (void*)ctx->xin, (void*)ctx->linvT, (void*)ctx->parts, (void*)ctx->status,
-                  (void*)ctx->result, (void*)ctx->farm_buf})
+                  (void*)ctx->result, (void*)ctx->farm_buf, (void*)ctx->gacc,
+                  (void*)ctx->psync})
     if (p) hipFree(p);
   if (ctx->hpin) hipHostFree(ctx->hpin);
   for (auto& p : ctx->pending) {

@@ -117,15 +117,16 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 // the four waves, and logdet / the first failing pivot are reduced.
 // PH (diagnostics only, lfm_probe_potrf): bit 0 = phase 1, bit 1 = phase 2, bit 2 = phase 3,
 // bit 3 = global load / store of the block. The product path always runs PH = 15.
+// only the 36 lower 16x16 blocks of the 128x128 block, each 16 x 17 (padded) doubles:
+// 78 KB, so the kernel fits on a CU beside one SYRK workgroup (look-ahead overlap)
+constexpr int MB_DOUBLES = (NB / IB) * (NB / IB + 1) / 2 * IB * (IB + 1);
+
 template <int PH>
-__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
-                                                        int64_t kb, int64_t npiv,
-                                                        double* __restrict__ dinv,
-                                                        double* __restrict__ parts, int k,
-                                                        int* __restrict__ status) {
-  // only the 36 lower 16x16 blocks of the 128x128 block, each 16 x 17 (padded) doubles:
-  // 78 KB, so the kernel fits on a CU beside one SYRK workgroup (look-ahead overlap)
-  __shared__ double Mb[(NB / IB) * (NB / IB + 1) / 2 * IB * (IB + 1)];
+__device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __restrict__ A,
+                                            int64_t lda, int64_t kb, int64_t npiv,
+                                            double* __restrict__ dinv,
+                                            double* __restrict__ parts, int k,
+                                            int* __restrict__ status) {
   __shared__ double pvs[NB];  // unscaled pivots
   __shared__ double ipv[NB];  // 1 / L_cc
   __shared__ double red[4];
@@ -299,6 +300,16 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
 #undef MS
 }
 
+template <int PH>
+__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
+                                                        int64_t kb, int64_t npiv,
+                                                        double* __restrict__ dinv,
+                                                        double* __restrict__ parts, int k,
+                                                        int* __restrict__ status) {
+  __shared__ double Mb[MB_DOUBLES];
+  potrf_block<PH>(Mb, A, lda, kb, npiv, dinv, parts, k, status);
+}
+
 // ----------------------------------------------------------------- trsm
 // Rows [s, Mp) of block column kb, 32 rows per workgroup (2 waves x 16 rows):
 //   X_cb = (A_cb - sum_{q < cb} X_q L_{cb,q}^T) * Dinv_cb^T,  cb = 0..7 (16 columns each).
@@ -400,18 +411,12 @@ __global__ __launch_bounds__(128) void trsm_kernel_v3(double* __restrict__ A, in
 // The wave's rows live in LDS; the L_{cb,q} fragments (the factored diagonal block, shared
 // by every workgroup, L2-resident) for column block cb+1 are loaded while cb computes,
 // and the K chain is split over two accumulators.
-__global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, int64_t lda, int64_t s,
-                                                   int64_t kb, const double* __restrict__ dinv) {
-  __shared__ double sA[64][NB + 1];
+// The solve proper on 64 rows already in LDS (sA, visible to every wave of the workgroup).
+__device__ __forceinline__ void trsm_rows(double (*__restrict__ sA)[NB + 1],
+                                          double* __restrict__ A, int64_t lda, int64_t r0,
+                                          int64_t kb, const double* __restrict__ dinv) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lk = lane >> 4;
-  const int64_t r0 = s + (int64_t)blockIdx.x * 64;
-  for (int idx = tid; idx < 64 * (NB / 2); idx += 256) {
-    const int r = idx / (NB / 2), q2 = idx - r * (NB / 2);
-    const double2 v = *reinterpret_cast<const double2*>(&A[(r0 + r) * lda + kb + 2 * q2]);
-    sA[r][2 * q2] = v.x;
-    sA[r][2 * q2 + 1] = v.y;
-  }
   const int wr = w * IB;
   const double* Lrow = A + (kb + li) * lda + kb + lk;  // L[li][lk]
   constexpr int NCB = NB / IB;
@@ -461,6 +466,20 @@ __global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, in
   }
 }
 
+__global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, int64_t lda, int64_t s,
+                                                   int64_t kb, const double* __restrict__ dinv) {
+  __shared__ double sA[64][NB + 1];
+  const int tid = threadIdx.x;
+  const int64_t r0 = s + (int64_t)blockIdx.x * 64;
+  for (int idx = tid; idx < 64 * (NB / 2); idx += 256) {
+    const int r = idx / (NB / 2), q2 = idx - r * (NB / 2);
+    const double2 v = *reinterpret_cast<const double2*>(&A[(r0 + r) * lda + kb + 2 * q2]);
+    sA[r][2 * q2] = v.x;
+    sA[r][2 * q2 + 1] = v.y;
+  }
+  trsm_rows(sA, A, lda, r0, kb, dinv);
+}
+
 // ----------------------------------------------------------------- syrk
 // Trailing update of the lower triangle: for 128x128 tiles (ti >= tj) of rows/cols
 // starting at s:  C[i][j] -= sum_q P[i][q] P[j][q],  P = A[:, kb:kb+NB].
@@ -487,16 +506,76 @@ __global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, in
 #ifndef LFM_SLAB_WGS
 #define LFM_SLAB_WGS 3
 #endif
-template <bool CIO, int TR, bool DB = false>
-__global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(double* __restrict__ A, int64_t lda,
-                                                      int64_t s, int64_t kb, int kd, int T,
-                                                      int tj_lo, int tj_hi) {
-  constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
-  constexpr int NBUF = DB ? 2 : 1;
-  __shared__ double sPb[NBUF][2][ST][KB + 1];
+// acc[ir][jr] (C[wr + ir*4 + (lane>>4)][wc + jr*16 + (lane&15)] of a TR x 128 block at rows
+// i0, cols j0; waves as 2 x 2) -= P_i P_j^T over panel columns kb .. kb + kd. sP: LDS staging,
+// [2][ST][KB + 1] doubles. Every thread of the (256-thread) workgroup must call it.
+template <int TR>
+__device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, int64_t lda,
+                                                int64_t i0, int64_t j0, int64_t kb, int kd,
+                                                double (&acc)[TR / 8][4],
+                                                double (*__restrict__ sP)[ST][KB + 1]) {
+  constexpr int IRN = TR / 8;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
   const int li = lane & 15, lk = lane >> 4, l3 = lane & 3;
+  // staging: TR rows of panel i and 128 rows of panel j, KB doubles each; thread tid moves
+  // chunk (tid & 7) of rows (tid >> 3) + 32u
+  static_assert(KB == 16, "staging map assumes 8 double2 chunks per row");
+  constexpr int NUI = TR / 32, NU = NUI + 4;
+  const int srow = tid >> 3, sch = tid & 7;
+  const double* gi = A + (i0 + srow) * lda + kb + 2 * sch;
+  const double* gj = A + (j0 + srow) * lda + kb + 2 * sch;
+  const int ld32 = (int)(32 * lda);
+  double2 pre[NU];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < NUI; ++u) pre[u] = *reinterpret_cast<const double2*>(gi + u * ld32 + k0);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) pre[NUI + u] = *reinterpret_cast<const double2*>(gj + u * ld32 + k0);
+  };
+  gload(0);
+  for (int k0 = 0; k0 < kd; k0 += KB) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      double* d = u < NUI ? &sP[0][srow + 32 * u][2 * sch] : &sP[1][srow + 32 * (u - NUI)][2 * sch];
+      d[0] = pre[u].x;
+      d[1] = pre[u].y;
+    }
+    __syncthreads();
+    if (k0 + KB < kd) gload(k0 + KB);
+#pragma unroll 1
+    for (int kk = 0; kk < KB; kk += 4) {
+      double bb[4];
+#pragma unroll
+      for (int jr = 0; jr < 4; ++jr) bb[jr] = sP[1][wc + jr * 16 + li][kk + lk];
+#pragma unroll
+      for (int h = 0; h < IRN / 8; ++h) {
+        double a[8];
+#pragma unroll
+        for (int ir = 0; ir < 8; ++ir) a[ir] = -sP[0][wr + (h * 8 + ir) * 4 + l3][kk + lk];
+#pragma unroll
+        for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+          for (int jr = 0; jr < 4; ++jr)
+            acc[h * 8 + ir][jr] = mfma4(a[ir], bb[jr], acc[h * 8 + ir][jr]);
+      }
+    }
+  }
+}
+
+#ifndef LFM_SLAB_WGS
+#define LFM_SLAB_WGS 3
+#endif
+template <bool CIO, int TR>
+__global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
+    double* __restrict__ A, int64_t lda, int64_t s, int64_t kb, int kd, int T, int tj_lo,
+    int tj_hi) {
+  constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
+  __shared__ double sP[2][ST][KB + 1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
+  const int li = lane & 15, lk = lane >> 4;
 
   constexpr int SUB = ST / TR;  // row tiles per 128 rows
   int64_t b = blockIdx.x;
@@ -528,72 +607,7 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
   for (int ir = 0; ir < IRN; ++ir)
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = CIO ? Cb[ir * ld4 + jr * 16] : 0.0;
-
-  // staging: TR rows of panel i and 128 rows of panel j, KB doubles each; thread tid moves
-  // chunk (tid & 7) of rows (tid >> 3) + 32u
-  static_assert(KB == 16, "staging map assumes 8 double2 chunks per row");
-  constexpr int NUI = TR / 32, NU = NUI + 4;
-  const int srow = tid >> 3, sch = tid & 7;
-  const double* gi = A + (i0 + srow) * lda + kb + 2 * sch;
-  const double* gj = A + (j0 + srow) * lda + kb + 2 * sch;
-  const int ld32 = (int)(32 * lda);
-  double2 pre[NU];
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int u = 0; u < NUI; ++u) pre[u] = *reinterpret_cast<const double2*>(gi + u * ld32 + k0);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) pre[NUI + u] = *reinterpret_cast<const double2*>(gj + u * ld32 + k0);
-  };
-  auto lstore = [&](int b) {
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      double* d = u < NUI ? &sPb[b][0][srow + 32 * u][2 * sch]
-                          : &sPb[b][1][srow + 32 * (u - NUI)][2 * sch];
-      d[0] = pre[u].x;
-      d[1] = pre[u].y;
-    }
-  };
-  auto compute = [&](int b) {
-#pragma unroll 1
-    for (int kk = 0; kk < KB; kk += 4) {
-      double bb[4];
-#pragma unroll
-      for (int jr = 0; jr < 4; ++jr) bb[jr] = sPb[b][1][wc + jr * 16 + li][kk + lk];
-#pragma unroll
-      for (int h = 0; h < IRN / 8; ++h) {
-        double a[8];
-#pragma unroll
-        for (int ir = 0; ir < 8; ++ir) a[ir] = -sPb[b][0][wr + (h * 8 + ir) * 4 + l3][kk + lk];
-#pragma unroll
-        for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-          for (int jr = 0; jr < 4; ++jr)
-            acc[h * 8 + ir][jr] = mfma4(a[ir], bb[jr], acc[h * 8 + ir][jr]);
-      }
-    }
-  };
-
-  gload(0);
-  if (!DB) {
-    for (int k0 = 0; k0 < kd; k0 += KB) {
-      __syncthreads();
-      lstore(0);
-      __syncthreads();
-      if (k0 + KB < kd) gload(k0 + KB);
-      compute(0);
-    }
-  } else {
-    // stage k lives in buffer k & 1; the global loads run one stage ahead in registers
-    lstore(0);
-    if (KB < kd) gload(KB);
-    __syncthreads();
-    for (int k0 = 0, b = 0; k0 < kd; k0 += KB, b ^= 1) {
-      if (k0 + KB < kd) lstore(b ^ 1);
-      if (k0 + 2 * KB < kd) gload(k0 + 2 * KB);
-      compute(b);
-      __syncthreads();
-    }
-  }
+  syrk_accumulate<TR>(A, lda, i0, j0, kb, kd, acc, sP);
 
   int ld4s = ld4;
   asm volatile("" : "+v"(ld4s));  // recompute store addresses instead of keeping 64 pointers live
@@ -605,6 +619,95 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
       if (CIO && (!diag || col <= row)) Cb[ir * ld4s + jr * 16] = acc[ir][jr];
       if (!CIO && acc[ir][jr] == 1.2345e300) Cb[0] = 0.0;  // keep the MFMAs live
     }
+}
+
+// ---------------------------------------------------------- fused panel
+// One block column of the look-ahead chain in one launch (w = 1 steps):
+//   workgroups 0, 1   apply the pending rank-pkd update (panel columns pkb .. pkb + pkd) to the
+//                     two 64-row slabs of the 128 x 128 diagonal block; workgroup 0 then waits
+//                     for both and factors the block (potrf_block);
+//   workgroups >= 2   each apply the pending update to 64 rows below the block, keep them in
+//                     LDS, wait for the factor and solve them (trsm_rows).
+// This replaces band-SYRK -> potrf -> trsm (three dependent launches) and their dispatch gaps.
+// Order across workgroups: device-scope release / acquire on sync[1] (diagonal slabs written,
+// +1 each) and sync[0] (factor written, = epoch). Workgroup 0 is dispatched first, so waiting
+// workgroups never hold the slots it needs; a bounded wait still ends every workgroup (status
+// PANEL_TIMEOUT) rather than hang.
+constexpr int PANEL_TIMEOUT = -2;
+constexpr size_t PANEL_LDS = (size_t)MB_DOUBLES * sizeof(double);
+static_assert(MB_DOUBLES >= 64 * (NB + 1) && MB_DOUBLES >= 2 * ST * (KB + 1), "LDS union");
+
+__device__ __forceinline__ bool wait_counter(unsigned* p, unsigned target) {
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    unsigned it = 0;
+    while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target &&
+           ++it < (1u << 26))
+      __builtin_amdgcn_s_sleep(2);
+    ok = it < (1u << 26);
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return ok;
+}
+
+__global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int64_t lda,
+                                                    int64_t kb, int64_t pkb, int pkd,
+                                                    int64_t npiv, double* __restrict__ dinv,
+                                                    double* __restrict__ parts, int k,
+                                                    int* __restrict__ status,
+                                                    unsigned* __restrict__ sync, unsigned epoch) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = (w >> 1) * 32, wc = (w & 1) * 64;
+  const int li = lane & 15, lk = lane >> 4;
+  const int b = blockIdx.x;
+  const int64_t i0 = b < 2 ? kb + 64 * b : kb + NB + 64 * (int64_t)(b - 2);
+  double* Cb = A + (i0 + wr + lk) * lda + kb + wc + li;  // C[wr + lk][wc + li]
+  const int ld4 = (int)(4 * lda);
+  double acc[8][4];
+#pragma unroll
+  for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = Cb[ir * ld4 + jr * 16];
+  if (pkd > 0)
+    syrk_accumulate<64>(A, lda, i0, kb, pkb, pkd, acc,
+                        reinterpret_cast<double (*)[ST][KB + 1]>(smem));
+  if (b < 2) {
+    // diagonal slab back to the matrix (the part above the diagonal is scratch)
+#pragma unroll
+    for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+      for (int jr = 0; jr < 4; ++jr) Cb[ir * ld4 + jr * 16] = acc[ir][jr];
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (b == 1) return;
+    if (!wait_counter(&sync[1], 2u * epoch)) {
+      if (tid == 0) {
+        atomicMin(status, PANEL_TIMEOUT);
+        __hip_atomic_store(&sync[0], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    potrf_block<15>(smem, A, lda, kb, npiv, dinv, parts, k, status);
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(&sync[0], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  // rows below the block: the solve's 64 x 129 LDS image (aliases the staging buffer)
+  double (*sA)[NB + 1] = reinterpret_cast<double (*)[NB + 1]>(smem);
+  __syncthreads();
+#pragma unroll
+  for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+    for (int jr = 0; jr < 4; ++jr) sA[wr + ir * 4 + lk][wc + jr * 16 + li] = acc[ir][jr];
+  if (!wait_counter(&sync[0], epoch)) {
+    if (tid == 0) atomicMin(status, PANEL_TIMEOUT);
+    return;
+  }
+  trsm_rows(sA, A, lda, i0, kb, dinv);
 }
 
 // ------------------------------------------------------------- finalize
@@ -701,15 +804,26 @@ struct Launcher {
     if (tr == 64)
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3((unsigned)tiles), dim3(256), 0, st, A, lda,
                          s0, kb, kd, (int)T, lo, hi);
-    else if (ctx->syrk_db)
-      hipLaunchKernelGGL((syrk_kernel<true, 128, true>), dim3((unsigned)tiles), dim3(256), 0, st,
-                         A, lda, s0, kb, kd, (int)T, lo, hi);
     else
       hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3((unsigned)tiles), dim3(256), 0, st, A,
                          lda, s0, kb, kd, (int)T, lo, hi);
     prof_end(ctx, K_SYRK, ev, elems * 2.0 * kd, elems * 16.0, st);
   }
   int64_t tiles_from(int64_t s0) const { return (end(s0) - s0) / ST; }
+  // Fused pending-update + factor + solve of block column k (panel_kernel).
+  void panel(hipStream_t st, int64_t k, int64_t pkb, int pkd, int64_t n) {
+    const int64_t kb = k * NB, s = kb + NB;
+    const int64_t rows = std::max<int64_t>(end(s) - s, 0);
+    const unsigned epoch = ++ctx->panel_epoch;
+    hipEvent_t ev;
+    prof_begin(ctx, K_PANEL, &ev, st);
+    hipLaunchKernelGGL(panel_kernel, dim3((unsigned)(2 + rows / 64)), dim3(256), PANEL_LDS, st, A,
+                       lda, kb, pkb, pkd, n, ctx->linvT, ctx->parts, (int)k, ctx->status,
+                       ctx->psync, epoch);
+    prof_end(ctx, K_PANEL, ev,
+             (double)NB * NB * NB / 3.0 + (double)rows * NB * NB + 2.0 * (rows + NB) * NB * pkd,
+             0, st);
+  }
   // Row height of the triangle's work units: 128-row tiles run 2 per CU, 64-row slabs 3 per
   // CU (fewer VGPRs); pick the one with fewer (cost-weighted) rounds of workgroups over the
   // chip, so a triangle just past a multiple of 512 tiles does not leave a mostly idle
@@ -725,6 +839,10 @@ struct Launcher {
   // Factor the super-panel of block columns [k, k + w): per column potrf + trsm, then the
   // update of the super-panel's remaining columns with it (K = 128).
   void superpanel(hipStream_t st, int64_t k, int w, int64_t n) {
+    if (w == 1 && ctx->fused) {
+      panel(st, k, 0, 0, n);
+      return;
+    }
     for (int i = 0; i < w; ++i) {
       potrf(st, k + i, n);
       trsm(st, k + i);
@@ -776,8 +894,7 @@ int probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us) {
 }
 
 // Diagnostic: average duration (us) of one full-lower-triangle SYRK launch over a T x T grid
-// of 128-tiles with update depth kd; cio bit 0 = C tile I/O, bit 1 = double-buffered stages,
-// bit 2 = 64-row slabs (with C I/O).
+// of 128-tiles with update depth kd; cio bit 0 = C tile I/O, bit 2 = 64-row slabs (with C I/O).
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const int64_t n = (int64_t)T * ST + 512;
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
@@ -791,23 +908,12 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
                          (int64_t)512, (int64_t)0, kd, T, 0, T);
       return;
     }
-    switch (cio & 3) {
-      case 1:
-        hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                           (int64_t)512, (int64_t)0, kd, T, 0, T);
-        break;
-      case 0:
-        hipLaunchKernelGGL((syrk_kernel<false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                           (int64_t)512, (int64_t)0, kd, T, 0, T);
-        break;
-      case 3:
-        hipLaunchKernelGGL((syrk_kernel<true, 128, true>), dim3(tiles), dim3(256), 0, st, ctx->A,
-                           n, (int64_t)512, (int64_t)0, kd, T, 0, T);
-        break;
-      default:
-        hipLaunchKernelGGL((syrk_kernel<false, 128, true>), dim3(tiles), dim3(256), 0, st,
-                           ctx->A, n, (int64_t)512, (int64_t)0, kd, T, 0, T);
-    }
+    if (cio & 1)
+      hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
+                         (int64_t)512, (int64_t)0, kd, T, 0, T);
+    else
+      hipLaunchKernelGGL((syrk_kernel<false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
+                         (int64_t)512, (int64_t)0, kd, T, 0, T);
   };
   go();
   hipEvent_t a, b;
@@ -856,6 +962,12 @@ int probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us) {
 
 int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,
                       double* d_out, int mode) {
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&panel_kernel),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)PANEL_LDS);
+    attr = true;
+  }
   // CHOL_MLL: factor the Mp x Mp augmented matrix (block columns holding pivots only).
   // CHOL_INVERSE: A is 2Mp x 2Mp, [[S_aug, .], [I, 0]]; all Mp/NB block columns of the top
   //   are eliminated with every trailing update restricted to the Mp-row window below the
@@ -925,8 +1037,12 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       // side: the next super-panel's columns first (after main's previous bulk update,
       // which wrote the same tiles), then its factorisation
       if (s > 0) hipStreamWaitEvent(side, ev[2 + 2 * (s - 1)], 0);
-      L.syrk(side, s0, k * NB, NB * w, T, 0, wn, 64);
-      L.superpanel(side, steps[s + 1].first, steps[s + 1].second, n);
+      if (wn == 1 && ctx->fused) {
+        L.panel(side, steps[s + 1].first, k * NB, NB * w, n);
+      } else {
+        L.syrk(side, s0, k * NB, NB * w, T, 0, wn, 64);
+        L.superpanel(side, steps[s + 1].first, steps[s + 1].second, n);
+      }
       hipEventRecord(ev[1 + 2 * (s + 1)], side);
     }
   }

@@ -25,6 +25,7 @@ enum KClass {
   K_SMALL,        // one-workgroup-per-problem fused small-N MLL
   K_MEAN,         // mean_function
   K_GRAD,         // MLL gradient: W-weighted kernel-derivative reduction
+  K_PANEL,        // fused pending update + diagonal factor + panel solve (one block column)
   K_NCLASS
 };
 
@@ -56,7 +57,6 @@ struct lfm_ctx {
   hipStream_t side = nullptr;    // high-priority look-ahead stream: panel factor + solve
   bool lookahead = true;
   int trsm_variant = 2;          // panel-solve kernel variant (LFM_TRSM=2|3)
-  int syrk_db = 0;               // double-buffered SYRK stages (LFM_SYRK_DB=1)
   int syrk_tr = 0;               // force SYRK triangle work-unit rows (LFM_SYRK_TR=64|128)
   int cus = 256;                 // compute units of the device
   double slab_cost = 0.75;       // time of a round of 64-row slabs / a round of 128-tiles
@@ -73,6 +73,9 @@ struct lfm_ctx {
   double* linvT = nullptr;                       // 8 x 16x16 inverses of the diagonal sub-blocks
   double* parts = nullptr; size_t parts_cap = 0; // per-block logdet partials
   int* status = nullptr;                         // [0] first failing pivot (INT_MAX = none)
+  unsigned* psync = nullptr;                     // fused panel: [0] factor epoch, [1] slab count
+  unsigned panel_epoch = 0;                      // fused panel launches so far
+  int fused = 1;                                 // fused panel kernel for w = 1 steps (LFM_FUSED)
   double* result = nullptr;                      // [0..] scalar results
   double* gacc = nullptr; size_t gacc_bytes = 0; // gradient accumulators + output
 

@@ -7,10 +7,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dis_project_amd import _lib  # noqa: E402
 
 ctx = _lib.get_context(0)
-# cio: bit 0 = C tile I/O, bit 1 = double-buffered LDS stages
+# cio: bit 0 = C tile I/O, bit 2 = 64-row slabs
 TS = [int(v) for v in os.environ.get("PROBE_T", "126,64,32").split(",")]
 KDS = [int(v) for v in os.environ.get("PROBE_KD", "128,256,512").split(",")]
-CIOS = [int(v) for v in os.environ.get("PROBE_CIO", "1,0,3,2").split(",")]
+CIOS = [int(v) for v in os.environ.get("PROBE_CIO", "1,0,5").split(",")]
 for T in TS:
     for kd in KDS:
         for cio in CIOS:
