@@ -307,6 +307,7 @@ __global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A,
                                                         double* __restrict__ parts, int k,
                                                         int* __restrict__ status) {
   __shared__ double Mb[MB_DOUBLES];
+  __builtin_amdgcn_s_setprio(3);  // critical path: win issue slots over co-resident SYRK waves
   potrf_block<PH>(Mb, A, lda, kb, npiv, dinv, parts, k, status);
 }
 
@@ -469,6 +470,7 @@ __device__ __forceinline__ void trsm_rows(double (*__restrict__ sA)[NB + 1],
 __global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, int64_t lda, int64_t s,
                                                    int64_t kb, const double* __restrict__ dinv) {
   __shared__ double sA[64][NB + 1];
+  __builtin_amdgcn_s_setprio(3);
   const int tid = threadIdx.x;
   const int64_t r0 = s + (int64_t)blockIdx.x * 64;
   for (int idx = tid; idx < 64 * (NB / 2); idx += 256) {
@@ -570,9 +572,10 @@ __device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, in
 template <bool CIO, int TR>
 __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
     double* __restrict__ A, int64_t lda, int64_t s, int64_t kb, int kd, int T, int tj_lo,
-    int tj_hi) {
+    int tj_hi, int prio) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
   __shared__ double sP[2][ST][KB + 1];
+  if (prio) __builtin_amdgcn_s_setprio(2);  // look-ahead bands: ahead of the bulk update
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
   const int li = lane & 15, lk = lane >> 4;
@@ -658,6 +661,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
                                                     int* __restrict__ status,
                                                     unsigned* __restrict__ sync, unsigned epoch) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
+  __builtin_amdgcn_s_setprio(3);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * 32, wc = (w & 1) * 64;
   const int li = lane & 15, lk = lane >> 4;
@@ -784,7 +788,8 @@ struct Launcher {
   }
   // Trailing update of tile columns [lo, hi) of the matrix starting at s0 (T = 128-tiles)
   // with panel columns kb .. kb + kd. tr = 64 (latency-critical narrow bands) or 128.
-  void syrk(hipStream_t st, int64_t s0, int64_t kb, int kd, int64_t T, int lo, int hi, int tr) {
+  void syrk(hipStream_t st, int64_t s0, int64_t kb, int kd, int64_t T, int lo, int hi, int tr,
+            int prio = 0) {
     if (T <= 0 || hi <= lo) return;
     hi = (int)std::min<int64_t>(hi, T);
     const bool band = hi - lo <= 8;
@@ -803,10 +808,10 @@ struct Launcher {
     prof_begin(ctx, K_SYRK, &ev, st);
     if (tr == 64)
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3((unsigned)tiles), dim3(256), 0, st, A, lda,
-                         s0, kb, kd, (int)T, lo, hi);
+                         s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask);
     else
       hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3((unsigned)tiles), dim3(256), 0, st, A,
-                         lda, s0, kb, kd, (int)T, lo, hi);
+                         lda, s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask);
     prof_end(ctx, K_SYRK, ev, elems * 2.0 * kd, elems * 16.0, st);
   }
   int64_t tiles_from(int64_t s0) const { return (end(s0) - s0) / ST; }
@@ -848,7 +853,7 @@ struct Launcher {
       trsm(st, k + i);
       if (i + 1 < w) {
         const int64_t s0 = (k + i + 1) * NB;
-        syrk(st, s0, (k + i) * NB, NB, tiles_from(s0), 0, w - 1 - i, 64);
+        syrk(st, s0, (k + i) * NB, NB, tiles_from(s0), 0, w - 1 - i, 64, 1);
       }
     }
   }
@@ -905,15 +910,15 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   auto go = [&]() {
     if (cio & 4) {  // 64-row slabs, C I/O
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(2 * tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T);
+                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0);
       return;
     }
     if (cio & 1)
       hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T);
+                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0);
     else
       hipLaunchKernelGGL((syrk_kernel<false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T);
+                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0);
   };
   go();
   hipEvent_t a, b;
@@ -1040,7 +1045,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       if (wn == 1 && ctx->fused) {
         L.panel(side, steps[s + 1].first, k * NB, NB * w, n);
       } else {
-        L.syrk(side, s0, k * NB, NB * w, T, 0, wn, 64);
+        L.syrk(side, s0, k * NB, NB * w, T, 0, wn, 64, 1);
         L.superpanel(side, steps[s + 1].first, steps[s + 1].second, n);
       }
       hipEventRecord(ev[1 + 2 * (s + 1)], side);
