@@ -572,7 +572,7 @@ __device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, in
 template <bool CIO, int TR>
 __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
     double* __restrict__ A, int64_t lda, int64_t s, int64_t kb, int kd, int T, int tj_lo,
-    int tj_hi, int prio) {
+    int tj_hi, int prio, int xcd_remap) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
   __shared__ double sP[2][ST][KB + 1];
   if (prio) __builtin_amdgcn_s_setprio(2);  // look-ahead bands: ahead of the bulk update
@@ -591,7 +591,14 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
     }
     ti = SUB * tj + (int)b;
   } else {
-    // triangle of 128-tiles over tile columns [tj_lo, T), SUB row slabs of TR rows per tile
+    // triangle of 128-tiles over tile columns [tj_lo, T), SUB row slabs of TR rows per tile.
+    // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (each with its own L2),
+    // so give XCD x the contiguous range x*q .. of the enumeration (bijective remap): the
+    // workgroups resident on one XCD then share panel rows instead of striding over them.
+    if (xcd_remap) {
+      const int64_t nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = b % 8;
+      b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+    }
     const int sub = (int)(b % SUB);
     b /= SUB;
     int a = (int)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
@@ -808,10 +815,10 @@ struct Launcher {
     prof_begin(ctx, K_SYRK, &ev, st);
     if (tr == 64)
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3((unsigned)tiles), dim3(256), 0, st, A, lda,
-                         s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask);
+                         s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask, ctx->xcd_remap);
     else
       hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3((unsigned)tiles), dim3(256), 0, st, A,
-                         lda, s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask);
+                         lda, s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask, ctx->xcd_remap);
     prof_end(ctx, K_SYRK, ev, elems * 2.0 * kd, elems * 16.0, st);
   }
   int64_t tiles_from(int64_t s0) const { return (end(s0) - s0) / ST; }
@@ -910,15 +917,15 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   auto go = [&]() {
     if (cio & 4) {  // 64-row slabs, C I/O
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(2 * tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0);
+                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0, ctx->xcd_remap);
       return;
     }
     if (cio & 1)
       hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0);
+                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0, ctx->xcd_remap);
     else
       hipLaunchKernelGGL((syrk_kernel<false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0);
+                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0, ctx->xcd_remap);
   };
   go();
   hipEvent_t a, b;
