@@ -420,7 +420,7 @@ namespace {
 // relies on the side stream's higher priority. LFM_LOOKAHEAD=0 serialises on one stream.
 hipError_t create_streams(lfm_ctx* ctx) {
   const char* xr = std::getenv("LFM_XCD_REMAP");
-  ctx->xcd_remap = xr ? std::atoi(xr) : 0;
+  ctx->xcd_remap = xr ? std::atoi(xr) : 1;
   const char* bp = std::getenv("LFM_BAND_PRIO");
   ctx->prio_mask = bp ? std::atoi(bp) : 1;
   const char* fv = std::getenv("LFM_FUSED");

@@ -509,7 +509,8 @@ __global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, in
 #define LFM_SLAB_WGS 3
 #endif
 // acc[ir][jr] (C[wr + ir*4 + (lane>>4)][wc + jr*16 + (lane&15)] of a TR x 128 block at rows
-// i0, cols j0; waves as 2 x 2) -= P_i P_j^T over panel columns kb .. kb + kd. sP: LDS staging,
+// i0, cols j0; waves as 2 x 2) += P_i P_j^T over panel columns kb .. kb + kd — callers hold
+// -C in acc (negated once at load / store instead of per fragment). sP: LDS staging,
 // [2][ST][KB + 1] doubles. Every thread of the (256-thread) workgroup must call it.
 template <int TR>
 __device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, int64_t lda,
@@ -530,10 +531,13 @@ __device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, in
   const int ld32 = (int)(32 * lda);
   double2 pre[NU];
   auto gload = [&](int k0) {
+    // row offsets recomputed per call (opaque stride) rather than held as live 64-bit pointers
+    int l32 = ld32;
+    asm volatile("" : "+v"(l32));
 #pragma unroll
-    for (int u = 0; u < NUI; ++u) pre[u] = *reinterpret_cast<const double2*>(gi + u * ld32 + k0);
+    for (int u = 0; u < NUI; ++u) pre[u] = *reinterpret_cast<const double2*>(gi + u * l32 + k0);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) pre[NUI + u] = *reinterpret_cast<const double2*>(gj + u * ld32 + k0);
+    for (int u = 0; u < 4; ++u) pre[NUI + u] = *reinterpret_cast<const double2*>(gj + u * l32 + k0);
   };
   gload(0);
   for (int k0 = 0; k0 < kd; k0 += KB) {
@@ -546,21 +550,43 @@ __device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, in
     }
     __syncthreads();
     if (k0 + KB < kd) gload(k0 + KB);
-#pragma unroll 1
-    for (int kk = 0; kk < KB; kk += 4) {
-      double bb[4];
+    if constexpr (IRN == 8) {
+      // 64-row slabs: the fragments of step kk + 4 are read from LDS while step kk's MFMAs
+      // issue (two register sets), so the waves do not stall on each LDS round trip
+      double bb[2][4], a[2][8];
+      auto frag = [&](int kk, int q) {
 #pragma unroll
-      for (int jr = 0; jr < 4; ++jr) bb[jr] = sP[1][wc + jr * 16 + li][kk + lk];
+        for (int jr = 0; jr < 4; ++jr) bb[q][jr] = sP[1][wc + jr * 16 + li][kk + lk];
 #pragma unroll
-      for (int h = 0; h < IRN / 8; ++h) {
-        double a[8];
+        for (int ir = 0; ir < 8; ++ir) a[q][ir] = sP[0][wr + ir * 4 + l3][kk + lk];
+      };
+      frag(0, 0);
 #pragma unroll
-        for (int ir = 0; ir < 8; ++ir) a[ir] = -sP[0][wr + (h * 8 + ir) * 4 + l3][kk + lk];
+      for (int kk = 0; kk < KB; kk += 4) {
+        const int q = (kk >> 2) & 1;
+        if (kk + 4 < KB) frag(kk + 4, q ^ 1);
 #pragma unroll
         for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
-          for (int jr = 0; jr < 4; ++jr)
-            acc[h * 8 + ir][jr] = mfma4(a[ir], bb[jr], acc[h * 8 + ir][jr]);
+          for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = mfma4(a[q][ir], bb[q][jr], acc[ir][jr]);
+      }
+    } else {
+#pragma unroll 1
+      for (int kk = 0; kk < KB; kk += 4) {
+        double bb[4];
+#pragma unroll
+        for (int jr = 0; jr < 4; ++jr) bb[jr] = sP[1][wc + jr * 16 + li][kk + lk];
+#pragma unroll
+        for (int h = 0; h < IRN / 8; ++h) {
+          double a[8];
+#pragma unroll
+          for (int ir = 0; ir < 8; ++ir) a[ir] = sP[0][wr + (h * 8 + ir) * 4 + l3][kk + lk];
+#pragma unroll
+          for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+            for (int jr = 0; jr < 4; ++jr)
+              acc[h * 8 + ir][jr] = mfma4(a[ir], bb[jr], acc[h * 8 + ir][jr]);
+        }
       }
     }
   }
@@ -616,7 +642,7 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
 #pragma unroll
   for (int ir = 0; ir < IRN; ++ir)
 #pragma unroll
-    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = CIO ? Cb[ir * ld4 + jr * 16] : 0.0;
+    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = CIO ? -Cb[ir * ld4 + jr * 16] : 0.0;
   syrk_accumulate<TR>(A, lda, i0, j0, kb, kd, acc, sP);
 
   int ld4s = ld4;
@@ -626,7 +652,7 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) {
       const int64_t row = i0 + wr + ir * 4 + lk, col = j0 + wc + jr * 16 + li;
-      if (CIO && (!diag || col <= row)) Cb[ir * ld4s + jr * 16] = acc[ir][jr];
+      if (CIO && (!diag || col <= row)) Cb[ir * ld4s + jr * 16] = -acc[ir][jr];
       if (!CIO && acc[ir][jr] == 1.2345e300) Cb[0] = 0.0;  // keep the MFMAs live
     }
 }
@@ -680,7 +706,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
 #pragma unroll
   for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
-    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = Cb[ir * ld4 + jr * 16];
+    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = -Cb[ir * ld4 + jr * 16];
   if (pkd > 0)
     syrk_accumulate<64>(A, lda, i0, kb, pkb, pkd, acc,
                         reinterpret_cast<double (*)[ST][KB + 1]>(smem));
@@ -689,7 +715,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
 #pragma unroll
     for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
-      for (int jr = 0; jr < 4; ++jr) Cb[ir * ld4 + jr * 16] = acc[ir][jr];
+      for (int jr = 0; jr < 4; ++jr) Cb[ir * ld4 + jr * 16] = -acc[ir][jr];
     __threadfence();
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -713,7 +739,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
 #pragma unroll
   for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
-    for (int jr = 0; jr < 4; ++jr) sA[wr + ir * 4 + lk][wc + jr * 16 + li] = acc[ir][jr];
+    for (int jr = 0; jr < 4; ++jr) sA[wr + ir * 4 + lk][wc + jr * 16 + li] = -acc[ir][jr];
   if (!wait_counter(&sync[0], epoch)) {
     if (tid == 0) atomicMin(status, PANEL_TIMEOUT);
     return;
