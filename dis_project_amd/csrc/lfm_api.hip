@@ -419,6 +419,8 @@ namespace {
 // the main stream off them (hipExtStreamCreateWithCUMask); 0 (default) shares every CU and
 // relies on the side stream's higher priority. LFM_LOOKAHEAD=0 serialises on one stream.
 hipError_t create_streams(lfm_ctx* ctx) {
+  const char* pk = std::getenv("LFM_SYRK_PAD_KB");
+  ctx->syrk_pad_kb = pk ? std::atoi(pk) : 0;
   const char* xr = std::getenv("LFM_XCD_REMAP");
   ctx->xcd_remap = xr ? std::atoi(xr) : 1;
   const char* bp = std::getenv("LFM_BAND_PRIO");

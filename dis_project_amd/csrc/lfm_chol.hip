@@ -550,27 +550,7 @@ __device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, in
     }
     __syncthreads();
     if (k0 + KB < kd) gload(k0 + KB);
-    if constexpr (IRN == 8) {
-      // 64-row slabs: the fragments of step kk + 4 are read from LDS while step kk's MFMAs
-      // issue (two register sets), so the waves do not stall on each LDS round trip
-      double bb[2][4], a[2][8];
-      auto frag = [&](int kk, int q) {
-#pragma unroll
-        for (int jr = 0; jr < 4; ++jr) bb[q][jr] = sP[1][wc + jr * 16 + li][kk + lk];
-#pragma unroll
-        for (int ir = 0; ir < 8; ++ir) a[q][ir] = sP[0][wr + ir * 4 + l3][kk + lk];
-      };
-      frag(0, 0);
-#pragma unroll
-      for (int kk = 0; kk < KB; kk += 4) {
-        const int q = (kk >> 2) & 1;
-        if (kk + 4 < KB) frag(kk + 4, q ^ 1);
-#pragma unroll
-        for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-          for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = mfma4(a[q][ir], bb[q][jr], acc[ir][jr]);
-      }
-    } else {
+    {
 #pragma unroll 1
       for (int kk = 0; kk < KB; kk += 4) {
         double bb[4];
@@ -840,7 +820,8 @@ struct Launcher {
     hipEvent_t ev;
     prof_begin(ctx, K_SYRK, &ev, st);
     if (tr == 64)
-      hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3((unsigned)tiles), dim3(256), 0, st, A, lda,
+      hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3((unsigned)tiles), dim3(256),
+                         (size_t)ctx->syrk_pad_kb * 1024, st, A, lda,
                          s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask, ctx->xcd_remap);
     else
       hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3((unsigned)tiles), dim3(256), 0, st, A,

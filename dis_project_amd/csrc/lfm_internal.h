@@ -76,6 +76,7 @@ struct lfm_ctx {
   unsigned* psync = nullptr;                     // fused panel: [0] factor epoch, [1] slab count
   unsigned panel_epoch = 0;                      // fused panel launches so far
   int fused = 1;                                 // fused panel kernel for w = 1 steps (LFM_FUSED)
+  int syrk_pad_kb = 0;                           // extra LDS per slab workgroup: caps residency (LFM_SYRK_PAD_KB)
   int xcd_remap = 1;                             // XCD-contiguous SYRK tile order (LFM_XCD_REMAP)
   int prio_mask = 1;                             // raise look-ahead SYRK band wave priority (LFM_BAND_PRIO)
   double* result = nullptr;                      // [0..] scalar results
