@@ -452,7 +452,23 @@ hipError_t create_streams(lfm_ctx* ctx) {
     if (e != hipSuccess) return e;
     return hipExtStreamCreateWithCUMask(&ctx->side, (uint32_t)mside.size(), mside.data());
   }
-  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  // LFM_MAIN_EXCLUDE=c (> 0): the main stream (bulk trailing updates) stays off c CUs spread
+  // over the device; the look-ahead stream may use every CU, so its latency-bound kernels
+  // always find free slots instead of waiting for bulk workgroups to drain.
+  const char* mx = std::getenv("LFM_MAIN_EXCLUDE");
+  const int excl = mx ? std::atoi(mx) : 0;
+  hipError_t e;
+  if (excl > 0 && excl < ncu) {
+    std::vector<uint32_t> mmain((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; ++c) mmain[c / 32] |= 1u << (c % 32);
+    for (int j = 0; j < excl; ++j) {
+      const int c = (int)((int64_t)j * ncu / excl);
+      mmain[c / 32] &= ~(1u << (c % 32));
+    }
+    e = hipExtStreamCreateWithCUMask(&ctx->stream, (uint32_t)mmain.size(), mmain.data());
+  } else {
+    e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  }
   if (e != hipSuccess) return e;
   return hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest);
 }
