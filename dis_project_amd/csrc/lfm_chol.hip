@@ -136,18 +136,21 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
 #define MS(r, q) Mb[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * (IB * (IB + 1)) + \
                     ((r) & 15) * (IB + 1) + ((q) & 15)]
 
-  // block load: row r, 16-B chunks; all 32 loads of a thread issued before any LDS write
-  {
-    double2 v[32];
+  // block load: row r, 16-B chunks of the lower 16x16 blocks; two batches of 16 loads per
+  // thread in flight (64 VGPRs), so the kernel fits in one bulk-SYRK workgroup's registers
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      const int idx = tid + 256 * u, r = idx >> 6, c2 = idx & 63;
-      v[u] = (PH & 8) ? *reinterpret_cast<const double2*>(&A[(kb + r) * lda + kb + 2 * c2])
-                      : double2{(r == 2 * c2) ? 2.0 : 0.0, (r == 2 * c2 + 1) ? 2.0 : 0.0};
+  for (int hb = 0; hb < 2; ++hb) {
+    double2 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int idx = tid + 256 * (u + 16 * hb), r = idx >> 6, c2 = idx & 63;
+      if ((2 * c2) >> 4 <= r >> 4)
+        v[u] = (PH & 8) ? *reinterpret_cast<const double2*>(&A[(kb + r) * lda + kb + 2 * c2])
+                        : double2{(r == 2 * c2) ? 2.0 : 0.0, (r == 2 * c2 + 1) ? 2.0 : 0.0};
     }
 #pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      const int idx = tid + 256 * u, r = idx >> 6, c2 = idx & 63;
+    for (int u = 0; u < 16; ++u) {
+      const int idx = tid + 256 * (u + 16 * hb), r = idx >> 6, c2 = idx & 63;
       if ((2 * c2) >> 4 <= r >> 4) {
         MS(r, 2 * c2) = v[u].x;
         MS(r, 2 * c2 + 1) = v[u].y;
@@ -156,6 +159,7 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
   }
   __syncthreads();
 
+#pragma unroll 1
   for (int ib = 0; ib < NB / IB; ++ib) {
     const int c0 = ib * IB;
     if ((PH & 1) && w == 0) {
@@ -178,12 +182,16 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
         for (int q = 0; q < IB; ++q)
           if (q <= lane) MS(c0 + lane, c0 + q) = d[q];
       }
-      if (lane == 0) {
+      // the pivots are wave-uniform after the broadcasts: lane c keeps pivot c
+      double pvl = 0.0, yvl = 0.0;
 #pragma unroll
-        for (int c = 0; c < IB; ++c) {
-          pvs[c0 + c] = pv[c];
-          ipv[c0 + c] = yv[c];
-        }
+      for (int c = 0; c < IB; ++c) {
+        pvl = (lane == c) ? pv[c] : pvl;
+        yvl = (lane == c) ? yv[c] : yvl;
+      }
+      if (lane < IB) {
+        pvs[c0 + lane] = pvl;
+        ipv[c0 + lane] = yvl;
       }
     }
     __syncthreads();
@@ -300,13 +308,16 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
 #undef MS
 }
 
+// (256, 4): at most 128 VGPRs, so the factor fits in the registers one bulk-SYRK workgroup frees
+// The block lives in dynamic LDS (MB_DOUBLES doubles, set at launch) so the occupancy target
+// (4 waves / SIMD) holds at compile time and caps the kernel at 128 VGPRs.
 template <int PH>
-__global__ __launch_bounds__(256) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
-                                                        int64_t kb, int64_t npiv,
-                                                        double* __restrict__ dinv,
-                                                        double* __restrict__ parts, int k,
-                                                        int* __restrict__ status) {
-  __shared__ double Mb[MB_DOUBLES];
+__global__ __launch_bounds__(256, 4) void potrf_diag_kernel(double* __restrict__ A, int64_t lda,
+                                                           int64_t kb, int64_t npiv,
+                                                           double* __restrict__ dinv,
+                                                           double* __restrict__ parts, int k,
+                                                           int* __restrict__ status) {
+  extern __shared__ __attribute__((aligned(16))) double Mb[];
   __builtin_amdgcn_s_setprio(3);  // critical path: win issue slots over co-resident SYRK waves
   potrf_block<PH>(Mb, A, lda, kb, npiv, dinv, parts, k, status);
 }
@@ -511,12 +522,13 @@ __global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, in
 // acc[ir][jr] (C[wr + ir*4 + (lane>>4)][wc + jr*16 + (lane&15)] of a TR x 128 block at rows
 // i0, cols j0; waves as 2 x 2) += P_i P_j^T over panel columns kb .. kb + kd — callers hold
 // -C in acc (negated once at load / store instead of per fragment). sP: LDS staging,
-// [2][ST][KB + 1] doubles. Every thread of the (256-thread) workgroup must call it.
+// (TR + ST) rows of KB + 1 doubles: rows [0, TR) panel i, rows [TR, TR + ST) panel j.
+// Every thread of the (256-thread) workgroup must call it.
 template <int TR>
 __device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, int64_t lda,
                                                 int64_t i0, int64_t j0, int64_t kb, int kd,
                                                 double (&acc)[TR / 8][4],
-                                                double (*__restrict__ sP)[ST][KB + 1]) {
+                                                double (*__restrict__ sP)[KB + 1]) {
   constexpr int IRN = TR / 8;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
@@ -544,7 +556,7 @@ __device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, in
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
-      double* d = u < NUI ? &sP[0][srow + 32 * u][2 * sch] : &sP[1][srow + 32 * (u - NUI)][2 * sch];
+      double* d = &sP[u < NUI ? srow + 32 * u : TR + srow + 32 * (u - NUI)][2 * sch];
       d[0] = pre[u].x;
       d[1] = pre[u].y;
     }
@@ -555,12 +567,12 @@ __device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, in
       for (int kk = 0; kk < KB; kk += 4) {
         double bb[4];
 #pragma unroll
-        for (int jr = 0; jr < 4; ++jr) bb[jr] = sP[1][wc + jr * 16 + li][kk + lk];
+        for (int jr = 0; jr < 4; ++jr) bb[jr] = sP[TR + wc + jr * 16 + li][kk + lk];
 #pragma unroll
         for (int h = 0; h < IRN / 8; ++h) {
           double a[8];
 #pragma unroll
-          for (int ir = 0; ir < 8; ++ir) a[ir] = sP[0][wr + (h * 8 + ir) * 4 + l3][kk + lk];
+          for (int ir = 0; ir < 8; ++ir) a[ir] = sP[wr + (h * 8 + ir) * 4 + l3][kk + lk];
 #pragma unroll
           for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
@@ -580,7 +592,7 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
     double* __restrict__ A, int64_t lda, int64_t s, int64_t kb, int kd, int T, int tj_lo,
     int tj_hi, int prio, int xcd_remap) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
-  __shared__ double sP[2][ST][KB + 1];
+  __shared__ double sP[TR + ST][KB + 1];
   if (prio) __builtin_amdgcn_s_setprio(2);  // look-ahead bands: ahead of the bulk update
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
@@ -651,7 +663,7 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
 // PANEL_TIMEOUT) rather than hang.
 constexpr int PANEL_TIMEOUT = -2;
 constexpr size_t PANEL_LDS = (size_t)MB_DOUBLES * sizeof(double);
-static_assert(MB_DOUBLES >= 64 * (NB + 1) && MB_DOUBLES >= 2 * ST * (KB + 1), "LDS union");
+static_assert(MB_DOUBLES >= 64 * (NB + 1) && MB_DOUBLES >= (64 + ST) * (KB + 1), "LDS union");
 
 __device__ __forceinline__ bool wait_counter(unsigned* p, unsigned target) {
   __shared__ int ok;
@@ -689,7 +701,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
     for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = -Cb[ir * ld4 + jr * 16];
   if (pkd > 0)
     syrk_accumulate<64>(A, lda, i0, kb, pkb, pkd, acc,
-                        reinterpret_cast<double (*)[ST][KB + 1]>(smem));
+                        reinterpret_cast<double (*)[KB + 1]>(smem));
   if (b < 2) {
     // diagonal slab back to the matrix (the part above the diagonal is scratch)
 #pragma unroll
@@ -781,7 +793,8 @@ struct Launcher {
   void potrf(hipStream_t st, int64_t k, int64_t n) {
     hipEvent_t ev;
     prof_begin(ctx, K_POTRF, &ev, st);
-    hipLaunchKernelGGL(potrf_diag_kernel<15>, dim3(1), dim3(256), 0, st, A, lda, k * NB, n,
+    hipLaunchKernelGGL(potrf_diag_kernel<15>, dim3(1), dim3(256), MB_DOUBLES * sizeof(double), st,
+                       A, lda, k * NB, n,
                        ctx->linvT, ctx->parts, (int)k, ctx->status);
     prof_end(ctx, K_POTRF, ev, (double)NB * NB * NB / 3.0, 0, st);
   }
@@ -889,7 +902,10 @@ int probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us) {
   hipStream_t st = ctx->stream;
   auto launch = [&](int m) {
     switch (m & 15) {
-#define LFM_PH(v) case v: hipLaunchKernelGGL(potrf_diag_kernel<v>, dim3(1), dim3(256), 0, st, \
+#define LFM_PH(v) case v: hipFuncSetAttribute(reinterpret_cast<const void*>(&potrf_diag_kernel<v>), \
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                             (int)(MB_DOUBLES * sizeof(double))); \
+                            hipLaunchKernelGGL(potrf_diag_kernel<v>, dim3(1), dim3(256), MB_DOUBLES * sizeof(double), st, \
                                               ctx->A, (int64_t)NB, (int64_t)0, (int64_t)NB, ctx->linvT, ctx->parts, 0, ctx->status); break;
       LFM_PH(0) LFM_PH(1) LFM_PH(2) LFM_PH(3) LFM_PH(4) LFM_PH(5) LFM_PH(6) LFM_PH(7)
       LFM_PH(8) LFM_PH(9) LFM_PH(10) LFM_PH(11) LFM_PH(12) LFM_PH(13) LFM_PH(14) LFM_PH(15)
@@ -985,6 +1001,9 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   if (!attr) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&panel_kernel),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)PANEL_LDS);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&potrf_diag_kernel<15>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)(MB_DOUBLES * sizeof(double)));
     attr = true;
   }
   // CHOL_MLL: factor the Mp x Mp augmented matrix (block columns holding pivots only).
