@@ -1,19 +1,23 @@
 #!/bin/bash
 # Round profile set (run on the GPU box from the repo root):
-#   1. bench.py (default workload, with the CPU baseline)            -> gpurun_out/bench.json
-#   2. rocprofv3 --kernel-trace --stats of a short bench            -> gpurun_out/prof_trace/
-#   3. two PMC passes (FETCH_SIZE, WRITE_SIZE), counters only       -> gpurun_out/prof_fetch|prof_write/
-# Each GPU step has its own time limit; the script stops at the first failure.
+#   1. rocprofv3 --kernel-trace --stats of a short bench            -> gpurun_out/prof_trace/
+#   2. two PMC passes (FETCH_SIZE, WRITE_SIZE), counters only       -> gpurun_out/prof_fetch|prof_write/
+#   3. summarize_profile.py: profiles/syrk_traffic.json (read by bench.py's roofline.traffic)
+#   4. bench.py (default workload, with the CPU baseline)            -> gpurun_out/bench_<R>.json
+# Each GPU step has its own time limit; the script stops at the first failure. Afterwards run
+# `python scripts/summarize_profile.py <R> gpurun_out/bench_<R>.json` in the container to
+# regenerate the same profiles/ files from the merged gpurun_out/.
 set -u
 export TMPDIR=/tmp
 R=${1:-r01}
 STEPS=${STEPS:-10}
-scripts/gpu_step.sh bench 600 python bench.py --steps $STEPS --warmup 2 || exit $?
-grep '^{' gpurun_out/bench.log | tail -1 > gpurun_out/bench_$R.json
 scripts/gpu_step.sh prof_trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace \
   -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $?
 scripts/gpu_step.sh prof_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch \
   -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile || exit $?
 scripts/gpu_step.sh prof_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write \
   -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile || exit $?
+python scripts/summarize_profile.py $R > gpurun_out/summary_pre.log 2>&1 || exit $?
+scripts/gpu_step.sh bench 600 python bench.py --steps $STEPS --warmup 2 || exit $?
+grep '^{' gpurun_out/bench.log | tail -1 > gpurun_out/bench_$R.json
 echo done
