@@ -425,6 +425,8 @@ hipError_t create_streams(lfm_ctx* ctx) {
   ctx->xcd_remap = xr ? std::atoi(xr) : 1;
   const char* bp = std::getenv("LFM_BAND_PRIO");
   ctx->prio_mask = bp ? std::atoi(bp) : 1;
+  const char* sv = std::getenv("LFM_SCHED");
+  ctx->sched = sv ? std::atoi(sv) : 1;
   const char* fv = std::getenv("LFM_FUSED");
   ctx->fused = fv ? std::atoi(fv) : 1;
   const char* trv = std::getenv("LFM_SYRK_TR");

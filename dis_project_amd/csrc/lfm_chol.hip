@@ -590,7 +590,7 @@ __device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, in
 template <bool CIO, int TR>
 __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
     double* __restrict__ A, int64_t lda, int64_t s, int64_t kb, int kd, int T, int tj_lo,
-    int tj_hi, int prio, int xcd_remap) {
+    int tj_hi, int prio, int xcd_remap, int ti0) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
   __shared__ double sP[TR + ST][KB + 1];
   if (prio) __builtin_amdgcn_s_setprio(2);  // look-ahead bands: ahead of the bulk update
@@ -602,12 +602,13 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
   int64_t b = blockIdx.x;
   int ti, tj;  // ti in TR-row units
   if (tj_hi - tj_lo <= 8) {
+    // band: tile columns [tj_lo, tj_hi), tile rows max(tj, ti0) .. T - 1
     tj = tj_lo;
-    while (b >= (int64_t)SUB * (T - tj)) {
-      b -= (int64_t)SUB * (T - tj);
+    while (b >= (int64_t)SUB * max(0, T - max(tj, ti0))) {
+      b -= (int64_t)SUB * max(0, T - max(tj, ti0));
       ++tj;
     }
-    ti = SUB * tj + (int)b;
+    ti = SUB * max(tj, ti0) + (int)b;
   } else {
     // triangle of 128-tiles over tile columns [tj_lo, T), SUB row slabs of TR rows per tile.
     // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (each with its own L2),
@@ -790,13 +791,22 @@ struct Launcher {
   int64_t Mp;   // rows of the (augmented) matrix being factored
   int64_t win;  // 0: trailing rows run to Mp; > 0: rows [s, s + win) only (bordered inverse)
   int64_t end(int64_t s) const { return win ? s + win : Mp; }
-  void potrf(hipStream_t st, int64_t k, int64_t n) {
+  void potrf(hipStream_t st, int64_t k, int64_t n, double* dinv = nullptr) {
     hipEvent_t ev;
     prof_begin(ctx, K_POTRF, &ev, st);
     hipLaunchKernelGGL(potrf_diag_kernel<15>, dim3(1), dim3(256), MB_DOUBLES * sizeof(double), st,
-                       A, lda, k * NB, n,
-                       ctx->linvT, ctx->parts, (int)k, ctx->status);
+                       A, lda, k * NB, n, dinv ? dinv : ctx->linvT, ctx->parts, (int)k,
+                       ctx->status);
     prof_end(ctx, K_POTRF, ev, (double)NB * NB * NB / 3.0, 0, st);
+  }
+  // Panel solve of block column k over rows [r0, r0 + rows) with the diagonal inverses dinv.
+  void trsm_rows(hipStream_t st, int64_t k, int64_t r0, int64_t rows, const double* dinv) {
+    if (rows <= 0) return;
+    hipEvent_t ev;
+    prof_begin(ctx, K_TRSM, &ev, st);
+    hipLaunchKernelGGL(trsm_kernel_v2, dim3((unsigned)(rows / 64)), dim3(256), 0, st, A, lda, r0,
+                       k * NB, dinv);
+    prof_end(ctx, K_TRSM, ev, (double)rows * NB * NB, 2.0 * rows * NB * 8, st);
   }
   void trsm(hipStream_t st, int64_t k) {
     const int64_t s = (k + 1) * NB;
@@ -814,31 +824,37 @@ struct Launcher {
   }
   // Trailing update of tile columns [lo, hi) of the matrix starting at s0 (T = 128-tiles)
   // with panel columns kb .. kb + kd. tr = 64 (latency-critical narrow bands) or 128.
+  // ti0 (band launches only): first tile row, so a band can skip the rows of a diagonal block.
   void syrk(hipStream_t st, int64_t s0, int64_t kb, int kd, int64_t T, int lo, int hi, int tr,
-            int prio = 0) {
+            int prio = 0, int ti0 = 0) {
     if (T <= 0 || hi <= lo) return;
     hi = (int)std::min<int64_t>(hi, T);
     const bool band = hi - lo <= 8;
     if (!band) {
       hi = (int)T;
       tr = tile_rows(T - lo);
+      ti0 = 0;
     }
     const int sub = ST / tr;
     int64_t tiles = 0;
     double elems = 0;
     for (int tj = lo; tj < hi; ++tj) {
-      tiles += (int64_t)sub * (T - tj);
-      elems += (double)(T - tj - 1) * ST * ST + (double)ST * (ST + 1) / 2;
+      const int r0 = std::max(tj, ti0);
+      if (r0 >= T) continue;
+      tiles += (int64_t)sub * (T - r0);
+      elems += r0 > tj ? (double)(T - r0) * ST * ST
+                       : (double)(T - tj - 1) * ST * ST + (double)ST * (ST + 1) / 2;
     }
+    if (tiles == 0) return;
     hipEvent_t ev;
     prof_begin(ctx, K_SYRK, &ev, st);
     if (tr == 64)
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3((unsigned)tiles), dim3(256),
                          (size_t)ctx->syrk_pad_kb * 1024, st, A, lda,
-                         s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask, ctx->xcd_remap);
+                         s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask, ctx->xcd_remap, ti0);
     else
       hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3((unsigned)tiles), dim3(256), 0, st, A,
-                         lda, s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask, ctx->xcd_remap);
+                         lda, s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask, ctx->xcd_remap, ti0);
     prof_end(ctx, K_SYRK, ev, elems * 2.0 * kd, elems * 16.0, st);
   }
   int64_t tiles_from(int64_t s0) const { return (end(s0) - s0) / ST; }
@@ -867,6 +883,33 @@ struct Launcher {
     const double r128 = (double)((tiles + 2 * ctx->cus - 1) / (2 * ctx->cus));
     const double r64 = (double)((2 * tiles + 3 * ctx->cus - 1) / (3 * ctx->cus));
     return r64 * ctx->slab_cost < r128 ? 64 : 128;
+  }
+  // Schedule 2, side stream: factor the diagonal block of super-panel [k, k + w) only (rows
+  // below (k + w) NB untouched): per column potrf into dinv slot c, the solve of the block's
+  // rows below it, and the update of the block's remaining columns.
+  void diag_factor(hipStream_t st, int64_t k, int w, int64_t n) {
+    const int64_t K1 = (k + w) * NB;
+    for (int c = 0; c < w; ++c) {
+      double* dv = ctx->linvT + (size_t)c * NB * IB;  // 8 x 16 x 16 inverses per column
+      potrf(st, k + c, n, dv);
+      if (c + 1 < w) {
+        const int64_t r0 = (k + c + 1) * NB;
+        trsm_rows(st, k + c, r0, K1 - r0, dv);
+        syrk(st, r0, (k + c) * NB, NB, w - 1 - c, 0, w - 1 - c, 64, 1);
+      }
+    }
+  }
+  // Schedule 2, main stream: the tall part of super-panel [k, k + w) — rows below its diagonal
+  // block, solved column by column with the band update of the super-panel's later columns.
+  void tall_solve(hipStream_t st, int64_t k, int w) {
+    const int64_t K1 = (k + w) * NB;
+    for (int c = 0; c < w; ++c) {
+      const double* dv = ctx->linvT + (size_t)c * NB * IB;
+      const int64_t sc = (k + c + 1) * NB;  // rows below block column k + c start here
+      trsm_rows(st, k + c, K1, end(sc) - K1, dv);
+      if (c + 1 < w)
+        syrk(st, sc, (k + c) * NB, NB, (end(sc) - sc) / ST, 0, w - 1 - c, 64, 0, w - 1 - c);
+    }
   }
   // Factor the super-panel of block columns [k, k + w): per column potrf + trsm, then the
   // update of the super-panel's remaining columns with it (K = 128).
@@ -940,15 +983,15 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   auto go = [&]() {
     if (cio & 4) {  // 64-row slabs, C I/O
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(2 * tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0, ctx->xcd_remap);
+                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0, ctx->xcd_remap, 0);
       return;
     }
     if (cio & 1)
       hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0, ctx->xcd_remap);
+                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0, ctx->xcd_remap, 0);
     else
       hipLaunchKernelGGL((syrk_kernel<false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0, ctx->xcd_remap);
+                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0, ctx->xcd_remap, 0);
   };
   go();
   hipEvent_t a, b;
@@ -1052,6 +1095,36 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     const int64_t m = bordered ? Mp + NB : Mp - steps[s].first * NB;
     return m >= serial_below;
   };
+  if (ctx->sched == 2 && ctx->lookahead) {
+    // Schedule 2: the side stream factors only each super-panel's diagonal block (a few
+    // workgroups); the main stream solves the tall panel below it and applies the bulk
+    // update, leaving the next super-panel's diagonal block to the side stream.
+    hipEventRecord(ev[0], main);
+    hipStreamWaitEvent(side, ev[0], 0);
+    L.diag_factor(side, steps[0].first, steps[0].second, n);
+    hipEventRecord(ev[1], side);
+    for (int s = 0; s < S; ++s) {
+      const int64_t k = steps[s].first;
+      const int w = steps[s].second;
+      const int64_t K0 = k * NB, K1 = (k + w) * NB;
+      hipStreamWaitEvent(main, ev[1 + 2 * s], 0);
+      L.tall_solve(main, k, w);
+      hipEventRecord(ev[2 + 2 * s], main);
+      const bool nxt = s + 1 < S;
+      const int wn = nxt ? steps[s + 1].second : 0;
+      if (trailing(s)) {
+        const int64_t T = L.tiles_from(K1);
+        if (wn) L.syrk(main, K1, K0, NB * w, T, 0, wn, 64, 0, wn);  // below the next block
+        if (wn < T) L.syrk(main, K1, K0, NB * w, T, wn, (int)T, 128);
+      }
+      if (nxt) {
+        hipStreamWaitEvent(side, ev[2 + 2 * s], 0);
+        L.syrk(side, K1, K0, NB * w, wn, 0, wn, 64, 1);  // the next diagonal block
+        L.diag_factor(side, steps[s + 1].first, wn, n);
+        hipEventRecord(ev[1 + 2 * (s + 1)], side);
+      }
+    }
+  } else {
   if (ahead(0)) {
     hipEventRecord(ev[0], main);
     hipStreamWaitEvent(side, ev[0], 0);
@@ -1084,6 +1157,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       hipEventRecord(ev[1 + 2 * (s + 1)], side);
     }
   }
+  }  // schedule 1
   r = hip_fail(ctx, hipGetLastError(), "cholesky launch");
   if (r) return r;
   hipEvent_t pe;

@@ -75,6 +75,7 @@ struct lfm_ctx {
   int* status = nullptr;                         // [0] first failing pivot (INT_MAX = none)
   unsigned* psync = nullptr;                     // fused panel: [0] factor epoch, [1] slab count
   unsigned panel_epoch = 0;                      // fused panel launches so far
+  int sched = 1;                                 // look-ahead schedule 1 or 2 (LFM_SCHED)
   int fused = 1;                                 // fused panel kernel for w = 1 steps (LFM_FUSED)
   int syrk_pad_kb = 0;                           // extra LDS per slab workgroup: caps residency (LFM_SYRK_PAD_KB)
   int xcd_remap = 1;                             // XCD-contiguous SYRK tile order (LFM_XCD_REMAP)
