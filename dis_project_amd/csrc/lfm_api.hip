@@ -448,8 +448,18 @@ hipError_t create_streams(lfm_ctx* ctx) {
   const int ncu = prop.multiProcessorCount;
   if (ncu > 0) ctx->cus = ncu;
   if (side_cus > 0 && side_cus < ncu) {
+    ctx->side_cus = side_cus;
+    // side CUs j * stride (mod ncu), j < side_cus: LFM_SIDE_STRIDE spreads them over the XCDs
+    const char* sst = std::getenv("LFM_SIDE_STRIDE");
+    const int stride = sst ? std::max(1, std::atoi(sst)) : 1;
+    std::vector<char> is_side(ncu, 0);
+    for (int j = 0, c = 0; j < side_cus; ++j) {
+      while (is_side[c]) c = (c + 1) % ncu;
+      is_side[c] = 1;
+      c = (c + stride) % ncu;
+    }
     std::vector<uint32_t> mside((ncu + 31) / 32, 0u), mmain((ncu + 31) / 32, 0u);
-    for (int c = 0; c < ncu; ++c) (c < side_cus ? mside : mmain)[c / 32] |= 1u << (c % 32);
+    for (int c = 0; c < ncu; ++c) (is_side[c] ? mside : mmain)[c / 32] |= 1u << (c % 32);
     hipError_t e = hipExtStreamCreateWithCUMask(&ctx->stream, (uint32_t)mmain.size(), mmain.data());
     if (e != hipSuccess) return e;
     return hipExtStreamCreateWithCUMask(&ctx->side, (uint32_t)mside.size(), mside.data());
@@ -524,7 +534,8 @@ void lfm_ctx_destroy(lfm_ctx* ctx) {
   for (void* p : {(void*)ctx->A, (void*)ctx->tab, (void*)ctx->tab32, (void*)ctx->par,
                   (void*)ctx->xin, (void*)ctx->linvT, (void*)ctx->parts, (void*)ctx->status,
                   (void*)ctx->result, (void*)ctx->farm_buf, (void*)ctx->gacc,
-                  (void*)ctx->psync})
+                  (void*)ctx->psync, (void*)ctx->wk, (void*)ctx->xbuf, (void*)ctx->zvec,
+                  (void*)ctx->flags})
     if (p) hipFree(p);
   if (ctx->hpin) hipHostFree(ctx->hpin);
   for (auto& p : ctx->pending) {

@@ -43,6 +43,7 @@ static constexpr int IB = 16;        // inner block of the diagonal factor / pan
 static constexpr int ST = 128;       // SYRK output tile edge
 static constexpr int KB = 16;        // SYRK K-step staged through LDS
 static constexpr int STATUS_NONE = INT_MAX;
+constexpr int PANEL_TIMEOUT = -2;  // status: a bounded device-side wait ran out
 
 __device__ __forceinline__ double4v mfma16(double a, double b, double4v c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -516,49 +517,78 @@ __global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, in
 // column; otherwise tj_hi must be T and the band is a triangle. Update depth kd (multiple
 // of KB): columns kb .. kb + kd of A. TR = tile rows (128, or 64 for latency-critical bands).
 // DB: double-buffered LDS stages (one barrier per K step instead of two).
-#ifndef LFM_SLAB_WGS
-#define LFM_SLAB_WGS 3
-#endif
-// acc[ir][jr] (C[wr + ir*4 + (lane>>4)][wc + jr*16 + (lane&15)] of a TR x 128 block at rows
-// i0, cols j0; waves as 2 x 2) += P_i P_j^T over panel columns kb .. kb + kd — callers hold
-// -C in acc (negated once at load / store instead of per fragment). sP: LDS staging,
-// (TR + ST) rows of KB + 1 doubles: rows [0, TR) panel i, rows [TR, TR + ST) panel j.
+// acc[ir][jr] (C[wr + ir*4 + (lane>>4)][wc + jr*16 + (lane&15)] of a TR x 128 block; waves
+// as 2 x 2) += sum_k Pi[i][k] Pj[j][k], k < kd. pi: row i0 of the i panel (k contiguous,
+// row stride ldi). pj: BT = false, row j0 of the j panel (k contiguous, row stride ldj);
+// BT = true, a K-major panel: element (k, j) at pj[k * ldj + j]. The SYRK callers hold -C in
+// acc (negated once at load / store instead of per fragment). sP: LDS staging, (TR + ST) rows
+// of KB + 1 doubles: rows [0, TR) panel i, rows [TR, TR + ST) panel j (j-major).
 // Every thread of the (256-thread) workgroup must call it.
-template <int TR>
-__device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, int64_t lda,
-                                                int64_t i0, int64_t j0, int64_t kb, int kd,
-                                                double (&acc)[TR / 8][4],
+// Two doubles; COH: device-coherent loads (agent-scope relaxed atomics bypass the XCD's L2,
+// which may hold stale lines of data another XCD wrote in the same launch).
+template <bool COH>
+__device__ __forceinline__ double2 ld2(const double* p) {
+  if (COH) {
+    double2 v;
+    v.x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v.y = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+  }
+  return *reinterpret_cast<const double2*>(p);
+}
+
+template <int TR, bool BT = false, bool COH = false>
+__device__ __forceinline__ void gemm_accumulate(const double* __restrict__ pi, int64_t ldi,
+                                                const double* __restrict__ pj, int64_t ldj,
+                                                int kd, double (&acc)[TR / 8][4],
                                                 double (*__restrict__ sP)[KB + 1]) {
   constexpr int IRN = TR / 8;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // opaque: lane offsets are recomputed, not held live
+  const int lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
   const int li = lane & 15, lk = lane >> 4, l3 = lane & 3;
   // staging: TR rows of panel i and 128 rows of panel j, KB doubles each; thread tid moves
-  // chunk (tid & 7) of rows (tid >> 3) + 32u
+  // chunk (tid & 7) of rows (tid >> 3) + 32u. K-major j panel: thread tid moves the double2
+  // (k = idx >> 6, j = 2 (idx & 63)) of idx = tid + 256u and stores it transposed.
   static_assert(KB == 16, "staging map assumes 8 double2 chunks per row");
   constexpr int NUI = TR / 32, NU = NUI + 4;
   const int srow = tid >> 3, sch = tid & 7;
-  const double* gi = A + (i0 + srow) * lda + kb + 2 * sch;
-  const double* gj = A + (j0 + srow) * lda + kb + 2 * sch;
-  const int ld32 = (int)(32 * lda);
+  const double* gi = pi + srow * ldi + 2 * sch;
+  const double* gj = BT ? pj + (tid >> 6) * ldj + 2 * (tid & 63) : pj + srow * ldj + 2 * sch;
+  const int li32 = (int)(32 * ldi);
+  const int lj32 = BT ? (int)(4 * ldj) : (int)(32 * ldj);
   double2 pre[NU];
   auto gload = [&](int k0) {
     // row offsets recomputed per call (opaque stride) rather than held as live 64-bit pointers
-    int l32 = ld32;
-    asm volatile("" : "+v"(l32));
+    int l32 = li32, m32 = lj32;
+    asm volatile("" : "+v"(l32), "+v"(m32));
 #pragma unroll
-    for (int u = 0; u < NUI; ++u) pre[u] = *reinterpret_cast<const double2*>(gi + u * l32 + k0);
+    for (int u = 0; u < NUI; ++u) pre[u] = ld2<COH>(gi + u * l32 + k0);
+    const double* gjk = BT ? gj + (int64_t)k0 * ldj : gj + k0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) pre[NUI + u] = *reinterpret_cast<const double2*>(gj + u * l32 + k0);
+    for (int u = 0; u < 4; ++u) pre[NUI + u] = ld2<COH>(gjk + u * m32);
   };
   gload(0);
   for (int k0 = 0; k0 < kd; k0 += KB) {
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      double* d = &sP[u < NUI ? srow + 32 * u : TR + srow + 32 * (u - NUI)][2 * sch];
+    for (int u = 0; u < NUI; ++u) {
+      double* d = &sP[srow + 32 * u][2 * sch];
       d[0] = pre[u].x;
       d[1] = pre[u].y;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (BT) {
+        const int kr = (tid >> 6) + 4 * u, jc = 2 * (tid & 63);
+        sP[TR + jc][kr] = pre[NUI + u].x;
+        sP[TR + jc + 1][kr] = pre[NUI + u].y;
+      } else {
+        double* d = &sP[TR + srow + 32 * u][2 * sch];
+        d[0] = pre[NUI + u].x;
+        d[1] = pre[NUI + u].y;
+      }
     }
     __syncthreads();
     if (k0 + KB < kd) gload(k0 + KB);
@@ -584,22 +614,30 @@ __device__ __forceinline__ void syrk_accumulate(const double* __restrict__ A, in
   }
 }
 
+// Source of a trailing update's panel rows: matrix row r (k = 0 at the panel's first column)
+// starts at p + (r - r0) * ld. The factor's own block column: {A + kb, lda, 0}; a separate
+// panel buffer holding rows r0 .. : {X, ldx, r0}.
+struct Panel {
+  const double* p;
+  int64_t ld, r0;
+};
+
 #ifndef LFM_SLAB_WGS
 #define LFM_SLAB_WGS 3
 #endif
-template <bool CIO, int TR>
-__global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
-    double* __restrict__ A, int64_t lda, int64_t s, int64_t kb, int kd, int T, int tj_lo,
-    int tj_hi, int prio, int xcd_remap, int ti0) {
+// One TR x 128 work unit of a band / triangle launch: C -= P_i P_j^T over panel depth kd,
+// C the lower part of the trailing matrix of A starting at row / column s. b = the unit's
+// index in the enumeration below.
+template <bool CIO, int TR, bool COH = false>
+__device__ __forceinline__ void syrk_unit(double* __restrict__ A, int64_t lda, int64_t s, Panel P,
+                                          int kd, int T, int tj_lo, int tj_hi, int64_t b, int ti0,
+                                          double (*__restrict__ sP)[KB + 1]) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
-  __shared__ double sP[TR + ST][KB + 1];
-  if (prio) __builtin_amdgcn_s_setprio(2);  // look-ahead bands: ahead of the bulk update
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
   const int li = lane & 15, lk = lane >> 4;
 
   constexpr int SUB = ST / TR;  // row tiles per 128 rows
-  int64_t b = blockIdx.x;
   int ti, tj;  // ti in TR-row units
   if (tj_hi - tj_lo <= 8) {
     // band: tile columns [tj_lo, tj_hi), tile rows max(tj, ti0) .. T - 1
@@ -610,14 +648,8 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
     }
     ti = SUB * max(tj, ti0) + (int)b;
   } else {
-    // triangle of 128-tiles over tile columns [tj_lo, T), SUB row slabs of TR rows per tile.
-    // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (each with its own L2),
-    // so give XCD x the contiguous range x*q .. of the enumeration (bijective remap): the
-    // workgroups resident on one XCD then share panel rows instead of striding over them.
-    if (xcd_remap) {
-      const int64_t nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = b % 8;
-      b = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
-    }
+    // triangle of 128-tiles over tile columns [tj_lo, T), SUB row slabs of TR rows per tile;
+    // tile rows are enumerated in order, so a launch can skip the first ones (b offset)
     const int sub = (int)(b % SUB);
     b /= SUB;
     int a = (int)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
@@ -636,7 +668,7 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
   for (int ir = 0; ir < IRN; ++ir)
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = CIO ? -Cb[ir * ld4 + jr * 16] : 0.0;
-  syrk_accumulate<TR>(A, lda, i0, j0, kb, kd, acc, sP);
+  gemm_accumulate<TR>(P.p + (i0 - P.r0) * P.ld, P.ld, P.p + (j0 - P.r0) * P.ld, P.ld, kd, acc, sP);
 
   int ld4s = ld4;
   asm volatile("" : "+v"(ld4s));  // recompute store addresses instead of keeping 64 pointers live
@@ -645,9 +677,243 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) {
       const int64_t row = i0 + wr + ir * 4 + lk, col = j0 + wc + jr * 16 + li;
-      if (CIO && (!diag || col <= row)) Cb[ir * ld4s + jr * 16] = -acc[ir][jr];
+      if (CIO && (!diag || col <= row)) {
+        // COH: device-coherent (write-through) stores, read by another XCD in this launch
+        if (COH)
+          __hip_atomic_store(&Cb[ir * ld4s + jr * 16], -acc[ir][jr], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        else
+          Cb[ir * ld4s + jr * 16] = -acc[ir][jr];
+      }
       if (!CIO && acc[ir][jr] == 1.2345e300) Cb[0] = 0.0;  // keep the MFMAs live
     }
+}
+
+// XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (each with its own L2), so
+// XCD x is given the contiguous range [lo_x, hi_x) of the enumeration: the workgroups resident
+// on one XCD then share panel rows instead of striding over them.
+__device__ __forceinline__ void xcd_range(int64_t nunits, int x, int64_t* lo, int64_t* hi) {
+  const int64_t q = nunits / 8, r = nunits % 8;
+  *lo = x * q + min((int64_t)x, r);
+  *hi = *lo + q + (x < r ? 1 : 0);
+}
+
+// Trailing update (mode by tile-column range, see syrk_unit); skip: units of the triangle
+// enumeration left out at its start (tile rows already updated elsewhere).
+template <bool CIO, int TR>
+__global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
+    double* __restrict__ A, int64_t lda, int64_t s, Panel P, int kd, int T, int tj_lo, int tj_hi,
+    int prio, int xcd_remap, int ti0, int64_t skip) {
+  __shared__ double sP[TR + ST][KB + 1];
+  if (prio) __builtin_amdgcn_s_setprio(2);  // look-ahead bands: ahead of the bulk update
+  int64_t b = blockIdx.x;
+  if (xcd_remap && tj_hi - tj_lo > 8) {
+    int64_t lo, hi;
+    xcd_range(gridDim.x, (int)(b % 8), &lo, &hi);
+    b = lo + b / 8;
+  }
+  syrk_unit<CIO, TR>(A, lda, s, P, kd, T, tj_lo, tj_hi, b + skip, ti0, sP);
+}
+
+// ------------------------------------------------------------ tall panel solve as a GEMM
+// Schedule 3: X = A21 L11^{-T} for the rows [r0, r0 + rows) below a super-panel of width
+// W = 128 w starting at column K0, given Bd = L11^{-T} (W x W, upper triangular, row-major,
+// ld W; the identity border of the chain factorisation). Unit (64-row slab rb, column block
+// cb): X[i][128 cb + j] = sum_{q < 128 (cb + 1)} A[i][K0 + q] Bd[q][128 cb + j]. X goes to a
+// separate buffer (ld W, row r0 first) — the A columns are still read by other units — and
+// row n of X (z = L^{-1} r) also to zvec[K0 + c].
+__global__ __launch_bounds__(256, LFM_SLAB_WGS) void tall_kernel(
+    const double* __restrict__ A, int64_t lda, int64_t K0, int64_t r0, int w,
+    const double* __restrict__ Bd, double* __restrict__ X, int64_t n, double* __restrict__ zvec) {
+  __shared__ double sP[64 + ST][KB + 1];
+  const int W = w * NB;
+  int64_t b = blockIdx.x;
+  {
+    int64_t lo, hi;
+    xcd_range(gridDim.x, (int)(b % 8), &lo, &hi);
+    b = lo + b / 8;
+  }
+  const int cb = (int)(b % w);
+  const int64_t i0 = r0 + (b / w) * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64;
+  const int li = lane & 15, lk = lane >> 4;
+  double acc[8][4];
+#pragma unroll
+  for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = 0.0;
+  gemm_accumulate<64, true>(A + i0 * lda + K0, lda, Bd + cb * NB, W, NB * (cb + 1), acc, sP);
+  double* Xb = X + (i0 - r0 + wr + lk) * W + cb * NB + wc + li;
+#pragma unroll
+  for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+    for (int jr = 0; jr < 4; ++jr) {
+      Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
+      if (i0 + wr + ir * 4 + lk == n) zvec[K0 + cb * NB + wc + jr * 16 + li] = acc[ir][jr];
+    }
+}
+
+// Schedule 3 chain workspace Wk (2W x W, ld W): rows [0, W) the diagonal block
+// A[K1 .. K1 + W, K1 .. K1 + W] (lower part), rows [W, 2W) the identity. Factoring its W
+// columns leaves L11 in the top and L11^{-T} in the bottom. With wait != NULL the copy starts
+// once *wait >= target (the main stream's update of the block has landed).
+template <bool ACQ = true>
+__device__ __forceinline__ bool spin_until(const unsigned* p, unsigned target) {
+  unsigned it = 0;
+  while (__hip_atomic_load(p, ACQ ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+             target &&
+         ++it < (1u << 26))
+    __builtin_amdgcn_s_sleep(2);
+  return it < (1u << 26);
+}
+
+__global__ __launch_bounds__(256) void chain_init_kernel(const double* __restrict__ A, int64_t lda,
+                                                         int64_t K1, int W, double* __restrict__ Wk,
+                                                         const unsigned* wait, unsigned target,
+                                                         int* __restrict__ status) {
+  if (wait) {
+    __shared__ int ok;
+    if (threadIdx.x == 0) ok = spin_until(wait, target);
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (!ok) {
+      if (threadIdx.x == 0) atomicMin(status, PANEL_TIMEOUT);
+      return;
+    }
+  }
+  const int64_t cells = (int64_t)W * W;  // 2W rows of W/2 double2
+  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < cells;
+       idx += (int64_t)gridDim.x * 256) {
+    const int r = (int)(idx / (W / 2)), c = 2 * (int)(idx % (W / 2));
+    double2 v;
+    if (r < W) {
+      v = *reinterpret_cast<const double2*>(&A[(K1 + r) * lda + K1 + c]);
+    } else {
+      v.x = (r - W == c) ? 1.0 : 0.0;
+      v.y = (r - W == c + 1) ? 1.0 : 0.0;
+    }
+    *reinterpret_cast<double2*>(&Wk[(int64_t)r * W + c]) = v;
+  }
+}
+
+// Sets *flag = 1 (release) once every earlier kernel of the stream has completed.
+__global__ void signal_kernel(unsigned* flag) {
+  __hip_atomic_store(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One main-stream launch per super-panel step s (schedule 3): step s's trailing update from
+// X_s (the next diagonal block excluded: chain_kernel applies it), then X_{s+1}. Roles of
+// 64 x 128 units in blockIdx order (each segment padded to a multiple of 8 workgroups,
+// XCD-contiguous within it):
+//   ahead the next super-panel's columns below its diagonal block; each unit bumps
+//         a_done[tile row]
+//   rest  the remaining trailing triangle (optionally split around the tall units)
+//   tall  X_{s+1} = A21 Bd_{s+1} for the rows below the next diagonal block: a unit waits for
+//         the side stream's factor (chain_done) and for its rows' `ahead` units.
+// Workgroups are dispatched in order per XCD, so a waiting `tall` unit never holds a slot an
+// unfinished `ahead` unit of its XCD still needs; waits are bounded (status PANEL_TIMEOUT).
+struct StepArgs {
+  double* A;
+  int64_t lda;
+  int64_t s0;     // trailing matrix of step s starts at row / column s0 = K1
+  Panel px;       // X_s (rows from s0)
+  int kd, T, wn;  // depth W_s, trailing 128-tiles, next width in tiles
+  int na, nr, nt;  // units per role
+  int nr1;        // rest units dispatched before the tall units
+  int exp;        // experiments: bit 0 = no ahead -> tall ordering (wrong results; timing only)
+  int64_t tr0;    // tall: first row (K1 of step s + 1), W_{s+1} = tw * 128, K0_{s+1} = tk0
+  int64_t tk0;
+  int tw;
+  const double* Bd;
+  double* X;      // X_{s+1}, ld tw * 128, row tr0 first
+  int64_t n;
+  double* zvec;
+  unsigned* a_done;  // [T] per tile row of step s (NULL: no wait)
+  const unsigned* chain_done;  // NULL: no wait
+  int* status;
+};
+
+
+__global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
+  __shared__ double sP[64 + ST][KB + 1];
+  const int64_t b = blockIdx.x;
+  // segments in blockIdx order: ahead, rest [0, nr1), tall, rest [nr1, nr)
+  const int cnt[4] = {g.na, g.nr1, g.nt, g.nr - g.nr1};
+  const int role_of[4] = {1, 2, 3, 2};
+  int seg = 0;
+  int64_t base = 0;
+  while (seg < 3 && b >= base + (cnt[seg] + 7) / 8 * 8) {
+    base += (cnt[seg] + 7) / 8 * 8;
+    ++seg;
+  }
+  int64_t lo, hi;
+  xcd_range(cnt[seg], (int)(b % 8), &lo, &hi);
+  int64_t u = lo + (b - base) / 8;
+  if (u >= hi) return;
+  const int role = role_of[seg];
+  if (seg == 3) u += g.nr1;
+  if (role == 1) {
+    // device-coherent stores + a counter bump once they have completed: the tall units read
+    // these rows with device-coherent loads (no L2 writeback / invalidate on either side)
+    syrk_unit<true, 64, true>(g.A, g.lda, g.s0, g.px, g.kd, g.T, 0, g.wn, u, g.wn, sP);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0 && !(g.exp & 1))
+      __hip_atomic_fetch_add(&g.a_done[g.wn + (int)(u % (2 * (g.T - g.wn))) / 2], 1u,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (role == 2) {
+    syrk_unit<true, 64>(g.A, g.lda, g.s0, g.px, g.kd, g.T, g.wn, g.T, u, 0, sP);
+    return;
+  }
+  // tall unit (row slab rb, column block cb) of step s + 1
+  // deepest column blocks first (longest units), so the launch ends on short ones
+  const int64_t nrb = g.nt / g.tw;
+  const int cb = g.tw - 1 - (int)(u / nrb);
+  const int64_t i0 = g.tr0 + (u % nrb) * 64;
+  {
+    __shared__ int ok;
+    // relaxed polling and device-coherent operand loads below instead of an acquire fence:
+    // an agent-scope acquire invalidates this XCD's L2 under the running bulk units
+    if (threadIdx.x == 0) {
+      bool good = !g.chain_done || spin_until<false>(g.chain_done, 1u);
+      if (good && g.a_done && !(g.exp & 1))
+        good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], 2u * g.wn);
+      ok = good;
+    }
+    __syncthreads();
+    if (!ok) {
+      if (threadIdx.x == 0) atomicMin(g.status, PANEL_TIMEOUT);
+      return;
+    }
+  }
+  const int W = g.tw * NB;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64;
+  const int li = lane & 15, lk = lane >> 4;
+  double acc[8][4];
+#pragma unroll
+  for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = 0.0;
+  gemm_accumulate<64, true, true>(g.A + i0 * g.lda + g.tk0, g.lda, g.Bd + cb * NB, W,
+                                  NB * (cb + 1), acc, sP);
+  double* Xb = g.X + (i0 - g.tr0 + wr + lk) * W + cb * NB + wc + li;
+#pragma unroll
+  for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+    for (int jr = 0; jr < 4; ++jr) {
+      Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
+      if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + cb * NB + wc + jr * 16 + li] = acc[ir][jr];
+    }
+}
+
+// Row n of the chain workspace (n inside the super-panel's diagonal block) into zvec.
+__global__ void zrow_kernel(const double* __restrict__ Wk, int W, int64_t rloc, int64_t K0,
+                            double* __restrict__ zvec) {
+  for (int c = threadIdx.x; c < W; c += blockDim.x) zvec[K0 + c] = Wk[rloc * W + c];
 }
 
 // ---------------------------------------------------------- fused panel
@@ -662,7 +928,6 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
 // +1 each) and sync[0] (factor written, = epoch). Workgroup 0 is dispatched first, so waiting
 // workgroups never hold the slots it needs; a bounded wait still ends every workgroup (status
 // PANEL_TIMEOUT) rather than hang.
-constexpr int PANEL_TIMEOUT = -2;
 constexpr size_t PANEL_LDS = (size_t)MB_DOUBLES * sizeof(double);
 static_assert(MB_DOUBLES >= 64 * (NB + 1) && MB_DOUBLES >= (64 + ST) * (KB + 1), "LDS union");
 
@@ -701,7 +966,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = -Cb[ir * ld4 + jr * 16];
   if (pkd > 0)
-    syrk_accumulate<64>(A, lda, i0, kb, pkb, pkd, acc,
+    gemm_accumulate<64>(A + i0 * lda + pkb, lda, A + kb * lda + pkb, lda, pkd, acc,
                         reinterpret_cast<double (*)[KB + 1]>(smem));
   if (b < 2) {
     // diagonal slab back to the matrix (the part above the diagonal is scratch)
@@ -740,16 +1005,154 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
   trsm_rows(sA, A, lda, i0, kb, dinv);
 }
 
+// ---------------------------------------------------- schedule 3 chain (side stream)
+// One launch per super-panel s on the side stream's own CUs (gridDim.x workgroups, one per
+// CU, all co-resident): the whole factorisation of the diagonal block in the workspace,
+// phases separated by grid barriers instead of kernel boundaries:
+//   P0  Wk top = A[D] - X_{s-1}[D rows] X_{s-1}[D rows]^T (step s - 1's update of the block,
+//       64 x 128 units), Wk bottom = identity
+//   per block column c: potrf (workgroup 0) | panel solve of the rows below in Wk (64-row
+//       units, D rows and identity rows) | update of the block's later columns (band units)
+// and finally z (row n, when it falls in the block) and chain_done[s] = 1. Wk bottom ends as
+// Bd = L11^{-T}, which the main stream's tall units multiply with.
+struct ChainArgs {
+  const double* A;
+  int64_t lda;
+  int64_t Kc;         // first row / column of the super-panel
+  int w;              // width in 128-column blocks
+  double* Wk;         // 2W x W, ld W
+  const double* Xp;   // X_{s-1}: row Kc first, ld ldx, depth kd (kd = 0: no pending update)
+  int64_t ldx;
+  int kd;
+  int64_t n;
+  double* dinv;
+  double* parts;
+  int* status;
+  double* zvec;
+  unsigned* bar;      // grid barrier counter (zeroed per call)
+  unsigned* done;     // chain_done[s]
+};
+
+// Grid barrier over the chain kernel's co-resident workgroups: release, count, acquire.
+// Bounded: on timeout (or a timeout already recorded in *status) it returns false at once.
+__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, int* status) {
+  __shared__ int ok;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned it = 0;
+    bool good = true;
+    while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++it >= (1u << 24) ||
+          __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == PANEL_TIMEOUT) {
+        good = false;
+        atomicMin(status, PANEL_TIMEOUT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    ok = good;
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return ok;
+}
+
+__global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  double (*sP)[KB + 1] = reinterpret_cast<double (*)[KB + 1]>(smem);
+  double (*sA)[NB + 1] = reinterpret_cast<double (*)[NB + 1]>(smem);
+  const int G = gridDim.x, wg = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int W = g.w * NB;
+  double* Aw = g.Wk - (g.Kc * W + g.Kc);  // the workspace with the matrix's row / column numbers
+  unsigned nbar = 0;
+  // P0: pending update of the block into the workspace (lower 128-tiles, 2 slabs each)
+  {
+    const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64, li = lane & 15, lk = lane >> 4;
+    const int nunit = g.w * (g.w + 1);
+    for (int u = wg; u < nunit; u += G) {
+      const int t = u >> 1, sub = u & 1;
+      int ti = 0;
+      while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+      const int tj = t - ti * (ti + 1) / 2;
+      const int64_t i0 = g.Kc + ti * NB + sub * 64, j0 = g.Kc + tj * NB;
+      const double* Cs = g.A + (i0 + wr + lk) * g.lda + j0 + wc + li;
+      double acc[8][4];
+#pragma unroll
+      for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+        for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = -Cs[(ir * 4) * g.lda + jr * 16];
+      if (g.kd > 0)
+        gemm_accumulate<64>(g.Xp + (i0 - g.Kc) * g.ldx, g.ldx, g.Xp + (j0 - g.Kc) * g.ldx, g.ldx,
+                            g.kd, acc, sP);
+      double* Cd = Aw + (i0 + wr + lk) * W + j0 + wc + li;
+#pragma unroll
+      for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+        for (int jr = 0; jr < 4; ++jr) Cd[(ir * 4) * W + jr * 16] = -acc[ir][jr];
+      __syncthreads();
+    }
+    for (int64_t idx = (int64_t)wg * 256 + tid; idx < (int64_t)W * W / 2; idx += (int64_t)G * 256) {
+      const int r = (int)(idx / (W / 2)), c = 2 * (int)(idx % (W / 2));
+      double2 v;
+      v.x = (r == c) ? 1.0 : 0.0;
+      v.y = (r == c + 1) ? 1.0 : 0.0;
+      *reinterpret_cast<double2*>(&g.Wk[(int64_t)(W + r) * W + c]) = v;
+    }
+  }
+  bool ok = grid_sync(g.bar, G * ++nbar, g.status);
+  for (int c = 0; c < g.w && ok; ++c) {
+    const int64_t kb = g.Kc + (int64_t)c * NB, r0 = kb + NB;
+    if (wg == 0) potrf_block<15>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB), g.status);
+    ok = grid_sync(g.bar, G * ++nbar, g.status);
+    if (!ok) break;
+    const int64_t rows = g.Kc + 2 * W - r0;
+    for (int64_t u = wg; u < rows / 64; u += G) {
+      const int64_t ra = r0 + 64 * u;
+      for (int idx = tid; idx < 64 * (NB / 2); idx += 256) {
+        const int r = idx / (NB / 2), q2 = idx - r * (NB / 2);
+        const double2 v = *reinterpret_cast<const double2*>(&Aw[(ra + r) * W + kb + 2 * q2]);
+        sA[r][2 * q2] = v.x;
+        sA[r][2 * q2 + 1] = v.y;
+      }
+      trsm_rows(sA, Aw, W, ra, kb, g.dinv);
+      __syncthreads();
+    }
+    ok = grid_sync(g.bar, G * ++nbar, g.status);
+    if (!ok || c + 1 == g.w) break;
+    const int T = (int)(rows / ST), hi = g.w - 1 - c;
+    int64_t nunit = 0;
+    for (int tj = 0; tj < hi; ++tj) nunit += 2 * (T - tj);
+    for (int64_t u = wg; u < nunit; u += G) {
+      syrk_unit<true, 64>(Aw, W, r0, Panel{Aw + kb, W, 0}, NB, T, 0, hi, u, 0, sP);
+      __syncthreads();
+    }
+    ok = grid_sync(g.bar, G * ++nbar, g.status);
+  }
+  if (wg == 0) {
+    if (g.n >= g.Kc && g.n < g.Kc + W)
+      for (int c = tid; c < W; c += 256) g.zvec[g.Kc + c] = g.Wk[(g.n - g.Kc) * W + c];
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(g.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // ------------------------------------------------------------- finalize
+// z = L^{-1} r: columns c < zsplit from zvec (schedule 3 keeps the panels out of A), the rest
+// from row n of the factor.
 __global__ __launch_bounds__(1024) void finalize_kernel(const double* __restrict__ A, int64_t lda,
                                                         int64_t n, const double* __restrict__ parts,
                                                         int nparts, const int* __restrict__ status,
-                                                        int negative, double* __restrict__ out) {
+                                                        int negative, double* __restrict__ out,
+                                                        const double* __restrict__ zvec,
+                                                        int64_t zsplit) {
   __shared__ double red[2][16];
   const int tid = threadIdx.x;
   double q = 0.0, ld = 0.0;
   for (int64_t c = tid; c < n; c += 1024) {
-    const double z = A[n * lda + c];
+    const double z = c < zsplit ? zvec[c] : A[n * lda + c];
     q += z * z;
   }
   for (int k = tid; k < nparts; k += 1024) ld += parts[k];
@@ -827,6 +1230,12 @@ struct Launcher {
   // ti0 (band launches only): first tile row, so a band can skip the rows of a diagonal block.
   void syrk(hipStream_t st, int64_t s0, int64_t kb, int kd, int64_t T, int lo, int hi, int tr,
             int prio = 0, int ti0 = 0) {
+    syrk_p(st, s0, Panel{A + kb, lda, 0}, kd, T, lo, hi, tr, prio, ti0, 0);
+  }
+  // Same with the panel rows taken from P; skip (triangle launches only): the first `skip`
+  // tile rows of the triangle are left out (updated by an earlier launch).
+  void syrk_p(hipStream_t st, int64_t s0, Panel P, int kd, int64_t T, int lo, int hi, int tr,
+              int prio, int ti0, int skip) {
     if (T <= 0 || hi <= lo) return;
     hi = (int)std::min<int64_t>(hi, T);
     const bool band = hi - lo <= 8;
@@ -845,16 +1254,28 @@ struct Launcher {
       elems += r0 > tj ? (double)(T - r0) * ST * ST
                        : (double)(T - tj - 1) * ST * ST + (double)ST * (ST + 1) / 2;
     }
-    if (tiles == 0) return;
+    int64_t skip_units = 0;
+    if (band && skip > 0) {
+      // a band enumerates tile rows from max(tj, ti0): skipping tile rows is a raised ti0
+      ti0 = std::max(ti0, skip);
+      return syrk_p(st, s0, P, kd, T, lo, hi, tr, prio, ti0, 0);
+    }
+    if (!band && skip > 0) {
+      skip_units = (int64_t)sub * skip * (skip + 1) / 2;
+      tiles -= skip_units;
+      elems -= (double)skip * (skip - 1) / 2 * ST * ST + (double)skip * ST * (ST + 1) / 2;
+    }
+    if (tiles <= 0) return;
     hipEvent_t ev;
     prof_begin(ctx, K_SYRK, &ev, st);
     if (tr == 64)
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3((unsigned)tiles), dim3(256),
-                         (size_t)ctx->syrk_pad_kb * 1024, st, A, lda,
-                         s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask, ctx->xcd_remap, ti0);
+                         (size_t)ctx->syrk_pad_kb * 1024, st, A, lda, s0, P, kd, (int)T, lo, hi,
+                         prio & ctx->prio_mask, ctx->xcd_remap, ti0, skip_units);
     else
       hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3((unsigned)tiles), dim3(256), 0, st, A,
-                         lda, s0, kb, kd, (int)T, lo, hi, prio & ctx->prio_mask, ctx->xcd_remap, ti0);
+                         lda, s0, P, kd, (int)T, lo, hi, prio & ctx->prio_mask, ctx->xcd_remap,
+                         ti0, skip_units);
     prof_end(ctx, K_SYRK, ev, elems * 2.0 * kd, elems * 16.0, st);
   }
   int64_t tiles_from(int64_t s0) const { return (end(s0) - s0) / ST; }
@@ -980,18 +1401,19 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8, ctx->stream);
   const unsigned tiles = (unsigned)((int64_t)T * (T + 1) / 2);
   hipStream_t st = ctx->stream;
+  const Panel pan{ctx->A, n, 0};
   auto go = [&]() {
     if (cio & 4) {  // 64-row slabs, C I/O
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(2 * tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0, ctx->xcd_remap, 0);
+                         (int64_t)512, pan, kd, T, 0, T, 0, ctx->xcd_remap, 0, (int64_t)0);
       return;
     }
     if (cio & 1)
       hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0, ctx->xcd_remap, 0);
+                         (int64_t)512, pan, kd, T, 0, T, 0, ctx->xcd_remap, 0, (int64_t)0);
     else
       hipLaunchKernelGGL((syrk_kernel<false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, (int64_t)0, kd, T, 0, T, 0, ctx->xcd_remap, 0);
+                         (int64_t)512, pan, kd, T, 0, T, 0, ctx->xcd_remap, 0, (int64_t)0);
   };
   go();
   hipEvent_t a, b;
@@ -1095,7 +1517,131 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     const int64_t m = bordered ? Mp + NB : Mp - steps[s].first * NB;
     return m >= serial_below;
   };
-  if (ctx->sched == 2 && ctx->lookahead) {
+  int64_t zsplit = 0;  // finalize: z columns below zsplit come from ctx->zvec
+  // schedule 3 needs CUs of its own for the side stream (LFM_SIDE_CUS): its waiting step
+  // units would otherwise hold every slot the side stream's factor kernels need
+  if (ctx->sched == 3 && ctx->lookahead && ctx->side_cus > 0 && mode == CHOL_MLL) {
+    // Schedule 3. Side stream, per super-panel s (columns [K0, K1), W = K1 - K0): the chain
+    // factors only the W x W diagonal block, copied into a workspace with an identity border
+    // (chain_init_kernel), so it also yields Bd = L11^{-T}. Main stream: one step_kernel per
+    // step applies step s's trailing update from X_s (next diagonal block first, then the next
+    // super-panel's columns, then the rest) and finishes with X_{s+1} = A21 Bd_{s+1}, the tall
+    // panel solve as a GEMM, once the side stream's factor of block s + 1 has landed.
+    // Cross-stream order within a step is by device flags (ctx->flags), reset per call.
+    int wmax = 1;
+    for (const auto& st : steps) wmax = std::max(wmax, st.second);
+    const int64_t Wmax = (int64_t)wmax * NB, Tmax = Mp / ST + 1;
+    r = ensure(ctx, (void**)&ctx->wk, &ctx->wk_bytes, (size_t)2 * Wmax * Wmax * sizeof(double));
+    if (!r)
+      r = ensure(ctx, (void**)&ctx->xbuf, &ctx->xbuf_bytes, (size_t)2 * Mp * Wmax * sizeof(double));
+    if (!r) r = ensure(ctx, (void**)&ctx->zvec, &ctx->zvec_bytes, (size_t)Mp * sizeof(double));
+    const size_t nflags = (size_t)S * (2 + Tmax);
+    if (!r) r = ensure(ctx, (void**)&ctx->flags, &ctx->flags_bytes, nflags * sizeof(unsigned));
+    if (r) return r;
+    unsigned* chain_done = ctx->flags;     // [S]
+    unsigned* a_done = ctx->flags + S;     // [S][Tmax]
+    hipMemsetAsync(ctx->flags, 0, nflags * sizeof(unsigned), main);
+    zsplit = n;
+    auto xbuf = [&](int s) { return ctx->xbuf + (size_t)(s & 1) * Mp * Wmax; };
+    unsigned* bars = a_done + (size_t)S * Tmax;  // [S] grid barrier counters of chain(s)
+    // chain(s): factor block s on the side stream's CUs (one launch, see chain_kernel)
+    auto chain = [&](int s) {
+      ChainArgs c{};
+      c.A = A;
+      c.lda = lda;
+      c.Kc = steps[s].first * NB;
+      c.w = steps[s].second;
+      c.Wk = ctx->wk;
+      if (s > 0) {
+        c.Xp = xbuf(s - 1);
+        c.ldx = (int64_t)steps[s - 1].second * NB;
+        c.kd = steps[s - 1].second * NB;
+      }
+      c.n = n;
+      c.dinv = ctx->linvT;
+      c.parts = ctx->parts;
+      c.status = ctx->status;
+      c.zvec = ctx->zvec;
+      c.bar = bars + s;
+      c.done = chain_done + s;
+      hipEvent_t pe;
+      prof_begin(ctx, K_POTRF, &pe, side);
+      hipLaunchKernelGGL(chain_kernel, dim3((unsigned)ctx->side_cus), dim3(256), PANEL_LDS, side, c);
+      const double W = c.w * NB;
+      prof_end(ctx, K_POTRF, pe, W * W * W / 3.0 + W * W * W, 0, side);
+    };
+    // tall units of step s: rows [K1_s, Mp) x w_s column blocks
+    auto tall_units = [&](int s) {
+      const int64_t K1 = (steps[s].first + steps[s].second) * NB;
+      return (int)((Mp - K1) / 64 * steps[s].second);
+    };
+    const char* tp = std::getenv("LFM_TALL_POS");
+    const double tall_pos = tp ? std::atof(tp) : 1.0;  // fraction of the rest ahead of the tall units
+    auto launch_step = [&](StepArgs& g) {
+      g.nr1 = (int)std::min<double>(g.nr, std::max(0.0, tall_pos * g.nr));
+      g.exp = env_int("LFM_STEP_EXP", 0);
+      const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 +
+                           (int64_t)(g.nr1 + 7) / 8 * 8 + (int64_t)(g.nt + 7) / 8 * 8 +
+                           (int64_t)(g.nr - g.nr1 + 7) / 8 * 8;
+      if (grid == 0) return;
+      double el = (double)g.na * 64 * ST + (double)g.nr * 64 * ST;
+      hipEvent_t pe;
+      prof_begin(ctx, K_SYRK, &pe, main);
+      hipLaunchKernelGGL(step_kernel, dim3((unsigned)grid), dim3(256), 0, main, g);
+      prof_end(ctx, K_SYRK, pe, el * 2.0 * g.kd + (double)g.nt * 64 * ST * NB * (g.tw + 1), 0, main);
+    };
+    auto tall_args = [&](StepArgs& g, int s) {  // tall part of the step launch: step s's rows
+      const int64_t K0 = steps[s].first * NB;
+      const int w = steps[s].second;
+      g.A = A;
+      g.lda = lda;
+      g.nt = tall_units(s);
+      g.tr0 = K0 + (int64_t)w * NB;
+      g.tk0 = K0;
+      g.tw = w;
+      g.Bd = ctx->wk + (int64_t)w * NB * w * NB;
+      g.X = xbuf(s);
+      g.n = n;
+      g.zvec = ctx->zvec;
+      g.chain_done = chain_done + s;
+      g.status = ctx->status;
+    };
+    hipEventRecord(ev[0], main);
+    hipStreamWaitEvent(side, ev[0], 0);
+    chain(0);
+    {
+      // X_0 once the first block is factored (its units wait for chain_done[0])
+      StepArgs g{};
+      tall_args(g, 0);
+      g.a_done = nullptr;
+      launch_step(g);
+      hipEventRecord(ev[1], main);
+    }
+    for (int s = 0; s + 1 < S; ++s) {
+      const int64_t K1 = (steps[s].first + steps[s].second) * NB;
+      const int W = steps[s].second * NB, wn = steps[s + 1].second;
+      const int T = (int)((Mp - K1) / ST);
+      // side: block s + 1 once X_s is complete (the previous main launch)
+      hipStreamWaitEvent(side, ev[1 + s], 0);
+      chain(s + 1);
+      StepArgs g{};
+      g.A = A;
+      g.lda = lda;
+      g.s0 = K1;
+      g.px = Panel{xbuf(s), W, K1};
+      g.kd = W;
+      g.T = T;
+      g.wn = wn;
+      g.na = 2 * wn * (T - wn);
+      g.nr = (T - wn) * (T - wn + 1);  // 2 slabs per tile of the (T - wn)-tile triangle
+      tall_args(g, s + 1);
+      g.a_done = a_done + (size_t)s * Tmax;
+      launch_step(g);
+      hipEventRecord(ev[2 + s], main);
+    }
+    hipEventRecord(ev[S + 1], side);
+    hipStreamWaitEvent(main, ev[S + 1], 0);
+  } else if (ctx->sched == 2 && ctx->lookahead) {  } else if (ctx->sched == 2 && ctx->lookahead) {
     // Schedule 2: the side stream factors only each super-panel's diagonal block (a few
     // workgroups); the main stream solves the tall panel below it and applies the bulk
     // update, leaving the next super-panel's diagonal block to the side stream.
@@ -1163,7 +1709,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   hipEvent_t pe;
   prof_begin(ctx, K_FINALIZE, &pe, main);
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, main, A, lda, n, ctx->parts,
-                     (int)npb, ctx->status, negative, d_out);
+                     (int)npb, ctx->status, negative, d_out, ctx->zvec, zsplit);
   prof_end(ctx, K_FINALIZE, pe, 0, (double)n * 8, main);
   return hip_fail(ctx, hipGetLastError(), "finalize_kernel");
 }

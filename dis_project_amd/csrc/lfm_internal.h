@@ -73,8 +73,13 @@ struct lfm_ctx {
   double* linvT = nullptr;                       // 8 x 16x16 inverses of the diagonal sub-blocks
   double* parts = nullptr; size_t parts_cap = 0; // per-block logdet partials
   int* status = nullptr;                         // [0] first failing pivot (INT_MAX = none)
+  double* wk = nullptr; size_t wk_bytes = 0;     // schedule 3: diagonal block + identity border
+  double* xbuf = nullptr; size_t xbuf_bytes = 0; // schedule 3: solved panel X = A21 L11^{-T}
+  double* zvec = nullptr; size_t zvec_bytes = 0; // schedule 3: z = L^{-1} r
+  unsigned* flags = nullptr; size_t flags_bytes = 0; // schedule 3: per-step device flags
   unsigned* psync = nullptr;                     // fused panel: [0] factor epoch, [1] slab count
   unsigned panel_epoch = 0;                      // fused panel launches so far
+  int side_cus = 0;                              // CUs reserved for the side stream (LFM_SIDE_CUS)
   int sched = 1;                                 // look-ahead schedule 1 or 2 (LFM_SCHED)
   int fused = 1;                                 // fused panel kernel for w = 1 steps (LFM_FUSED)
   int syrk_pad_kb = 0;                           // extra LDS per slab workgroup: caps residency (LFM_SYRK_PAD_KB)
