@@ -102,6 +102,13 @@ __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmc
 // ---------------------------------------------------------------- potrf
 // 1/sqrt(x) to ~1 ulp: v_rsq_f64 estimate + two Newton steps (a pivot and its inverse
 // come from one estimate instead of a correctly rounded sqrt followed by a divide).
+// One Newton step: the pivot's relative error stays far below the 1e-9 MLL tolerance (a
+// perturbation of the pivot by a factor (1 + e) is a backward error e in that column).
+__device__ __forceinline__ double rsqrt_1nr(double x) {
+  const double h = -0.5 * x;
+  const double y = __builtin_amdgcn_rsq(x);
+  return y * fma(h * y, y, 1.5);
+}
 __device__ __forceinline__ double rsqrt_nr(double x) {
   double y = __builtin_amdgcn_rsq(x);
   y = y * fma(-0.5 * x * y, y, 1.5);
@@ -160,42 +167,59 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
   }
   __syncthreads();
 
+  // Look-ahead over the eight 16-column panels: after the rows below panel ib are solved,
+  // wave 0 applies panel ib to the next diagonal 16x16 block alone and factors it (the serial
+  // leaf) while waves 1-3 apply panel ib to the rest of the trailing triangle.
+  // leaf: wave 0 factors diagonal block cb in registers (lane = row)
+  auto leaf = [&](int cb) {
+    const int c0 = cb * IB;
+    double d[IB], pv[IB], yv[IB];
+#pragma unroll
+    for (int q = 0; q < IB; ++q) d[q] = (lane < IB && q <= lane) ? MS(c0 + li, c0 + q) : 0.0;
+#pragma unroll
+    for (int c = 0; c < IB; ++c) {
+      double dc = row_bcast(d[c], c);
+      if (kb + c0 + c >= npiv) dc = 1.0;
+      const double y = rsqrt_1nr(dc);
+      pv[c] = dc;
+      yv[c] = y;
+      d[c] = (lane == c) ? dc * y : d[c] * y;
+#pragma unroll
+      for (int q = c + 1; q < IB; ++q) d[q] = fma(-d[c], row_bcast(d[c], q), d[q]);
+    }
+    if (lane < IB) {
+#pragma unroll
+      for (int q = 0; q < IB; ++q)
+        if (q <= lane) MS(c0 + lane, c0 + q) = d[q];
+    }
+    // the pivots are wave-uniform after the broadcasts: lane c keeps pivot c
+    double pvl = 0.0, yvl = 0.0;
+#pragma unroll
+    for (int c = 0; c < IB; ++c) {
+      pvl = (lane == c) ? pv[c] : pvl;
+      yvl = (lane == c) ? yv[c] : yvl;
+    }
+    if (lane < IB) {
+      pvs[c0 + lane] = pvl;
+      ipv[c0 + lane] = yvl;
+    }
+  };
+  // one 16x16 tile (i0, j0) -= panel c0 rows i0 x rows j0 (fp64 MFMA), in LDS
+  auto tile_update = [&](int i0, int j0, int c0) {
+    double4v acc;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = MS(i0 + lk + 4 * r, j0 + li);
+#pragma unroll
+    for (int ks = 0; ks < IB / 4; ++ks)
+      acc = mfma16(-MS(i0 + li, c0 + ks * 4 + lk), MS(j0 + li, c0 + ks * 4 + lk), acc);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) MS(i0 + lk + 4 * r, j0 + li) = acc[r];
+  };
+  if ((PH & 1) && w == 0) leaf(0);
+  __syncthreads();
 #pragma unroll 1
   for (int ib = 0; ib < NB / IB; ++ib) {
     const int c0 = ib * IB;
-    if ((PH & 1) && w == 0) {
-      double d[IB], pv[IB], yv[IB];
-#pragma unroll
-      for (int q = 0; q < IB; ++q) d[q] = (lane < IB && q <= lane) ? MS(c0 + li, c0 + q) : 0.0;
-#pragma unroll
-      for (int c = 0; c < IB; ++c) {
-        double dc = row_bcast(d[c], c);
-        if (kb + c0 + c >= npiv) dc = 1.0;
-        const double y = rsqrt_nr(dc);
-        pv[c] = dc;
-        yv[c] = y;
-        d[c] = (lane == c) ? dc * y : d[c] * y;
-#pragma unroll
-        for (int q = c + 1; q < IB; ++q) d[q] = fma(-d[c], row_bcast(d[c], q), d[q]);
-      }
-      if (lane < IB) {
-#pragma unroll
-        for (int q = 0; q < IB; ++q)
-          if (q <= lane) MS(c0 + lane, c0 + q) = d[q];
-      }
-      // the pivots are wave-uniform after the broadcasts: lane c keeps pivot c
-      double pvl = 0.0, yvl = 0.0;
-#pragma unroll
-      for (int c = 0; c < IB; ++c) {
-        pvl = (lane == c) ? pv[c] : pvl;
-        yvl = (lane == c) ? yv[c] : yvl;
-      }
-      if (lane < IB) {
-        pvs[c0 + lane] = pvl;
-        ipv[c0 + lane] = yvl;
-      }
-    }
-    __syncthreads();
     // (2) rows below: x_c = (p_c - sum_{q<c} x_q L[c][q]) / L_cc
     const int nr = NB - c0 - IB;
     if ((PH & 2) && w * 64 < nr) {
@@ -217,39 +241,28 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
       }
     }
     __syncthreads();
-    // (3) rank-16 update of the trailing lower triangle, two 16x16 tiles per wave at a time
+    if (nr == 0) break;
+    // (3) wave 0: next diagonal block, then its leaf; waves 1-3: the other trailing tiles
     const int nrb = nr / IB;
-    const int ntiles = (PH & 4) ? nrb * (nrb + 1) / 2 : 0;
-    for (int t = w; t < ntiles; t += 8) {
-      int i0[2], j0[2];
-      bool on[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int tt = t + 4 * u;
-        on[u] = tt < ntiles;
-        const int tc = on[u] ? tt : t;
-        int ti = (int)((sqrtf(8.0f * tc + 1.0f) - 1.0f) * 0.5f);
-        while ((ti + 1) * (ti + 2) / 2 <= tc) ++ti;
-        while (ti * (ti + 1) / 2 > tc) --ti;
-        i0[u] = c0 + IB + ti * IB;
-        j0[u] = c0 + IB + (tc - ti * (ti + 1) / 2) * IB;
+    if (w == 0) {
+      if (PH & 4) {
+        tile_update(c0 + IB, c0 + IB, c0);
+        wave_lds_fence();
       }
-      double4v acc[2];
+      if (PH & 1) leaf(ib + 1);
+    } else if (PH & 4) {
+      const int ntiles = nrb * (nrb + 1) / 2;
+      for (int t = w; t < ntiles; t += 6) {
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[u][r] = MS(i0[u] + lk + 4 * r, j0[u] + li);
-#pragma unroll
-      for (int ks = 0; ks < IB / 4; ++ks)
-#pragma unroll
-        for (int u = 0; u < 2; ++u)
-          acc[u] = mfma16(-MS(i0[u] + li, c0 + ks * 4 + lk), MS(j0[u] + li, c0 + ks * 4 + lk), acc[u]);
-#pragma unroll
-      for (int u = 0; u < 2; ++u)
-        if (on[u]) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) MS(i0[u] + lk + 4 * r, j0[u] + li) = acc[u][r];
+        for (int u = 0; u < 2; ++u) {
+          const int tc = t + 3 * u;
+          if (tc >= ntiles) break;
+          int ti = (int)((sqrtf(8.0f * tc + 1.0f) - 1.0f) * 0.5f);
+          while ((ti + 1) * (ti + 2) / 2 <= tc) ++ti;
+          while (ti * (ti + 1) / 2 > tc) --ti;
+          tile_update(c0 + IB + ti * IB, c0 + IB + (tc - ti * (ti + 1) / 2) * IB, c0);
         }
+      }
     }
     __syncthreads();
   }
