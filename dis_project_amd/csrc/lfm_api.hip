@@ -415,9 +415,9 @@ static int gram_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* h
 }
 
 namespace {
-// Main + side streams. LFM_SIDE_CUS=c (> 0) reserves c CUs for the side stream and keeps
-// the main stream off them (hipExtStreamCreateWithCUMask); 0 (default) shares every CU and
-// relies on the side stream's higher priority. LFM_LOOKAHEAD=0 serialises on one stream.
+// Main + high-priority side stream (every CU), and for schedule 3 a CU-partitioned pair:
+// LFM_SIDE_CUS (default 16) CUs for the factor chain, the rest for the bulk
+// (hipExtStreamCreateWithCUMask). LFM_LOOKAHEAD=0 serialises on one stream.
 hipError_t create_streams(lfm_ctx* ctx) {
   const char* pk = std::getenv("LFM_SYRK_PAD_KB");
   ctx->syrk_pad_kb = pk ? std::atoi(pk) : 0;
@@ -426,7 +426,7 @@ hipError_t create_streams(lfm_ctx* ctx) {
   const char* bp = std::getenv("LFM_BAND_PRIO");
   ctx->prio_mask = bp ? std::atoi(bp) : 1;
   const char* sv = std::getenv("LFM_SCHED");
-  ctx->sched = sv ? std::atoi(sv) : 1;
+  ctx->sched = sv ? std::atoi(sv) : 3;
   const char* fv = std::getenv("LFM_FUSED");
   ctx->fused = fv ? std::atoi(fv) : 1;
   const char* trv = std::getenv("LFM_SYRK_TR");
@@ -442,47 +442,31 @@ hipError_t create_streams(lfm_ctx* ctx) {
   int least = 0, greatest = 0;
   hipDeviceGetStreamPriorityRange(&least, &greatest);
   const char* sc = std::getenv("LFM_SIDE_CUS");
-  const int side_cus = sc ? std::atoi(sc) : 0;
+  const int side_cus = sc ? std::atoi(sc) : 16;
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, ctx->device);
   const int ncu = prop.multiProcessorCount;
   if (ncu > 0) ctx->cus = ncu;
-  if (side_cus > 0 && side_cus < ncu) {
-    ctx->side_cus = side_cus;
-    // side CUs j * stride (mod ncu), j < side_cus: LFM_SIDE_STRIDE spreads them over the XCDs
-    const char* sst = std::getenv("LFM_SIDE_STRIDE");
-    const int stride = sst ? std::max(1, std::atoi(sst)) : 1;
-    std::vector<char> is_side(ncu, 0);
-    for (int j = 0, c = 0; j < side_cus; ++j) {
-      while (is_side[c]) c = (c + 1) % ncu;
-      is_side[c] = 1;
-      c = (c + stride) % ncu;
-    }
-    std::vector<uint32_t> mside((ncu + 31) / 32, 0u), mmain((ncu + 31) / 32, 0u);
-    for (int c = 0; c < ncu; ++c) (is_side[c] ? mside : mmain)[c / 32] |= 1u << (c % 32);
-    hipError_t e = hipExtStreamCreateWithCUMask(&ctx->stream, (uint32_t)mmain.size(), mmain.data());
-    if (e != hipSuccess) return e;
-    return hipExtStreamCreateWithCUMask(&ctx->side, (uint32_t)mside.size(), mside.data());
+  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest);
+  if (e != hipSuccess || side_cus <= 0 || side_cus >= ncu) return e;
+  // Schedule 3 stream pair: side CUs j * stride (mod ncu), j < side_cus, for the factor chain
+  // (LFM_SIDE_STRIDE = 1: consecutive mask bits, which the hardware spreads over the XCDs),
+  // every other CU for the main (bulk) stream.
+  ctx->side_cus = side_cus;
+  const char* sst = std::getenv("LFM_SIDE_STRIDE");
+  const int stride = sst ? std::max(1, std::atoi(sst)) : 1;
+  std::vector<char> is_side(ncu, 0);
+  for (int j = 0, c = 0; j < side_cus; ++j) {
+    while (is_side[c]) c = (c + 1) % ncu;
+    is_side[c] = 1;
+    c = (c + stride) % ncu;
   }
-  // LFM_MAIN_EXCLUDE=c (> 0): the main stream (bulk trailing updates) stays off c CUs spread
-  // over the device; the look-ahead stream may use every CU, so its latency-bound kernels
-  // always find free slots instead of waiting for bulk workgroups to drain.
-  const char* mx = std::getenv("LFM_MAIN_EXCLUDE");
-  const int excl = mx ? std::atoi(mx) : 0;
-  hipError_t e;
-  if (excl > 0 && excl < ncu) {
-    std::vector<uint32_t> mmain((ncu + 31) / 32, 0u);
-    for (int c = 0; c < ncu; ++c) mmain[c / 32] |= 1u << (c % 32);
-    for (int j = 0; j < excl; ++j) {
-      const int c = (int)((int64_t)j * ncu / excl);
-      mmain[c / 32] &= ~(1u << (c % 32));
-    }
-    e = hipExtStreamCreateWithCUMask(&ctx->stream, (uint32_t)mmain.size(), mmain.data());
-  } else {
-    e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-  }
+  std::vector<uint32_t> mside((ncu + 31) / 32, 0u), mmain((ncu + 31) / 32, 0u);
+  for (int c = 0; c < ncu; ++c) (is_side[c] ? mside : mmain)[c / 32] |= 1u << (c % 32);
+  e = hipExtStreamCreateWithCUMask(&ctx->m3, (uint32_t)mmain.size(), mmain.data());
   if (e != hipSuccess) return e;
-  return hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest);
+  return hipExtStreamCreateWithCUMask(&ctx->s3, (uint32_t)mside.size(), mside.data());
 }
 }  // namespace
 
@@ -544,10 +528,11 @@ void lfm_ctx_destroy(lfm_ctx* ctx) {
   }
   for (auto e : ctx->pool) hipEventDestroy(e);
   for (auto e : ctx->evs) hipEventDestroy(e);
-  if (ctx->side) {
-    hipStreamSynchronize(ctx->side);
-    hipStreamDestroy(ctx->side);
-  }
+  for (hipStream_t* st : {&ctx->side, &ctx->s3, &ctx->m3})
+    if (*st) {
+      hipStreamSynchronize(*st);
+      hipStreamDestroy(*st);
+    }
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
 }

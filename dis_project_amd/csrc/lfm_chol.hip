@@ -1407,11 +1407,25 @@ int probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us) {
 
 // Diagnostic: average duration (us) of one full-lower-triangle SYRK launch over a T x T grid
 // of 128-tiles with update depth kd; cio bit 0 = C tile I/O, bit 2 = 64-row slabs (with C I/O).
+// Pseudo-random doubles in [-1/32, 1/32) (probe data: MFMA power, hence clocks, depends on it).
+__global__ void fill_hash_kernel(double* a, int64_t cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) {
+    uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 29;
+    a[i] = ((double)(h >> 11) * 0x1.0p-53 - 0.5) * 0.0625;
+  }
+}
+
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const int64_t n = (int64_t)T * ST + 512;
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
   if (r) return r;
-  hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8, ctx->stream);
+  if (cio & 8)  // random operands instead of zeros
+    hipLaunchKernelGGL(fill_hash_kernel, dim3(4096), dim3(256), 0, ctx->stream, ctx->A, n * n);
+  else
+    hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8, ctx->stream);
   const unsigned tiles = (unsigned)((int64_t)T * (T + 1) / 2);
   hipStream_t st = ctx->stream;
   const Panel pan{ctx->A, n, 0};
@@ -1513,7 +1527,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     k += w;
   }
   const int S = (int)steps.size();
-  r = ensure_events(ctx, 2 * (size_t)S + 2);
+  r = ensure_events(ctx, 2 * (size_t)S + 3);
   if (r) return r;
   hipStream_t main = ctx->stream, side = ctx->side;
   hipEvent_t* ev = ctx->evs.data();  // [0]: inputs ready; E1_s = ev[1 + 2s]; E2_s = ev[2 + 2s]
@@ -1534,6 +1548,11 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   // schedule 3 needs CUs of its own for the side stream (LFM_SIDE_CUS): its waiting step
   // units would otherwise hold every slot the side stream's factor kernels need
   if (ctx->sched == 3 && ctx->lookahead && ctx->side_cus > 0 && mode == CHOL_MLL) {
+    // the CU-partitioned stream pair, ordered after / before ctx->stream's work
+    hipEventRecord(ev[0], ctx->stream);
+    main = ctx->m3;
+    side = ctx->s3;
+    hipStreamWaitEvent(main, ev[0], 0);
     // Schedule 3. Side stream, per super-panel s (columns [K0, K1), W = K1 - K0): the chain
     // factors only the W x W diagonal block, copied into a workspace with an identity border
     // (chain_init_kernel), so it also yields Bd = L11^{-T}. Main stream: one step_kernel per
@@ -1724,6 +1743,10 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, main, A, lda, n, ctx->parts,
                      (int)npb, ctx->status, negative, d_out, ctx->zvec, zsplit);
   prof_end(ctx, K_FINALIZE, pe, 0, (double)n * 8, main);
+  if (main != ctx->stream) {  // schedule 3 ran on the partitioned pair: back to ctx->stream
+    hipEventRecord(ev[2 * S + 2], main);
+    hipStreamWaitEvent(ctx->stream, ev[2 * S + 2], 0);
+  }
   return hip_fail(ctx, hipGetLastError(), "finalize_kernel");
 }
 

@@ -55,6 +55,8 @@ struct lfm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;  // main stream: gram fill, bulk trailing updates, finalize
   hipStream_t side = nullptr;    // high-priority look-ahead stream: panel factor + solve
+  hipStream_t m3 = nullptr;      // schedule 3: bulk stream (CUs outside the chain's)
+  hipStream_t s3 = nullptr;      // schedule 3: factor-chain stream (LFM_SIDE_CUS CUs)
   bool lookahead = true;
   int trsm_variant = 2;          // panel-solve kernel variant (LFM_TRSM=2|3)
   int syrk_tr = 0;               // force SYRK triangle work-unit rows (LFM_SYRK_TR=64|128)
@@ -80,7 +82,7 @@ struct lfm_ctx {
   unsigned* psync = nullptr;                     // fused panel: [0] factor epoch, [1] slab count
   unsigned panel_epoch = 0;                      // fused panel launches so far
   int side_cus = 0;                              // CUs reserved for the side stream (LFM_SIDE_CUS)
-  int sched = 1;                                 // look-ahead schedule 1 or 2 (LFM_SCHED)
+  int sched = 3;                                 // look-ahead schedule 1, 2 or 3 (LFM_SCHED)
   int fused = 1;                                 // fused panel kernel for w = 1 steps (LFM_FUSED)
   int syrk_pad_kb = 0;                           // extra LDS per slab workgroup: caps residency (LFM_SYRK_PAD_KB)
   int xcd_remap = 1;                             // XCD-contiguous SYRK tile order (LFM_XCD_REMAP)
