@@ -416,7 +416,7 @@ static int gram_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* h
 
 namespace {
 // Main + high-priority side stream (every CU), and for schedule 3 a CU-partitioned pair:
-// LFM_SIDE_CUS (default 16) CUs for the factor chain, the rest for the bulk
+// LFM_SIDE_CUS (default 32) CUs for the factor chain, the rest for the bulk
 // (hipExtStreamCreateWithCUMask). LFM_LOOKAHEAD=0 serialises on one stream.
 hipError_t create_streams(lfm_ctx* ctx) {
   const char* pk = std::getenv("LFM_SYRK_PAD_KB");
@@ -442,7 +442,7 @@ hipError_t create_streams(lfm_ctx* ctx) {
   int least = 0, greatest = 0;
   hipDeviceGetStreamPriorityRange(&least, &greatest);
   const char* sc = std::getenv("LFM_SIDE_CUS");
-  const int side_cus = sc ? std::atoi(sc) : 16;
+  const int side_cus = sc ? std::atoi(sc) : 32;
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, ctx->device);
   const int ncu = prop.multiProcessorCount;
@@ -452,21 +452,35 @@ hipError_t create_streams(lfm_ctx* ctx) {
   if (e != hipSuccess || side_cus <= 0 || side_cus >= ncu) return e;
   // Schedule 3 stream pair: side CUs j * stride (mod ncu), j < side_cus, for the factor chain
   // (LFM_SIDE_STRIDE = 1: consecutive mask bits, which the hardware spreads over the XCDs),
-  // every other CU for the main (bulk) stream.
-  ctx->side_cus = side_cus;
+  // every other CU for the main (bulk) stream. The chain kernel needs all of its workgroups
+  // (one per CU) resident at once: checked here, halving the reservation until it holds.
   const char* sst = std::getenv("LFM_SIDE_STRIDE");
   const int stride = sst ? std::max(1, std::atoi(sst)) : 1;
-  std::vector<char> is_side(ncu, 0);
-  for (int j = 0, c = 0; j < side_cus; ++j) {
-    while (is_side[c]) c = (c + 1) % ncu;
-    is_side[c] = 1;
-    c = (c + stride) % ncu;
+  for (int cus = side_cus; cus >= 4; cus /= 2) {
+    std::vector<char> is_side(ncu, 0);
+    for (int j = 0, c = 0; j < cus; ++j) {
+      while (is_side[c]) c = (c + 1) % ncu;
+      is_side[c] = 1;
+      c = (c + stride) % ncu;
+    }
+    std::vector<uint32_t> mside((ncu + 31) / 32, 0u), mmain((ncu + 31) / 32, 0u);
+    for (int c = 0; c < ncu; ++c) (is_side[c] ? mside : mmain)[c / 32] |= 1u << (c % 32);
+    e = hipExtStreamCreateWithCUMask(&ctx->m3, (uint32_t)mmain.size(), mmain.data());
+    if (e == hipSuccess)
+      e = hipExtStreamCreateWithCUMask(&ctx->s3, (uint32_t)mside.size(), mside.data());
+    if (e != hipSuccess) return e;
+    bool good = false;
+    if (lfm::chain_coresident(ctx, ctx->s3, cus, &good) != LFM_OK) return hipErrorUnknown;
+    if (good) {
+      ctx->side_cus = cus;
+      return hipSuccess;
+    }
+    hipStreamDestroy(ctx->m3);
+    hipStreamDestroy(ctx->s3);
+    ctx->m3 = ctx->s3 = nullptr;
   }
-  std::vector<uint32_t> mside((ncu + 31) / 32, 0u), mmain((ncu + 31) / 32, 0u);
-  for (int c = 0; c < ncu; ++c) (is_side[c] ? mside : mmain)[c / 32] |= 1u << (c % 32);
-  e = hipExtStreamCreateWithCUMask(&ctx->m3, (uint32_t)mmain.size(), mmain.data());
-  if (e != hipSuccess) return e;
-  return hipExtStreamCreateWithCUMask(&ctx->s3, (uint32_t)mside.size(), mside.data());
+  ctx->side_cus = 0;  // no usable partition: schedule 1
+  return hipSuccess;
 }
 }  // namespace
 
@@ -519,7 +533,7 @@ void lfm_ctx_destroy(lfm_ctx* ctx) {
                   (void*)ctx->xin, (void*)ctx->linvT, (void*)ctx->parts, (void*)ctx->status,
                   (void*)ctx->result, (void*)ctx->farm_buf, (void*)ctx->gacc,
                   (void*)ctx->psync, (void*)ctx->wk, (void*)ctx->xbuf, (void*)ctx->zvec,
-                  (void*)ctx->flags})
+                  (void*)ctx->flags, (void*)ctx->linv_full, (void*)ctx->dbg_stamps})
     if (p) hipFree(p);
   if (ctx->hpin) hipHostFree(ctx->hpin);
   for (auto& p : ctx->pending) {
@@ -955,6 +969,29 @@ int lfm_profile_read(lfm_ctx* ctx, lfm_kstat* stats, int max, int* count) {
   *count = K_NCLASS;
   for (int i = 0; i < std::min(max, (int)K_NCLASS); ++i) stats[i] = ctx->stats[i];
   return LFM_OK;
+}
+
+// Diagnostics: enable = 1 turns on s_memrealtime (100 MHz) stamps of the schedule-3 chain
+// kernel's phases (16 per super-panel step, 256 steps); enable = 0 copies them out (max
+// values) and turns them off.
+int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max) {
+  if (!ctx) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  const size_t cnt = 256 * 16;
+  if (enable) {
+    if (!ctx->dbg_stamps) {
+      hipError_t e = hipMalloc((void**)&ctx->dbg_stamps, cnt * 8);
+      if (e != hipSuccess) return hip_fail(ctx, e, "debug stamps");
+    }
+    return hip_fail(ctx, hipMemset(ctx->dbg_stamps, 0, cnt * 8), "debug stamps");
+  }
+  if (!ctx->dbg_stamps) return LFM_OK;
+  finish(ctx);
+  hipError_t e = hipMemcpy(out, ctx->dbg_stamps, std::min<size_t>(cnt, (size_t)max) * 8,
+                           hipMemcpyDeviceToHost);
+  hipFree(ctx->dbg_stamps);
+  ctx->dbg_stamps = nullptr;
+  return hip_fail(ctx, e, "debug stamps");
 }
 
 // ------------------------------------------------------------- RCCL farm

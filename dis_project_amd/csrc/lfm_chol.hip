@@ -134,7 +134,8 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
                                             int64_t lda, int64_t kb, int64_t npiv,
                                             double* __restrict__ dinv,
                                             double* __restrict__ parts, int k,
-                                            int* __restrict__ status) {
+                                            int* __restrict__ status,
+                                            double* __restrict__ Li = nullptr) {
   __shared__ double pvs[NB];  // unscaled pivots
   __shared__ double ipv[NB];  // 1 / L_cc
   __shared__ double red[4];
@@ -281,7 +282,10 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
     }
     if (lane < IB) {
 #pragma unroll
-      for (int r = 0; r < IB; ++r) dinv[(ib * IB + r) * IB + lane] = x[r];
+      for (int r = 0; r < IB; ++r) {
+        dinv[(ib * IB + r) * IB + lane] = x[r];
+        if (Li) Li[(ib * (ib + 1) / 2 + ib) * (IB * (IB + 1)) + r * (IB + 1) + lane] = x[r];
+      }
     }
   }
   // block store (lower triangle incl. diagonal)
@@ -320,6 +324,48 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
     if (b != STATUS_NONE) atomicMin(status, b);
   }
 #undef MS
+}
+
+// Full inverse of a factored 128x128 block (one 256-thread workgroup, after potrf_block with
+// Li): Mb holds L, Li (same packed layout) its 16x16 diagonal inverses; block rows in order,
+//   Linv_IJ = -Dinv_I sum_{K=J}^{I-1} L_IK Linv_KJ   (I > J; fp64 MFMA, waves over J).
+// The 16x16 accumulator layout (row lk + 4r, col li) is the B-operand layout of the next
+// product, so S feeds Dinv_I * S straight from registers. Finally out[k][j] = Linv[j][k]
+// (the transposed inverse: upper triangular, zeros below the diagonal), ld ldo.
+__device__ __forceinline__ void tri_inverse(const double* __restrict__ Mb, double* __restrict__ Li,
+                                            double* __restrict__ out, int64_t ldo) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lk = lane >> 4;
+#define MS(r, q) Mb[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * (IB * (IB + 1)) + \
+                    ((r) & 15) * (IB + 1) + ((q) & 15)]
+#define LI(r, q) Li[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * (IB * (IB + 1)) + \
+                    ((r) & 15) * (IB + 1) + ((q) & 15)]
+  __syncthreads();
+#pragma unroll 1
+  for (int I = 1; I < NB / IB; ++I) {
+    for (int J = w; J < I; J += 4) {
+      double4v sacc = {0, 0, 0, 0};
+      for (int K = J; K < I; ++K)
+#pragma unroll
+        for (int ks = 0; ks < IB / 4; ++ks)
+          sacc = mfma16(MS(I * IB + li, K * IB + 4 * ks + lk), LI(K * IB + 4 * ks + lk, J * IB + li),
+                        sacc);
+      double4v o = {0, 0, 0, 0};
+#pragma unroll
+      for (int ks = 0; ks < IB / 4; ++ks) o = mfma16(LI(I * IB + li, I * IB + 4 * ks + lk), sacc[ks], o);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) LI(I * IB + lk + 4 * r, J * IB + li) = -o[r];
+    }
+    __syncthreads();
+  }
+  for (int idx = tid; idx < NB * (NB / 2); idx += 256) {
+    const int k = idx / (NB / 2), j = 2 * (idx % (NB / 2));
+    double2 v;
+    v.x = j >= k ? LI(j, k) : 0.0;
+    v.y = j + 1 >= k ? LI(j + 1, k) : 0.0;
+    *reinterpret_cast<double2*>(&out[k * ldo + j]) = v;
+  }
+#undef MS
+#undef LI
 }
 
 // (256, 4): at most 128 VGPRs, so the factor fits in the registers one bulk-SYRK workgroup frees
@@ -550,27 +596,31 @@ __device__ __forceinline__ double2 ld2(const double* p) {
   return *reinterpret_cast<const double2*>(p);
 }
 
-template <int TR, bool BT = false, bool COH = false>
+// KS: depth of one LDS stage (16 in the bulk kernels; 64 where one workgroup per CU has no
+// neighbours to hide the global-load latency behind — the side stream's chain kernel).
+template <int TR, bool BT = false, bool COH = false, int KS = KB>
 __device__ __forceinline__ void gemm_accumulate(const double* __restrict__ pi, int64_t ldi,
                                                 const double* __restrict__ pj, int64_t ldj,
                                                 int kd, double (&acc)[TR / 8][4],
-                                                double (*__restrict__ sP)[KB + 1]) {
+                                                double (*__restrict__ sP)[KS + 1]) {
   constexpr int IRN = TR / 8;
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));  // opaque: lane offsets are recomputed, not held live
   const int lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
   const int li = lane & 15, lk = lane >> 4, l3 = lane & 3;
-  // staging: TR rows of panel i and 128 rows of panel j, KB doubles each; thread tid moves
-  // chunk (tid & 7) of rows (tid >> 3) + 32u. K-major j panel: thread tid moves the double2
-  // (k = idx >> 6, j = 2 (idx & 63)) of idx = tid + 256u and stores it transposed.
-  static_assert(KB == 16, "staging map assumes 8 double2 chunks per row");
-  constexpr int NUI = TR / 32, NU = NUI + 4;
-  const int srow = tid >> 3, sch = tid & 7;
+  // staging: TR rows of panel i and 128 rows of panel j, KS doubles each; a row is CH double2
+  // chunks, thread tid moves chunk (tid % CH) of rows tid / CH + RP u. K-major j panel:
+  // thread tid moves the double2 (k = idx >> 6, j = 2 (idx & 63)) of idx = tid + 256u and
+  // stores it transposed.
+  static_assert(KS % 16 == 0 && KS <= 64, "stage depth");
+  constexpr int CH = KS / 2, RP = 256 / CH;
+  constexpr int NUI = TR / RP, NUJ = ST / RP, NU = NUI + NUJ;
+  const int srow = tid / CH, sch = tid % CH;
   const double* gi = pi + srow * ldi + 2 * sch;
   const double* gj = BT ? pj + (tid >> 6) * ldj + 2 * (tid & 63) : pj + srow * ldj + 2 * sch;
-  const int li32 = (int)(32 * ldi);
-  const int lj32 = BT ? (int)(4 * ldj) : (int)(32 * ldj);
+  const int li32 = (int)(RP * ldi);
+  const int lj32 = BT ? (int)(4 * ldj) : (int)(RP * ldj);
   double2 pre[NU];
   auto gload = [&](int k0) {
     // row offsets recomputed per call (opaque stride) rather than held as live 64-bit pointers
@@ -580,34 +630,34 @@ __device__ __forceinline__ void gemm_accumulate(const double* __restrict__ pi, i
     for (int u = 0; u < NUI; ++u) pre[u] = ld2<COH>(gi + u * l32 + k0);
     const double* gjk = BT ? gj + (int64_t)k0 * ldj : gj + k0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) pre[NUI + u] = ld2<COH>(gjk + u * m32);
+    for (int u = 0; u < NUJ; ++u) pre[NUI + u] = ld2<COH>(gjk + u * m32);
   };
   gload(0);
-  for (int k0 = 0; k0 < kd; k0 += KB) {
+  for (int k0 = 0; k0 < kd; k0 += KS) {
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < NUI; ++u) {
-      double* d = &sP[srow + 32 * u][2 * sch];
+      double* d = &sP[srow + RP * u][2 * sch];
       d[0] = pre[u].x;
       d[1] = pre[u].y;
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < NUJ; ++u) {
       if (BT) {
         const int kr = (tid >> 6) + 4 * u, jc = 2 * (tid & 63);
         sP[TR + jc][kr] = pre[NUI + u].x;
         sP[TR + jc + 1][kr] = pre[NUI + u].y;
       } else {
-        double* d = &sP[TR + srow + 32 * u][2 * sch];
+        double* d = &sP[TR + srow + RP * u][2 * sch];
         d[0] = pre[NUI + u].x;
         d[1] = pre[NUI + u].y;
       }
     }
     __syncthreads();
-    if (k0 + KB < kd) gload(k0 + KB);
+    if (k0 + KS < kd) gload(k0 + KS);
     {
 #pragma unroll 1
-      for (int kk = 0; kk < KB; kk += 4) {
+      for (int kk = 0; kk < KS; kk += 4) {
         double bb[4];
 #pragma unroll
         for (int jr = 0; jr < 4; ++jr) bb[jr] = sP[TR + wc + jr * 16 + li][kk + lk];
@@ -641,10 +691,10 @@ struct Panel {
 // One TR x 128 work unit of a band / triangle launch: C -= P_i P_j^T over panel depth kd,
 // C the lower part of the trailing matrix of A starting at row / column s. b = the unit's
 // index in the enumeration below.
-template <bool CIO, int TR, bool COH = false>
+template <bool CIO, int TR, bool COH = false, int KS = KB>
 __device__ __forceinline__ void syrk_unit(double* __restrict__ A, int64_t lda, int64_t s, Panel P,
                                           int kd, int T, int tj_lo, int tj_hi, int64_t b, int ti0,
-                                          double (*__restrict__ sP)[KB + 1]) {
+                                          double (*__restrict__ sP)[KS + 1]) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
@@ -681,7 +731,8 @@ __device__ __forceinline__ void syrk_unit(double* __restrict__ A, int64_t lda, i
   for (int ir = 0; ir < IRN; ++ir)
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = CIO ? -Cb[ir * ld4 + jr * 16] : 0.0;
-  gemm_accumulate<TR>(P.p + (i0 - P.r0) * P.ld, P.ld, P.p + (j0 - P.r0) * P.ld, P.ld, kd, acc, sP);
+  gemm_accumulate<TR, false, false, KS>(P.p + (i0 - P.r0) * P.ld, P.ld, P.p + (j0 - P.r0) * P.ld,
+                                        P.ld, kd, acc, sP);
 
   int ld4s = ld4;
   asm volatile("" : "+v"(ld4s));  // recompute store addresses instead of keeping 64 pointers live
@@ -1039,12 +1090,17 @@ struct ChainArgs {
   int kd;
   int64_t n;
   double* dinv;
+  double* linv;       // 128 x 128: transposed inverse of the current diagonal block (w > 1)
   double* parts;
   int* status;
   double* zvec;
   unsigned* bar;      // grid barrier counter (zeroed per call)
   unsigned* done;     // chain_done[s]
+  unsigned long long* stamps;  // diagnostics (NULL: off): s_memrealtime per phase, [16]
 };
+
+// dynamic LDS of chain_kernel: the factor block and its inverse (packed 16x16 blocks)
+constexpr size_t CHAIN_LDS = 2 * (size_t)MB_DOUBLES * sizeof(double);
 
 // Grid barrier over the chain kernel's co-resident workgroups: release, count, acquire.
 // Bounded: on timeout (or a timeout already recorded in *status) it returns false at once.
@@ -1072,14 +1128,19 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, int* s
   return ok;
 }
 
+constexpr int CKS = 64;  // chain kernel GEMM stage depth
+static_assert(2 * MB_DOUBLES >= (64 + ST) * (CKS + 1), "chain LDS union");
 __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double (*sP)[KB + 1] = reinterpret_cast<double (*)[KB + 1]>(smem);
-  double (*sA)[NB + 1] = reinterpret_cast<double (*)[NB + 1]>(smem);
+  double (*sP)[CKS + 1] = reinterpret_cast<double (*)[CKS + 1]>(smem);
   const int G = gridDim.x, wg = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int W = g.w * NB;
   double* Aw = g.Wk - (g.Kc * W + g.Kc);  // the workspace with the matrix's row / column numbers
   unsigned nbar = 0;
+  auto stamp = [&](int p) {
+    if (g.stamps && wg == 0 && tid == 0 && p < 16) g.stamps[p] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   // P0: pending update of the block into the workspace (lower 128-tiles, 2 slabs each)
   {
     const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64, li = lane & 15, lk = lane >> 4;
@@ -1097,8 +1158,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
 #pragma unroll
         for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = -Cs[(ir * 4) * g.lda + jr * 16];
       if (g.kd > 0)
-        gemm_accumulate<64>(g.Xp + (i0 - g.Kc) * g.ldx, g.ldx, g.Xp + (j0 - g.Kc) * g.ldx, g.ldx,
-                            g.kd, acc, sP);
+        gemm_accumulate<64, false, false, CKS>(g.Xp + (i0 - g.Kc) * g.ldx, g.ldx,
+                                               g.Xp + (j0 - g.Kc) * g.ldx, g.ldx, g.kd, acc, sP);
       double* Cd = Aw + (i0 + wr + lk) * W + j0 + wc + li;
 #pragma unroll
       for (int ir = 0; ir < 8; ++ir)
@@ -1114,31 +1175,51 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
       *reinterpret_cast<double2*>(&g.Wk[(int64_t)(W + r) * W + c]) = v;
     }
   }
+  stamp(1);
   bool ok = grid_sync(g.bar, G * ++nbar, g.status);
+  stamp(2);
   for (int c = 0; c < g.w && ok; ++c) {
     const int64_t kb = g.Kc + (int64_t)c * NB, r0 = kb + NB;
-    if (wg == 0) potrf_block<15>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB), g.status);
+    // workgroup 0: factor block c and its full inverse; transposed into Bd directly when it is
+    // the only block (w = 1: Bd = L11^{-T}), else into linv for the panel solve below
+    if (wg == 0) {
+      double* Li = smem + MB_DOUBLES;
+      potrf_block<15>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB), g.status, Li);
+      stamp(3 + 3 * c);
+      tri_inverse(smem, Li, g.w == 1 ? g.Wk + (int64_t)W * W : g.linv, g.w == 1 ? W : NB);
+      stamp(4 + 3 * c);
+    }
+    if (g.w == 1) break;
     ok = grid_sync(g.bar, G * ++nbar, g.status);
     if (!ok) break;
+    // panel solve of every workspace row below block c as a GEMM: X = A_c Linv_c^T
     const int64_t rows = g.Kc + 2 * W - r0;
-    for (int64_t u = wg; u < rows / 64; u += G) {
-      const int64_t ra = r0 + 64 * u;
-      for (int idx = tid; idx < 64 * (NB / 2); idx += 256) {
-        const int r = idx / (NB / 2), q2 = idx - r * (NB / 2);
-        const double2 v = *reinterpret_cast<const double2*>(&Aw[(ra + r) * W + kb + 2 * q2]);
-        sA[r][2 * q2] = v.x;
-        sA[r][2 * q2 + 1] = v.y;
+    {
+      const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64, li = lane & 15, lk = lane >> 4;
+      for (int64_t u = wg; u < rows / 64; u += G) {
+        const int64_t ra = r0 + 64 * u;
+        double acc[8][4];
+#pragma unroll
+        for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+          for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = 0.0;
+        gemm_accumulate<64, true, false, CKS>(Aw + ra * W + kb, W, g.linv, NB, NB, acc, sP);
+        __syncthreads();  // every wave's operand reads of these rows are done
+        double* Xb = Aw + (ra + wr + lk) * W + kb + wc + li;
+#pragma unroll
+        for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+          for (int jr = 0; jr < 4; ++jr) Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
       }
-      trsm_rows(sA, Aw, W, ra, kb, g.dinv);
-      __syncthreads();
     }
     ok = grid_sync(g.bar, G * ++nbar, g.status);
+    stamp(5 + 3 * c);
     if (!ok || c + 1 == g.w) break;
     const int T = (int)(rows / ST), hi = g.w - 1 - c;
     int64_t nunit = 0;
     for (int tj = 0; tj < hi; ++tj) nunit += 2 * (T - tj);
     for (int64_t u = wg; u < nunit; u += G) {
-      syrk_unit<true, 64>(Aw, W, r0, Panel{Aw + kb, W, 0}, NB, T, 0, hi, u, 0, sP);
+      syrk_unit<true, 64, false, CKS>(Aw, W, r0, Panel{Aw + kb, W, 0}, NB, T, 0, hi, u, 0, sP);
       __syncthreads();
     }
     ok = grid_sync(g.bar, G * ++nbar, g.status);
@@ -1148,8 +1229,43 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
       for (int c = tid; c < W; c += 256) g.zvec[g.Kc + c] = g.Wk[(g.n - g.Kc) * W + c];
     __threadfence();
     __syncthreads();
+    stamp(15);
     if (tid == 0) __hip_atomic_store(g.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// Start-up check for schedule 3: can gridDim.x chain-sized workgroups (CHAIN_LDS each, so one
+// per CU) be resident together on the side stream's CUs? Each arrives at a counter and waits
+// (bounded, ~0.1 s) for all; ok[0] = 1 when every one saw the full count.
+__global__ __launch_bounds__(256) void coresident_kernel(unsigned* bar, int* ok) {
+  extern __shared__ double pad[];
+  if (threadIdx.x == 0) {
+    pad[0] = 0.0;
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned it = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gridDim.x &&
+           ++it < (1u << 20))
+      __builtin_amdgcn_s_sleep(2);
+    if (it >= (1u << 20)) atomicExch(ok, 0);
+  }
+}
+
+int chain_coresident(lfm_ctx* ctx, hipStream_t st, int G, bool* good) {
+  hipFuncSetAttribute(reinterpret_cast<const void*>(&coresident_kernel),
+                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS);
+  unsigned* d = nullptr;
+  hipError_t e = hipMalloc((void**)&d, 16);
+  if (e != hipSuccess) return hip_fail(ctx, e, "coresident probe");
+  const unsigned init[2] = {0u, 1u};
+  hipMemcpyAsync(d, init, 8, hipMemcpyHostToDevice, st);
+  hipLaunchKernelGGL(coresident_kernel, dim3((unsigned)G), dim3(256), CHAIN_LDS, st, d,
+                     reinterpret_cast<int*>(d + 1));
+  unsigned h[2] = {0u, 0u};
+  hipMemcpyAsync(h, d, 8, hipMemcpyDeviceToHost, st);
+  e = hipStreamSynchronize(st);
+  hipFree(d);
+  *good = e == hipSuccess && h[0] == (unsigned)G && h[1] == 1u;
+  return hip_fail(ctx, e, "coresident probe");
 }
 
 // ------------------------------------------------------------- finalize
@@ -1496,6 +1612,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     hipFuncSetAttribute(reinterpret_cast<const void*>(&potrf_diag_kernel<15>),
                         hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)(MB_DOUBLES * sizeof(double)));
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_kernel),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS);
     attr = true;
   }
   // CHOL_MLL: factor the Mp x Mp augmented matrix (block columns holding pivots only).
@@ -1567,6 +1685,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     if (!r)
       r = ensure(ctx, (void**)&ctx->xbuf, &ctx->xbuf_bytes, (size_t)2 * Mp * Wmax * sizeof(double));
     if (!r) r = ensure(ctx, (void**)&ctx->zvec, &ctx->zvec_bytes, (size_t)Mp * sizeof(double));
+    if (!r)
+      r = ensure(ctx, (void**)&ctx->linv_full, &ctx->linv_full_bytes, (size_t)NB * NB * sizeof(double));
     const size_t nflags = (size_t)S * (2 + Tmax);
     if (!r) r = ensure(ctx, (void**)&ctx->flags, &ctx->flags_bytes, nflags * sizeof(unsigned));
     if (r) return r;
@@ -1591,14 +1711,16 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       }
       c.n = n;
       c.dinv = ctx->linvT;
+      c.linv = ctx->linv_full;
       c.parts = ctx->parts;
       c.status = ctx->status;
       c.zvec = ctx->zvec;
       c.bar = bars + s;
       c.done = chain_done + s;
+      c.stamps = ctx->dbg_stamps ? ctx->dbg_stamps + 16 * (size_t)std::min(s, 255) : nullptr;
       hipEvent_t pe;
       prof_begin(ctx, K_POTRF, &pe, side);
-      hipLaunchKernelGGL(chain_kernel, dim3((unsigned)ctx->side_cus), dim3(256), PANEL_LDS, side, c);
+      hipLaunchKernelGGL(chain_kernel, dim3((unsigned)ctx->side_cus), dim3(256), CHAIN_LDS, side, c);
       const double W = c.w * NB;
       prof_end(ctx, K_POTRF, pe, W * W * W / 3.0 + W * W * W, 0, side);
     };

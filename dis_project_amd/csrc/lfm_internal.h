@@ -78,6 +78,7 @@ struct lfm_ctx {
   double* wk = nullptr; size_t wk_bytes = 0;     // schedule 3: diagonal block + identity border
   double* xbuf = nullptr; size_t xbuf_bytes = 0; // schedule 3: solved panel X = A21 L11^{-T}
   double* zvec = nullptr; size_t zvec_bytes = 0; // schedule 3: z = L^{-1} r
+  double* linv_full = nullptr; size_t linv_full_bytes = 0; // schedule 3: 128x128 block inverse
   unsigned* flags = nullptr; size_t flags_bytes = 0; // schedule 3: per-step device flags
   unsigned* psync = nullptr;                     // fused panel: [0] factor epoch, [1] slab count
   unsigned panel_epoch = 0;                      // fused panel launches so far
@@ -89,6 +90,8 @@ struct lfm_ctx {
   int prio_mask = 1;                             // raise look-ahead SYRK band wave priority (LFM_BAND_PRIO)
   double* result = nullptr;                      // [0..] scalar results
   double* gacc = nullptr; size_t gacc_bytes = 0; // gradient accumulators + output
+
+  unsigned long long* dbg_stamps = nullptr;     // chain phase stamps (lfm_debug_stamps), 256 x 16
 
   // pinned host staging
   double* hpin = nullptr; size_t hpin_bytes = 0;
@@ -122,6 +125,7 @@ int ensure_events(lfm_ctx* ctx, size_t count);
 int prof_flush(lfm_ctx* ctx);
 
 GridLayout detect_grid(const double* x, int64_t n, int64_t G);
+int chain_coresident(lfm_ctx* ctx, hipStream_t st, int G, bool* good);
 int gene_clamp_host(double g, int64_t G);
 
 // device-side gene index semantics: trunc toward zero, negative wraps, clamp

@@ -170,6 +170,9 @@ int lfm_profile_classes(lfm_ctx* ctx, unsigned mask);
 int lfm_profile_reset(lfm_ctx* ctx);
 /* Copies up to max entries; *count = number of kernel classes seen. */
 int lfm_profile_read(lfm_ctx* ctx, lfm_kstat* stats, int max, int* count);
+/* Diagnostics: phase timestamps (s_memrealtime, 100 MHz) of the schedule-3 factor chain,
+ * 16 per super-panel step. enable = 1 arms them; enable = 0 copies up to max out. */
+int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max);
 
 /* -------------------------------- multi-GPU farm: RCCL all-gather over xGMI */
 /* Rank 0 creates the 128-byte unique id; the caller ships it to every rank. */
