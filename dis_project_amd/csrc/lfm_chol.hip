@@ -216,6 +216,40 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
 #pragma unroll
     for (int r = 0; r < 4; ++r) MS(i0 + lk + 4 * r, j0 + li) = acc[r];
   };
+  // With Li (the full inverse is wanted), waves 1-3 build it in the time the look-ahead leaves
+  // them: Dinv_I (16x16 inverse of L_II, forward substitution, lane = column) and the blocks
+  // Linv_IJ = -Dinv_I sum_{K=J}^{I-1} L_IK Linv_KJ of block row I (fp64 MFMA; the 16x16
+  // accumulator layout is the B-operand layout of the next product).
+#define LI(r, q) Li[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * (IB * (IB + 1)) + \
+                    ((r) & 15) * (IB + 1) + ((q) & 15)]
+  auto dinv_block = [&](int I) {
+    const int c0 = I * IB;
+    double x[IB];
+#pragma unroll
+    for (int r = 0; r < IB; ++r) {
+      double sacc = (li == r) ? 1.0 : 0.0;
+#pragma unroll
+      for (int q = 0; q < r; ++q) sacc = fma(-MS(c0 + r, c0 + q), x[q], sacc);
+      x[r] = sacc * ipv[c0 + r];
+    }
+    if (lane < IB) {
+#pragma unroll
+      for (int r = 0; r < IB; ++r) LI(c0 + r, c0 + lane) = x[r];
+    }
+  };
+  auto linv_block = [&](int I, int J) {
+    double4v sacc = {0, 0, 0, 0};
+    for (int K = J; K < I; ++K)
+#pragma unroll
+      for (int ks = 0; ks < IB / 4; ++ks)
+        sacc = mfma16(MS(I * IB + li, K * IB + 4 * ks + lk), LI(K * IB + 4 * ks + lk, J * IB + li),
+                      sacc);
+    double4v o = {0, 0, 0, 0};
+#pragma unroll
+    for (int ks = 0; ks < IB / 4; ++ks) o = mfma16(LI(I * IB + li, I * IB + 4 * ks + lk), sacc[ks], o);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) LI(I * IB + lk + 4 * r, J * IB + li) = -o[r];
+  };
   if ((PH & 1) && w == 0) leaf(0);
   __syncthreads();
 #pragma unroll 1
@@ -265,12 +299,29 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
         }
       }
     }
+    if (Li && w > 0) {
+      // Dinv_ib (L_ib,ib final since leaf(ib)); block row ib - 1 (Dinv_{ib-1} from last pass)
+      if (w == 1) dinv_block(ib);
+      else
+        for (int J = w - 2; J < ib - 1; J += 2) linv_block(ib - 1, J);
+    }
     __syncthreads();
   }
+  if (Li) {
+    // remaining: Dinv_7 with block row 6, then block row 7
+    constexpr int L7 = NB / IB - 1;
+    if (w == 0) dinv_block(L7);
+    else
+      for (int J = w - 1; J < L7 - 1; J += 3) linv_block(L7 - 1, J);
+    __syncthreads();
+    for (int J = w; J < L7; J += 4) linv_block(L7, J);
+  }
+#undef LI
   // inverses of the eight 16x16 diagonal blocks: wave w builds blocks w and w + 4,
   // lane c (< 16) column c by forward substitution; dinv[ib][r][c] = X[r][c]
+  // (not needed with Li: the caller uses the full inverse)
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < (Li ? 0 : 2); ++h) {
     const int ib = w + 4 * h, c0 = ib * IB;
     double x[IB];
 #pragma unroll
@@ -284,7 +335,6 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
 #pragma unroll
       for (int r = 0; r < IB; ++r) {
         dinv[(ib * IB + r) * IB + lane] = x[r];
-        if (Li) Li[(ib * (ib + 1) / 2 + ib) * (IB * (IB + 1)) + r * (IB + 1) + lane] = x[r];
       }
     }
   }
@@ -326,45 +376,20 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
 #undef MS
 }
 
-// Full inverse of a factored 128x128 block (one 256-thread workgroup, after potrf_block with
-// Li): Mb holds L, Li (same packed layout) its 16x16 diagonal inverses; block rows in order,
-//   Linv_IJ = -Dinv_I sum_{K=J}^{I-1} L_IK Linv_KJ   (I > J; fp64 MFMA, waves over J).
-// The 16x16 accumulator layout (row lk + 4r, col li) is the B-operand layout of the next
-// product, so S feeds Dinv_I * S straight from registers. Finally out[k][j] = Linv[j][k]
-// (the transposed inverse: upper triangular, zeros below the diagonal), ld ldo.
-__device__ __forceinline__ void tri_inverse(const double* __restrict__ Mb, double* __restrict__ Li,
-                                            double* __restrict__ out, int64_t ldo) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 15, lk = lane >> 4;
-#define MS(r, q) Mb[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * (IB * (IB + 1)) + \
-                    ((r) & 15) * (IB + 1) + ((q) & 15)]
+// out[k][j] = Linv[j][k] (the transposed inverse of the factored block: upper triangular,
+// zeros below the diagonal), ld ldo, from Li (packed 16x16 blocks, built by potrf_block).
+__device__ __forceinline__ void store_inverse_t(const double* __restrict__ Li,
+                                                double* __restrict__ out, int64_t ldo) {
 #define LI(r, q) Li[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * (IB * (IB + 1)) + \
                     ((r) & 15) * (IB + 1) + ((q) & 15)]
   __syncthreads();
-#pragma unroll 1
-  for (int I = 1; I < NB / IB; ++I) {
-    for (int J = w; J < I; J += 4) {
-      double4v sacc = {0, 0, 0, 0};
-      for (int K = J; K < I; ++K)
-#pragma unroll
-        for (int ks = 0; ks < IB / 4; ++ks)
-          sacc = mfma16(MS(I * IB + li, K * IB + 4 * ks + lk), LI(K * IB + 4 * ks + lk, J * IB + li),
-                        sacc);
-      double4v o = {0, 0, 0, 0};
-#pragma unroll
-      for (int ks = 0; ks < IB / 4; ++ks) o = mfma16(LI(I * IB + li, I * IB + 4 * ks + lk), sacc[ks], o);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) LI(I * IB + lk + 4 * r, J * IB + li) = -o[r];
-    }
-    __syncthreads();
-  }
-  for (int idx = tid; idx < NB * (NB / 2); idx += 256) {
+  for (int idx = threadIdx.x; idx < NB * (NB / 2); idx += 256) {
     const int k = idx / (NB / 2), j = 2 * (idx % (NB / 2));
     double2 v;
     v.x = j >= k ? LI(j, k) : 0.0;
     v.y = j + 1 >= k ? LI(j + 1, k) : 0.0;
     *reinterpret_cast<double2*>(&out[k * ldo + j]) = v;
   }
-#undef MS
 #undef LI
 }
 
@@ -691,10 +716,12 @@ struct Panel {
 // One TR x 128 work unit of a band / triangle launch: C -= P_i P_j^T over panel depth kd,
 // C the lower part of the trailing matrix of A starting at row / column s. b = the unit's
 // index in the enumeration below.
+// Returns whether the unit's tile lies in the leading coh_lim x coh_lim tiles of the trailing
+// matrix (stores then write through to memory: device-coherent, for an in-flight reader).
 template <bool CIO, int TR, bool COH = false, int KS = KB>
-__device__ __forceinline__ void syrk_unit(double* __restrict__ A, int64_t lda, int64_t s, Panel P,
+__device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, int64_t s, Panel P,
                                           int kd, int T, int tj_lo, int tj_hi, int64_t b, int ti0,
-                                          double (*__restrict__ sP)[KS + 1]) {
+                                          double (*__restrict__ sP)[KS + 1], int coh_lim = 0) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
@@ -723,6 +750,8 @@ __device__ __forceinline__ void syrk_unit(double* __restrict__ A, int64_t lda, i
   }
   const int64_t i0 = s + (int64_t)ti * TR, j0 = s + (int64_t)tj * ST;
   const bool diag = i0 < j0 + ST;  // the tile reaches the diagonal: keep col <= row only
+  const bool in_lead = (i0 - s) / ST < coh_lim && (j0 - s) / ST < coh_lim;
+  const bool coh = COH || in_lead;
   double* Cb = A + (i0 + wr + lk) * lda + j0 + wc + li;  // C[wr + lk][wc + li]
   const int ld4 = (int)(4 * lda);  // row-group stride (elements); 60 * ld4 < 2^31 for lda < 2^23
 
@@ -742,8 +771,8 @@ __device__ __forceinline__ void syrk_unit(double* __restrict__ A, int64_t lda, i
     for (int jr = 0; jr < 4; ++jr) {
       const int64_t row = i0 + wr + ir * 4 + lk, col = j0 + wc + jr * 16 + li;
       if (CIO && (!diag || col <= row)) {
-        // COH: device-coherent (write-through) stores, read by another XCD in this launch
-        if (COH)
+        // coh: device-coherent (write-through) stores, read by another XCD in flight
+        if (coh)
           __hip_atomic_store(&Cb[ir * ld4s + jr * 16], -acc[ir][jr], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
         else
@@ -751,6 +780,7 @@ __device__ __forceinline__ void syrk_unit(double* __restrict__ A, int64_t lda, i
       }
       if (!CIO && acc[ir][jr] == 1.2345e300) Cb[0] = 0.0;  // keep the MFMAs live
     }
+  return in_lead;
 }
 
 // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs (each with its own L2), so
@@ -896,7 +926,19 @@ struct StepArgs {
   unsigned* a_done;  // [T] per tile row of step s (NULL: no wait)
   const unsigned* chain_done;  // NULL: no wait
   int* status;
+  // inputs of chain(s + 2), which starts while this launch runs: the rest units of the block
+  // (lead x lead leading tiles of the rest triangle) and the tall units of its rows (row
+  // slabs < lead_slabs) write through to memory and bump *xready when done
+  unsigned* xready;  // NULL: no chain waits on this launch
+  int lead, lead_slabs;
 };
+
+__device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
+  __builtin_amdgcn_s_waitcnt(0);  // this thread's write-through stores have completed
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 
 __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
@@ -929,7 +971,9 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
     return;
   }
   if (role == 2) {
-    syrk_unit<true, 64>(g.A, g.lda, g.s0, g.px, g.kd, g.T, g.wn, g.T, u, 0, sP);
+    const bool lead = syrk_unit<true, 64>(g.A, g.lda, g.s0, g.px, g.kd, g.T, g.wn, g.T, u, 0, sP,
+                                          g.xready ? g.wn + g.lead : 0);
+    if (lead) bump_after_stores(g.xready);
     return;
   }
   // tall unit (row slab rb, column block cb) of step s + 1
@@ -965,13 +1009,19 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
   gemm_accumulate<64, true, true>(g.A + i0 * g.lda + g.tk0, g.lda, g.Bd + cb * NB, W,
                                   NB * (cb + 1), acc, sP);
   double* Xb = g.X + (i0 - g.tr0 + wr + lk) * W + cb * NB + wc + li;
+  const bool lead = g.xready && (i0 - g.tr0) / 64 < g.lead_slabs;
 #pragma unroll
   for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) {
-      Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
+      if (lead)
+        __hip_atomic_store(&Xb[(ir * 4) * W + jr * 16], acc[ir][jr], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      else
+        Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
       if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + cb * NB + wc + jr * 16 + li] = acc[ir][jr];
     }
+  if (lead) bump_after_stores(g.xready);
 }
 
 // Row n of the chain workspace (n inside the super-panel's diagonal block) into zvec.
@@ -1097,6 +1147,8 @@ struct ChainArgs {
   unsigned* bar;      // grid barrier counter (zeroed per call)
   unsigned* done;     // chain_done[s]
   unsigned long long* stamps;  // diagnostics (NULL: off): s_memrealtime per phase, [16]
+  const unsigned* xready;  // NULL: inputs ready at launch; else wait for *xready >= xtarget and
+  unsigned xtarget;        // read A[D] and X_{s-1} with device-coherent loads
 };
 
 // dynamic LDS of chain_kernel: the factor block and its inverse (packed 16x16 blocks)
@@ -1141,6 +1193,17 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     if (g.stamps && wg == 0 && tid == 0 && p < 16) g.stamps[p] = __builtin_amdgcn_s_memrealtime();
   };
   stamp(0);
+  // the block's inputs come from the main stream's launch in flight: wait for its count
+  if (g.xready) {
+    __shared__ int okx;
+    if (tid == 0) okx = spin_until<false>(g.xready, g.xtarget);
+    __syncthreads();
+    if (!okx) {
+      if (tid == 0) atomicMin(g.status, PANEL_TIMEOUT);
+      return;
+    }
+  }
+  stamp(14);
   // P0: pending update of the block into the workspace (lower 128-tiles, 2 slabs each)
   {
     const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64, li = lane & 15, lk = lane >> 4;
@@ -1156,10 +1219,18 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
 #pragma unroll
       for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
-        for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = -Cs[(ir * 4) * g.lda + jr * 16];
-      if (g.kd > 0)
-        gemm_accumulate<64, false, false, CKS>(g.Xp + (i0 - g.Kc) * g.ldx, g.ldx,
-                                               g.Xp + (j0 - g.Kc) * g.ldx, g.ldx, g.kd, acc, sP);
+        for (int jr = 0; jr < 4; ++jr)
+          acc[ir][jr] = -(g.xready ? __hip_atomic_load(&Cs[(ir * 4) * g.lda + jr * 16],
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : Cs[(ir * 4) * g.lda + jr * 16]);
+      if (g.kd > 0) {
+        if (g.xready)
+          gemm_accumulate<64, false, true, CKS>(g.Xp + (i0 - g.Kc) * g.ldx, g.ldx,
+                                                g.Xp + (j0 - g.Kc) * g.ldx, g.ldx, g.kd, acc, sP);
+        else
+          gemm_accumulate<64, false, false, CKS>(g.Xp + (i0 - g.Kc) * g.ldx, g.ldx,
+                                                 g.Xp + (j0 - g.Kc) * g.ldx, g.ldx, g.kd, acc, sP);
+      }
       double* Cd = Aw + (i0 + wr + lk) * W + j0 + wc + li;
 #pragma unroll
       for (int ir = 0; ir < 8; ++ir)
@@ -1186,7 +1257,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
       double* Li = smem + MB_DOUBLES;
       potrf_block<15>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB), g.status, Li);
       stamp(3 + 3 * c);
-      tri_inverse(smem, Li, g.w == 1 ? g.Wk + (int64_t)W * W : g.linv, g.w == 1 ? W : NB);
+      store_inverse_t(Li, g.w == 1 ? g.Wk + (int64_t)W * W : g.linv, g.w == 1 ? W : NB);
       stamp(4 + 3 * c);
     }
     if (g.w == 1) break;
@@ -1632,15 +1703,23 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   if (r) return r;
   // step plan: super-panels of w = 4, 2 or 1 block columns while the trailing matrix is
   // large, so the bulk trailing update runs with depth 128 w (C traffic per flop / w)
-  const int64_t w4min = env_int("LFM_W4_MIN", 6144), w2min = env_int("LFM_W2_MIN", 4096);
+  const bool s3 = ctx->sched == 3 && ctx->lookahead && ctx->side_cus > 0 && mode == CHOL_MLL;
+  // schedule 3 goes from w = 4 straight to w = 1 (its w = 2 steps are chain-bound and slower
+  // per block column than w = 1 steps)
+  const int64_t w4min = env_int("LFM_W4_MIN", 6144);
+  const int64_t w2min = env_int("LFM_W2_MIN", s3 ? (1 << 30) : 4096);
   const int64_t w8min = env_int("LFM_W8_MIN", 1 << 30);
   std::vector<std::pair<int64_t, int>> steps;
+  // schedule 3: the first super-panel's factor and solve precede any bulk work, so it is kept
+  // narrow (LFM_FIRST_W, default 1); the next one's chain hides behind step 0's update
+  const int first_w = s3 ? env_int("LFM_FIRST_W", 1) : 0;
   for (int64_t k = 0; k < nblk;) {
     const int64_t m = bordered ? Mp + NB : Mp - k * NB;
     int w = 1;
     if (m >= w8min && k + 8 <= nblk) w = 8;
     else if (m >= w4min && k + 4 <= nblk) w = 4;
     else if (m >= w2min && k + 2 <= nblk) w = 2;
+    if (k == 0 && first_w > 0) w = std::min(w, first_w);
     steps.emplace_back(k, w);
     k += w;
   }
@@ -1665,7 +1744,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   int64_t zsplit = 0;  // finalize: z columns below zsplit come from ctx->zvec
   // schedule 3 needs CUs of its own for the side stream (LFM_SIDE_CUS): its waiting step
   // units would otherwise hold every slot the side stream's factor kernels need
-  if (ctx->sched == 3 && ctx->lookahead && ctx->side_cus > 0 && mode == CHOL_MLL) {
+  if (s3) {
     // the CU-partitioned stream pair, ordered after / before ctx->stream's work
     hipEventRecord(ev[0], ctx->stream);
     main = ctx->m3;
@@ -1681,13 +1760,14 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     int wmax = 1;
     for (const auto& st : steps) wmax = std::max(wmax, st.second);
     const int64_t Wmax = (int64_t)wmax * NB, Tmax = Mp / ST + 1;
-    r = ensure(ctx, (void**)&ctx->wk, &ctx->wk_bytes, (size_t)2 * Wmax * Wmax * sizeof(double));
+    // two workspaces: chain(s + 1) starts while the tall units of step s still read Bd_s
+    r = ensure(ctx, (void**)&ctx->wk, &ctx->wk_bytes, (size_t)4 * Wmax * Wmax * sizeof(double));
     if (!r)
       r = ensure(ctx, (void**)&ctx->xbuf, &ctx->xbuf_bytes, (size_t)2 * Mp * Wmax * sizeof(double));
     if (!r) r = ensure(ctx, (void**)&ctx->zvec, &ctx->zvec_bytes, (size_t)Mp * sizeof(double));
     if (!r)
       r = ensure(ctx, (void**)&ctx->linv_full, &ctx->linv_full_bytes, (size_t)NB * NB * sizeof(double));
-    const size_t nflags = (size_t)S * (2 + Tmax);
+    const size_t nflags = (size_t)S * (3 + Tmax);
     if (!r) r = ensure(ctx, (void**)&ctx->flags, &ctx->flags_bytes, nflags * sizeof(unsigned));
     if (r) return r;
     unsigned* chain_done = ctx->flags;     // [S]
@@ -1696,6 +1776,14 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     zsplit = n;
     auto xbuf = [&](int s) { return ctx->xbuf + (size_t)(s & 1) * Mp * Wmax; };
     unsigned* bars = a_done + (size_t)S * Tmax;  // [S] grid barrier counters of chain(s)
+    unsigned* xready = bars + S;                  // [S] inputs of chain(s) landed (s >= 1)
+    auto wkbuf = [&](int s) { return ctx->wk + (size_t)(s & 1) * 2 * Wmax * Wmax; };
+    // launch j (j = -1: X_0 only) writes the inputs of chain(j + 2): the leading rest units
+    // (w_{j+2} (w_{j+2} + 1) slabs, none for j = -1) and the tall units of its rows
+    auto xtarget = [&](int s) {
+      const int ws = steps[s].second;
+      return (unsigned)((s >= 2 ? ws * (ws + 1) : 0) + 2 * ws * steps[s - 1].second);
+    };
     // chain(s): factor block s on the side stream's CUs (one launch, see chain_kernel)
     auto chain = [&](int s) {
       ChainArgs c{};
@@ -1703,8 +1791,10 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       c.lda = lda;
       c.Kc = steps[s].first * NB;
       c.w = steps[s].second;
-      c.Wk = ctx->wk;
+      c.Wk = wkbuf(s);
       if (s > 0) {
+        c.xready = xready + s;
+        c.xtarget = xtarget(s);
         c.Xp = xbuf(s - 1);
         c.ldx = (int64_t)steps[s - 1].second * NB;
         c.kd = steps[s - 1].second * NB;
@@ -1753,13 +1843,20 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.tr0 = K0 + (int64_t)w * NB;
       g.tk0 = K0;
       g.tw = w;
-      g.Bd = ctx->wk + (int64_t)w * NB * w * NB;
+      g.Bd = wkbuf(s) + (int64_t)w * NB * w * NB;
       g.X = xbuf(s);
       g.n = n;
       g.zvec = ctx->zvec;
       g.chain_done = chain_done + s;
       g.status = ctx->status;
+      if (s + 1 < S) {  // chain(s + 1) waits for this launch's part of its inputs
+        g.xready = xready + s + 1;
+        g.lead = steps[s + 1].second;
+        g.lead_slabs = 2 * steps[s + 1].second;
+      }
     };
+    // side: chain(0) after the gram; every later chain(s) follows chain(s - 1) in stream order
+    // and waits on the device for its inputs (xready[s]) from the main launch in flight
     hipEventRecord(ev[0], main);
     hipStreamWaitEvent(side, ev[0], 0);
     chain(0);
@@ -1768,15 +1865,14 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       StepArgs g{};
       tall_args(g, 0);
       g.a_done = nullptr;
+      g.lead = 0;  // X_0 launch: no rest units; only its tall units feed chain(1)
+      if (S > 1) g.lead = steps[1].second;
       launch_step(g);
-      hipEventRecord(ev[1], main);
     }
     for (int s = 0; s + 1 < S; ++s) {
       const int64_t K1 = (steps[s].first + steps[s].second) * NB;
       const int W = steps[s].second * NB, wn = steps[s + 1].second;
       const int T = (int)((Mp - K1) / ST);
-      // side: block s + 1 once X_s is complete (the previous main launch)
-      hipStreamWaitEvent(side, ev[1 + s], 0);
       chain(s + 1);
       StepArgs g{};
       g.A = A;
@@ -1790,8 +1886,10 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.nr = (T - wn) * (T - wn + 1);  // 2 slabs per tile of the (T - wn)-tile triangle
       tall_args(g, s + 1);
       g.a_done = a_done + (size_t)s * Tmax;
+      // the rest units of the block after next feed chain(s + 2) (xready set by tall_args)
+      if (s + 2 < S) g.lead = steps[s + 2].second;
+      else g.xready = nullptr;
       launch_step(g);
-      hipEventRecord(ev[2 + s], main);
     }
     hipEventRecord(ev[S + 1], side);
     hipStreamWaitEvent(main, ev[S + 1], 0);

@@ -110,13 +110,52 @@ __global__ __launch_bounds__(256) void mfma4_rate_kernel(double* out, int iters,
   if (s == 12345.678) out[blockIdx.x] = s;
 }
 
+// Random-operand variants (which = 2: 16x16x4, 3: 4x4x4_4b): 16 pseudo-random operand
+// pairs per lane cycled through, so the matrix cores see toggling data (power-limited rate).
+__device__ __forceinline__ double hash_val(unsigned x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return ((double)x * 2.3283064365386963e-10 - 0.5) * 0.0625;
+}
+template <bool BIG>
+__global__ __launch_bounds__(256) void mfma_rand_kernel(double* out, int iters) {
+  const unsigned l = threadIdx.x + 256u * blockIdx.x;
+  double a[16], b[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    a[u] = hash_val(l * 32u + u);
+    b[u] = hash_val(l * 32u + 16u + u);
+  }
+  double4v acc4[8];
+  double acc1[8];
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    acc4[u] = (double4v){0, 0, 0, 0};
+    acc1[u] = 0;
+  }
+  for (int it = 0; it < iters; it += 2) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (BIG) acc4[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[8 * h + u], b[8 * h + u], acc4[u], 0, 0, 0);
+        else acc1[u] = __builtin_amdgcn_mfma_f64_4x4x4f64(a[8 * h + u], b[8 * h + u], acc1[u], 0, 0, 0);
+      }
+  }
+  double s = 0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) s += BIG ? acc4[u][0] + acc4[u][1] + acc4[u][2] + acc4[u][3] : acc1[u];
+  if (s == 12345.678) out[blockIdx.x] = s;
+}
+
 int probe_rates(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflops) {
   double* dv = nullptr;
   hipError_t e = hipMallocAsync((void**)&dv, nblocks * sizeof(double), ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "probe alloc");
   auto go = [&](int it) {
     if (which == 0) hipLaunchKernelGGL(valu_rate_kernel, dim3(nblocks), dim3(256), 0, ctx->stream, dv, it, 1.0);
-    else hipLaunchKernelGGL(mfma4_rate_kernel, dim3(nblocks), dim3(256), 0, ctx->stream, dv, it, 1.0);
+    else if (which == 1) hipLaunchKernelGGL(mfma4_rate_kernel, dim3(nblocks), dim3(256), 0, ctx->stream, dv, it, 1.0);
+    else if (which == 2) hipLaunchKernelGGL(mfma_rand_kernel<true>, dim3(nblocks), dim3(256), 0, ctx->stream, dv, it);
+    else hipLaunchKernelGGL(mfma_rand_kernel<false>, dim3(nblocks), dim3(256), 0, ctx->stream, dv, it);
   };
   hipEvent_t a, b;
   hipEventCreate(&a);
@@ -133,7 +172,9 @@ int probe_rates(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflops)
   hipFreeAsync(dv, ctx->stream);
   hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "probe rates");
-  const double per = which == 0 ? 256.0 * 8 * 2 : 4.0 * 8 * (4 * 4 * 4 * 4 * 2);
+  const double per = which == 0 ? 256.0 * 8 * 2
+                     : which == 2 ? 4.0 * 8 * (16 * 16 * 4 * 2)
+                                  : 4.0 * 8 * (4 * 4 * 4 * 4 * 2);
   *tflops = (double)nblocks * iters * per / (t * 1e-3) / 1e12;
   return LFM_OK;
 }

@@ -1,5 +1,6 @@
-scripts/gpu_step.sh tests 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread || exit $?
 run() { timeout -k 10 100 python scripts/chol_sweep.py "$@" > gpurun_out/tp.log 2>&1 || exit 1; python -c "import json,sys; d=json.loads(open('gpurun_out/tp.log').read().strip().splitlines()[-1]); print(sys.argv[1:], round(d['ms_median'],3), round(d['ms_min'],3), d['mll'])" "$@"; }
-for c in 48 32; do LFM_SIDE_CUS=$c run 1,$c; done
-scripts/gpu_step.sh bench 300 python bench.py --steps 10 --warmup 2 || exit $?
-grep '^{' gpurun_out/bench.log | cut -c1-330
+run 1,32
+run 1,32,6144,1073741824,8192
+run 1,32,6144,1073741824,10240
+run 1,32,6144,1073741824,12288
+run 1,32

@@ -35,3 +35,6 @@ for s in range(256):
         break
     t = {p: (row[p] - row[0]) * 0.01 for p in range(16) if row[p]}
     print(s, " ".join(f"{p}:{v:.1f}" for p, v in t.items()))
+done = [st[s][15] for s in range(256) if st[s][0]]
+per = np.diff(np.array(done, dtype=np.int64)) * 0.01
+print("period (us) between chain completions:", " ".join(f"{v:.0f}" for v in per))
