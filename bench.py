@@ -228,11 +228,13 @@ def main():
             tf = os.path.join(ROOT, "profiles", "syrk_traffic.json")
             if os.path.exists(tf):
                 try:
-                    traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+                    # PMC bytes per evaluation over this run's launches per evaluation
+                    per_eval = json.load(open(tf)).get("hbm_bytes_per_eval")
+                    traffic = per_eval / (syrk["launches"] / a.steps) if per_eval else None
                 except Exception:
                     traffic = None
             line["roofline"] = {
-                "kernel": "syrk_kernel (fp64 MFMA trailing update)",
+                "kernel": "step_kernel (fp64 MFMA trailing update + tall panel-solve GEMM)",
                 "bound": "mfma", "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
                 "launches": syrk["launches"],

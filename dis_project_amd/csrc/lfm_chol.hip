@@ -965,7 +965,7 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
     syrk_unit<true, 64, true>(g.A, g.lda, g.s0, g.px, g.kd, g.T, 0, g.wn, u, g.wn, sP);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    if (threadIdx.x == 0 && !(g.exp & 1))
+    if (threadIdx.x == 0 && g.a_done && !(g.exp & 1))
       __hip_atomic_fetch_add(&g.a_done[g.wn + (int)(u % (2 * (g.T - g.wn))) / 2], 1u,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
@@ -1785,7 +1785,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       return (unsigned)((s >= 2 ? ws * (ws + 1) : 0) + 2 * ws * steps[s - 1].second);
     };
     // chain(s): factor block s on the side stream's CUs (one launch, see chain_kernel)
-    auto chain = [&](int s) {
+    auto chain = [&](int s, bool dev_wait = true) {
       ChainArgs c{};
       c.A = A;
       c.lda = lda;
@@ -1793,8 +1793,10 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       c.w = steps[s].second;
       c.Wk = wkbuf(s);
       if (s > 0) {
-        c.xready = xready + s;
-        c.xtarget = xtarget(s);
+        if (dev_wait) {
+          c.xready = xready + s;
+          c.xtarget = xtarget(s);
+        }
         c.Xp = xbuf(s - 1);
         c.ldx = (int64_t)steps[s - 1].second * NB;
         c.kd = steps[s - 1].second * NB;
@@ -1859,6 +1861,49 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     // and waits on the device for its inputs (xready[s]) from the main launch in flight
     hipEventRecord(ev[0], main);
     hipStreamWaitEvent(side, ev[0], 0);
+    // LFM_S3_EVENTS=1: the same work ordered by stream events only (tall units in launches of
+    // their own after the factor's event, chains after the tall launch's event) — for tools
+    // that serialise dispatches (rocprofv3 --pmc), under which device-side waits between the
+    // two streams could never be met
+    const bool evmode = env_int("LFM_S3_EVENTS", 0) != 0;
+    hipEvent_t* evc = ev + 1;      // [S] chain(s) done (events mode)
+    hipEvent_t* evt = ev + 1 + S;  // [S] X_s complete (events mode)
+    if (evmode) {
+      chain(0);
+      hipEventRecord(evc[0], side);
+      for (int s = 0; s < S; ++s) {
+        if (s > 0) {
+          const int64_t K1 = (steps[s - 1].first + steps[s - 1].second) * NB;
+          const int W = steps[s - 1].second * NB, wn = steps[s].second;
+          const int T = (int)((Mp - K1) / ST);
+          StepArgs g{};  // step s - 1's trailing update only
+          g.A = A;
+          g.lda = lda;
+          g.s0 = K1;
+          g.px = Panel{xbuf(s - 1), W, K1};
+          g.kd = W;
+          g.T = T;
+          g.wn = wn;
+          g.na = 2 * wn * (T - wn);
+          g.nr = (T - wn) * (T - wn + 1);
+          g.status = ctx->status;
+          launch_step(g);
+        }
+        hipStreamWaitEvent(main, evc[s], 0);
+        StepArgs g{};  // X_s
+        tall_args(g, s);
+        g.chain_done = nullptr;
+        g.a_done = nullptr;
+        g.xready = nullptr;
+        launch_step(g);
+        hipEventRecord(evt[s], main);
+        if (s + 1 < S) {
+          hipStreamWaitEvent(side, evt[s], 0);
+          chain(s + 1, false);
+          hipEventRecord(evc[s + 1], side);
+        }
+      }
+    } else {
     chain(0);
     {
       // X_0 once the first block is factored (its units wait for chain_done[0])
@@ -1891,9 +1936,10 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       else g.xready = nullptr;
       launch_step(g);
     }
-    hipEventRecord(ev[S + 1], side);
-    hipStreamWaitEvent(main, ev[S + 1], 0);
-  } else if (ctx->sched == 2 && ctx->lookahead) {  } else if (ctx->sched == 2 && ctx->lookahead) {
+    }  // device-ordered mode
+    hipEventRecord(ev[2 * S + 1], side);
+    hipStreamWaitEvent(main, ev[2 * S + 1], 0);
+  } else if (ctx->sched == 2 && ctx->lookahead) {
     // Schedule 2: the side stream factors only each super-panel's diagonal block (a few
     // workgroups); the main stream solves the tall panel below it and applies the bulk
     // update, leaving the next super-panel's diagonal block to the side stream.

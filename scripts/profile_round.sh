@@ -13,9 +13,9 @@ R=${1:-r01}
 STEPS=${STEPS:-10}
 scripts/gpu_step.sh prof_trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace \
   -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $?
-scripts/gpu_step.sh prof_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch \
+LFM_S3_EVENTS=1 scripts/gpu_step.sh prof_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch \
   -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile || exit $?
-scripts/gpu_step.sh prof_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write \
+LFM_S3_EVENTS=1 scripts/gpu_step.sh prof_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write \
   -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile || exit $?
 python scripts/summarize_profile.py $R > gpurun_out/summary_pre.log 2>&1 || exit $?
 scripts/gpu_step.sh bench 600 python bench.py --steps $STEPS --warmup 2 || exit $?

@@ -65,14 +65,20 @@ def main():
                   "fetch_bytes_per_launch_x2": 2 * f, "write_bytes_per_launch": w,
                   "hbm_bytes_per_launch": 2 * f + w}
     json.dump(out, open(os.path.join(PROF, f"{rnd}_hbm.json"), "w"), indent=1)
-    # every SYRK instantiation (128-row bulk tiles, 64-row look-ahead bands) together: the
-    # same population bench.py's roofline averages over
-    syrk = [(k, v) for k, v in out.items() if k.startswith("syrk_kernel")]
+    # the trailing-update kernels together (schedule 3: step_kernel = SYRK + tall-solve GEMM;
+    # schedule 1: every syrk_kernel instantiation): the population bench.py's roofline averages
+    syrk = [(k, v) for k, v in out.items() if k.startswith("step_kernel")] or \
+        [(k, v) for k, v in out.items() if k.startswith("syrk_kernel")]
     if syrk:
         launches = sum(v["launches"] for _, v in syrk)
         total = sum(v["hbm_bytes_per_launch"] * v["launches"] for _, v in syrk)
+        # evaluations in the PMC run = gram launches (one per MLL evaluation); the PMC passes run
+        # schedule 3 event-ordered (LFM_S3_EVENTS=1), which splits the launches differently from
+        # the bench, so bench.py converts the per-evaluation bytes to its own launch count
+        evals = max(1, out.get("gram_grid_aligned_kernel<double>", {}).get("launches", 1))
         json.dump({"round": rnd, "source": f"profiles/{rnd}_hbm.json (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                    "kernels": [k for k, _ in syrk],
+                   "hbm_bytes_per_eval": total / evals, "evals": evals,
                    "hbm_bytes_per_launch": total / max(1, launches), "launches": launches},
                   open(os.path.join(PROF, "syrk_traffic.json"), "w"), indent=1)
     lines += ["", "HBM per launch (PMC, separate passes; read side x2 per MI355X_MICROARCH.md §HBM):",
