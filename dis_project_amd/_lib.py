@@ -121,6 +121,7 @@ SIGNATURES = [
     ("lfm_profile_reset", c_int, [_c_ctx]),
     ("lfm_profile_read", c_int, [_c_ctx, POINTER(LfmKstat), c_int, POINTER(c_int)]),
     ("lfm_debug_stamps", c_int, [_c_ctx, c_int, POINTER(ctypes.c_ulonglong), c_int]),
+    ("lfm_probe_rsq", c_int, [_c_ctx, c_void_p, c_int64, c_void_p]),
     ("lfm_farm_unique_id", c_int, [_c_ctx, POINTER(ctypes.c_ubyte)]),
     ("lfm_farm_init", c_int, [_c_ctx, POINTER(ctypes.c_ubyte), c_int, c_int]),
     ("lfm_farm_allgather_f64", c_int, [_c_ctx, _dptr, c_int64, _dptr]),

@@ -971,6 +971,12 @@ int lfm_profile_read(lfm_ctx* ctx, lfm_kstat* stats, int max, int* count) {
   return LFM_OK;
 }
 
+int lfm_probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y) {
+  if (!ctx || !x || !y || n < 1) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_rsq(ctx, x, n, y);
+}
+
 // Diagnostics: enable = 1 turns on s_memrealtime (100 MHz) stamps of the schedule-3 chain
 // kernel's phases (16 per super-panel step, 256 steps); enable = 0 copies them out (max
 // values) and turns them off.

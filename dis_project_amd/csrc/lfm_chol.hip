@@ -1594,6 +1594,26 @@ int probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us) {
 
 // Diagnostic: average duration (us) of one full-lower-triangle SYRK launch over a T x T grid
 // of 128-tiles with update depth kd; cio bit 0 = C tile I/O, bit 2 = 64-row slabs (with C I/O).
+// Diagnostic: the pivot reciprocal square root of the diagonal factor (v_rsq_f64 + one
+// Newton step) over host values x[n] -> y[n] (tests bound its relative error).
+__global__ void rsq_probe_kernel(const double* x, double* y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] = rsqrt_1nr(x[i]);
+}
+
+int probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y) {
+  double* d = nullptr;
+  hipError_t e = hipMalloc((void**)&d, 2 * n * sizeof(double));
+  if (e != hipSuccess) return hip_fail(ctx, e, "probe rsq");
+  hipMemcpyAsync(d, x, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipLaunchKernelGGL(rsq_probe_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
+                     d, d + n, n);
+  hipMemcpyAsync(y, d + n, n * 8, hipMemcpyDeviceToHost, ctx->stream);
+  e = hipStreamSynchronize(ctx->stream);
+  hipFree(d);
+  return hip_fail(ctx, e, "probe rsq");
+}
+
 // Pseudo-random doubles in [-1/32, 1/32) (probe data: MFMA power, hence clocks, depends on it).
 __global__ void fill_hash_kernel(double* a, int64_t cnt) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) {

@@ -126,6 +126,7 @@ int prof_flush(lfm_ctx* ctx);
 
 GridLayout detect_grid(const double* x, int64_t n, int64_t G);
 int chain_coresident(lfm_ctx* ctx, hipStream_t st, int G, bool* good);
+int probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y);
 int gene_clamp_host(double g, int64_t G);
 
 // device-side gene index semantics: trunc toward zero, negative wraps, clamp

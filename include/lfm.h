@@ -203,6 +203,8 @@ int lfm_probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us);
 /* Diagonal-block factor kernel with phase mask (bit0 register factor, bit1 panel,
  * bit2 trailing update, bit3 HBM load/store; 15 = product kernel): average us/launch. */
 int lfm_probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us);
+/* The diagonal factor's pivot reciprocal square root (v_rsq_f64 + one Newton step) on x[n]. */
+int lfm_probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y);
 /* Layout probe: D = A(16x4) * B(4x16) on one wave; A,B,D row-major host arrays. */
 int lfm_probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d);
 
