@@ -721,7 +721,8 @@ struct Panel {
 template <bool CIO, int TR, bool COH = false, int KS = KB>
 __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, int64_t s, Panel P,
                                           int kd, int T, int tj_lo, int tj_hi, int64_t b, int ti0,
-                                          double (*__restrict__ sP)[KS + 1], int coh_lim = 0) {
+                                          double (*__restrict__ sP)[KS + 1], int coh_lim = 0,
+                                          int64_t pad_after = INT64_MAX) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
@@ -751,6 +752,8 @@ __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, i
   const int64_t i0 = s + (int64_t)ti * TR, j0 = s + (int64_t)tj * ST;
   const bool diag = i0 < j0 + ST;  // the tile reaches the diagonal: keep col <= row only
   const bool in_lead = (i0 - s) / ST < coh_lim && (j0 - s) / ST < coh_lim;
+  // rows past pad_after are identity padding of the augmented matrix: nothing reads their update
+  if (i0 > pad_after && !in_lead) return false;
   const bool coh = COH || in_lead;
   double* Cb = A + (i0 + wr + lk) * lda + j0 + wc + li;  // C[wr + lk][wc + li]
   const int ld4 = (int)(4 * lda);  // row-group stride (elements); 60 * ld4 < 2^31 for lda < 2^23
@@ -962,7 +965,7 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
   if (role == 1) {
     // device-coherent stores + a counter bump once they have completed: the tall units read
     // these rows with device-coherent loads (no L2 writeback / invalidate on either side)
-    syrk_unit<true, 64, true>(g.A, g.lda, g.s0, g.px, g.kd, g.T, 0, g.wn, u, g.wn, sP);
+    syrk_unit<true, 64, true>(g.A, g.lda, g.s0, g.px, g.kd, g.T, 0, g.wn, u, g.wn, sP, 0, g.n);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (threadIdx.x == 0 && g.a_done && !(g.exp & 1))
@@ -972,7 +975,7 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
   }
   if (role == 2) {
     const bool lead = syrk_unit<true, 64>(g.A, g.lda, g.s0, g.px, g.kd, g.T, g.wn, g.T, u, 0, sP,
-                                          g.xready ? g.wn + g.lead : 0);
+                                          g.xready ? g.wn + g.lead : 0, g.n);
     if (lead) bump_after_stores(g.xready);
     return;
   }
@@ -981,6 +984,8 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
   const int64_t nrb = g.nt / g.tw;
   const int cb = g.tw - 1 - (int)(u / nrb);
   const int64_t i0 = g.tr0 + (u % nrb) * 64;
+  const bool lead = g.xready && (i0 - g.tr0) / 64 < g.lead_slabs;
+  if (i0 > g.n && !lead) return;  // identity padding rows: their X is never read
   {
     __shared__ int ok;
     // relaxed polling and device-coherent operand loads below instead of an acquire fence:
@@ -1009,7 +1014,6 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
   gemm_accumulate<64, true, true>(g.A + i0 * g.lda + g.tk0, g.lda, g.Bd + cb * NB, W,
                                   NB * (cb + 1), acc, sP);
   double* Xb = g.X + (i0 - g.tr0 + wr + lk) * W + cb * NB + wc + li;
-  const bool lead = g.xready && (i0 - g.tr0) / 64 < g.lead_slabs;
 #pragma unroll
   for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
@@ -1844,6 +1848,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     const char* tp = std::getenv("LFM_TALL_POS");
     const double tall_pos = tp ? std::atof(tp) : 1.0;  // fraction of the rest ahead of the tall units
     auto launch_step = [&](StepArgs& g) {
+      g.n = n;  // padding rows past n are skipped
       g.nr1 = (int)std::min<double>(g.nr, std::max(0.0, tall_pos * g.nr));
       g.exp = env_int("LFM_STEP_EXP", 0);
       const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 +
