@@ -533,7 +533,7 @@ void lfm_ctx_destroy(lfm_ctx* ctx) {
                   (void*)ctx->xin, (void*)ctx->linvT, (void*)ctx->parts, (void*)ctx->status,
                   (void*)ctx->result, (void*)ctx->farm_buf, (void*)ctx->gacc,
                   (void*)ctx->psync, (void*)ctx->wk, (void*)ctx->xbuf, (void*)ctx->zvec,
-                  (void*)ctx->flags, (void*)ctx->linv_full, (void*)ctx->dbg_stamps})
+                  (void*)ctx->flags, (void*)ctx->linv_full, (void*)ctx->dbg_stamps, (void*)ctx->xd})
     if (p) hipFree(p);
   if (ctx->hpin) hipHostFree(ctx->hpin);
   for (auto& p : ctx->pending) {

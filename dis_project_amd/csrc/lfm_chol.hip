@@ -929,11 +929,11 @@ struct StepArgs {
   unsigned* a_done;  // [T] per tile row of step s (NULL: no wait)
   const unsigned* chain_done;  // NULL: no wait
   int* status;
-  // inputs of chain(s + 2), which starts while this launch runs: the rest units of the block
-  // (lead x lead leading tiles of the rest triangle) and the tall units of its rows (row
-  // slabs < lead_slabs) write through to memory and bump *xready when done
+  // inputs of chain(s + 2), which starts while this launch runs: the rest units of its block
+  // (lead x lead leading tiles of the rest triangle) and the ahead units of its rows (tile
+  // rows < wn + lead) write through to memory and bump *xready when done
   unsigned* xready;  // NULL: no chain waits on this launch
-  int lead, lead_slabs;
+  int lead;
 };
 
 __device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
@@ -968,9 +968,11 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
     syrk_unit<true, 64, true>(g.A, g.lda, g.s0, g.px, g.kd, g.T, 0, g.wn, u, g.wn, sP, 0, g.n);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
+    const int trow = g.wn + (int)(u % (2 * (g.T - g.wn))) / 2;  // 128-tile row of the unit
     if (threadIdx.x == 0 && g.a_done && !(g.exp & 1))
-      __hip_atomic_fetch_add(&g.a_done[g.wn + (int)(u % (2 * (g.T - g.wn))) / 2], 1u,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&g.a_done[trow], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0 && g.xready && trow < g.wn + g.lead)
+      __hip_atomic_fetch_add(g.xready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return;
   }
   if (role == 2) {
@@ -984,8 +986,7 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
   const int64_t nrb = g.nt / g.tw;
   const int cb = g.tw - 1 - (int)(u / nrb);
   const int64_t i0 = g.tr0 + (u % nrb) * 64;
-  const bool lead = g.xready && (i0 - g.tr0) / 64 < g.lead_slabs;
-  if (i0 > g.n && !lead) return;  // identity padding rows: their X is never read
+  if (i0 > g.n) return;  // identity padding rows: their X is never read
   {
     __shared__ int ok;
     // relaxed polling and device-coherent operand loads below instead of an acquire fence:
@@ -1018,14 +1019,9 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
   for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) {
-      if (lead)
-        __hip_atomic_store(&Xb[(ir * 4) * W + jr * 16], acc[ir][jr], __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      else
-        Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
+      Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
       if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + cb * NB + wc + jr * 16 + li] = acc[ir][jr];
     }
-  if (lead) bump_after_stores(g.xready);
 }
 
 // Row n of the chain workspace (n inside the super-panel's diagonal block) into zvec.
@@ -1139,9 +1135,7 @@ struct ChainArgs {
   int64_t Kc;         // first row / column of the super-panel
   int w;              // width in 128-column blocks
   double* Wk;         // 2W x W, ld W
-  const double* Xp;   // X_{s-1}: row Kc first, ld ldx, depth kd (kd = 0: no pending update)
-  int64_t ldx;
-  int kd;
+  int kd;             // W_{s-1}: depth of the pending update (0: none)
   int64_t n;
   double* dinv;
   double* linv;       // 128 x 128: transposed inverse of the current diagonal block (w > 1)
@@ -1152,7 +1146,12 @@ struct ChainArgs {
   unsigned* done;     // chain_done[s]
   unsigned long long* stamps;  // diagnostics (NULL: off): s_memrealtime per phase, [16]
   const unsigned* xready;  // NULL: inputs ready at launch; else wait for *xready >= xtarget and
-  unsigned xtarget;        // read A[D] and X_{s-1} with device-coherent loads
+  unsigned xtarget;        // read A[D] and the panel rows with device-coherent loads
+  // PX (kd > 0): the block's rows of X_{s-1} = A[D rows, K0p .. K0p + kd) Bd_{s-1} are formed
+  // here (into xd, ld kd) instead of waiting for the main stream's tall units
+  int64_t K0p;             // first column of super-panel s - 1
+  const double* Bdp;       // Bd_{s-1}: kd x kd, ld kd
+  double* xd;              // W x kd scratch
 };
 
 // dynamic LDS of chain_kernel: the factor block and its inverse (packed 16x16 blocks)
@@ -1202,12 +1201,39 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     __shared__ int okx;
     if (tid == 0) okx = spin_until<false>(g.xready, g.xtarget);
     __syncthreads();
+    // one agent-scope acquire (L2 invalidate) so the inputs below come through plain, cached
+    // loads: the chain starts once per super-panel, the bulk units lose little
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (!okx) {
       if (tid == 0) atomicMin(g.status, PANEL_TIMEOUT);
       return;
     }
   }
   stamp(14);
+  if (g.kd > 0) {
+    // PX: X_{s-1} rows of the block, 64-row x 128-column units (K = 128 (cb + 1), Bd upper)
+    const int wp = g.kd / NB;
+    const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64, li = lane & 15, lk = lane >> 4;
+    for (int u = wg; u < 2 * g.w * wp; u += G) {
+      const int cb = u % wp, rb = u / wp;
+      const int64_t i0 = g.Kc + 64 * rb;
+      double acc[8][4];
+#pragma unroll
+      for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+        for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = 0.0;
+      gemm_accumulate<64, true, false, CKS>(g.A + i0 * g.lda + g.K0p, g.lda, g.Bdp + cb * NB, g.kd,
+                                            NB * (cb + 1), acc, sP);
+      double* Xb = g.xd + (64 * rb + wr + lk) * g.kd + cb * NB + wc + li;
+#pragma unroll
+      for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+        for (int jr = 0; jr < 4; ++jr) Xb[(ir * 4) * g.kd + jr * 16] = acc[ir][jr];
+      __syncthreads();
+    }
+    if (!grid_sync(g.bar, G * ++nbar, g.status)) return;
+  }
+  stamp(13);
   // P0: pending update of the block into the workspace (lower 128-tiles, 2 slabs each)
   {
     const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64, li = lane & 15, lk = lane >> 4;
@@ -1224,17 +1250,10 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
       for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
         for (int jr = 0; jr < 4; ++jr)
-          acc[ir][jr] = -(g.xready ? __hip_atomic_load(&Cs[(ir * 4) * g.lda + jr * 16],
-                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                   : Cs[(ir * 4) * g.lda + jr * 16]);
-      if (g.kd > 0) {
-        if (g.xready)
-          gemm_accumulate<64, false, true, CKS>(g.Xp + (i0 - g.Kc) * g.ldx, g.ldx,
-                                                g.Xp + (j0 - g.Kc) * g.ldx, g.ldx, g.kd, acc, sP);
-        else
-          gemm_accumulate<64, false, false, CKS>(g.Xp + (i0 - g.Kc) * g.ldx, g.ldx,
-                                                 g.Xp + (j0 - g.Kc) * g.ldx, g.ldx, g.kd, acc, sP);
-      }
+          acc[ir][jr] = -Cs[(ir * 4) * g.lda + jr * 16];
+      if (g.kd > 0)
+        gemm_accumulate<64, false, false, CKS>(g.xd + (i0 - g.Kc) * g.kd, g.kd,
+                                               g.xd + (j0 - g.Kc) * g.kd, g.kd, g.kd, acc, sP);
       double* Cd = Aw + (i0 + wr + lk) * W + j0 + wc + li;
 #pragma unroll
       for (int ir = 0; ir < 8; ++ir)
@@ -1791,6 +1810,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     if (!r) r = ensure(ctx, (void**)&ctx->zvec, &ctx->zvec_bytes, (size_t)Mp * sizeof(double));
     if (!r)
       r = ensure(ctx, (void**)&ctx->linv_full, &ctx->linv_full_bytes, (size_t)NB * NB * sizeof(double));
+    if (!r) r = ensure(ctx, (void**)&ctx->xd, &ctx->xd_bytes, (size_t)Wmax * Wmax * sizeof(double));
     const size_t nflags = (size_t)S * (3 + Tmax);
     if (!r) r = ensure(ctx, (void**)&ctx->flags, &ctx->flags_bytes, nflags * sizeof(unsigned));
     if (r) return r;
@@ -1802,11 +1822,12 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     unsigned* bars = a_done + (size_t)S * Tmax;  // [S] grid barrier counters of chain(s)
     unsigned* xready = bars + S;                  // [S] inputs of chain(s) landed (s >= 1)
     auto wkbuf = [&](int s) { return ctx->wk + (size_t)(s & 1) * 2 * Wmax * Wmax; };
-    // launch j (j = -1: X_0 only) writes the inputs of chain(j + 2): the leading rest units
-    // (w_{j+2} (w_{j+2} + 1) slabs, none for j = -1) and the tall units of its rows
+    // launch j = s - 2 (step j's update) writes the inputs of chain(s), s >= 2: the block's
+    // tiles (leading rest units, w_s (w_s + 1) slabs) and its rows of the columns of super-
+    // panel s - 1 (leading ahead units, 2 w_s w_{s-1} slabs); chain(s) forms X_{s-1} of its rows
     auto xtarget = [&](int s) {
       const int ws = steps[s].second;
-      return (unsigned)((s >= 2 ? ws * (ws + 1) : 0) + 2 * ws * steps[s - 1].second);
+      return (unsigned)(ws * (ws + 1) + 2 * ws * steps[s - 1].second);
     };
     // chain(s): factor block s on the side stream's CUs (one launch, see chain_kernel)
     auto chain = [&](int s, bool dev_wait = true) {
@@ -1817,13 +1838,14 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       c.w = steps[s].second;
       c.Wk = wkbuf(s);
       if (s > 0) {
-        if (dev_wait) {
+        if (dev_wait && s >= 2) {
           c.xready = xready + s;
           c.xtarget = xtarget(s);
         }
-        c.Xp = xbuf(s - 1);
-        c.ldx = (int64_t)steps[s - 1].second * NB;
         c.kd = steps[s - 1].second * NB;
+        c.K0p = steps[s - 1].first * NB;
+        c.Bdp = wkbuf(s - 1) + (int64_t)c.kd * c.kd;
+        c.xd = ctx->xd;
       }
       c.n = n;
       c.dinv = ctx->linvT;
@@ -1876,11 +1898,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.zvec = ctx->zvec;
       g.chain_done = chain_done + s;
       g.status = ctx->status;
-      if (s + 1 < S) {  // chain(s + 1) waits for this launch's part of its inputs
-        g.xready = xready + s + 1;
-        g.lead = steps[s + 1].second;
-        g.lead_slabs = 2 * steps[s + 1].second;
-      }
     };
     // side: chain(0) after the gram; every later chain(s) follows chain(s - 1) in stream order
     // and waits on the device for its inputs (xready[s]) from the main launch in flight
@@ -1935,8 +1952,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       StepArgs g{};
       tall_args(g, 0);
       g.a_done = nullptr;
-      g.lead = 0;  // X_0 launch: no rest units; only its tall units feed chain(1)
-      if (S > 1) g.lead = steps[1].second;
       launch_step(g);
     }
     for (int s = 0; s + 1 < S; ++s) {
@@ -1956,9 +1971,11 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.nr = (T - wn) * (T - wn + 1);  // 2 slabs per tile of the (T - wn)-tile triangle
       tall_args(g, s + 1);
       g.a_done = a_done + (size_t)s * Tmax;
-      // the rest units of the block after next feed chain(s + 2) (xready set by tall_args)
-      if (s + 2 < S) g.lead = steps[s + 2].second;
-      else g.xready = nullptr;
+      // the block after next: its tiles (rest) and rows (ahead) feed chain(s + 2)
+      if (s + 2 < S) {
+        g.xready = xready + s + 2;
+        g.lead = steps[s + 2].second;
+      }
       launch_step(g);
     }
     }  // device-ordered mode

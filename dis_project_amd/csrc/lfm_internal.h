@@ -79,6 +79,7 @@ struct lfm_ctx {
   double* xbuf = nullptr; size_t xbuf_bytes = 0; // schedule 3: solved panel X = A21 L11^{-T}
   double* zvec = nullptr; size_t zvec_bytes = 0; // schedule 3: z = L^{-1} r
   double* linv_full = nullptr; size_t linv_full_bytes = 0; // schedule 3: 128x128 block inverse
+  double* xd = nullptr; size_t xd_bytes = 0;     // schedule 3: the chain's rows of X_{s-1}
   unsigned* flags = nullptr; size_t flags_bytes = 0; // schedule 3: per-step device flags
   unsigned* psync = nullptr;                     // fused panel: [0] factor epoch, [1] slab count
   unsigned panel_epoch = 0;                      // fused panel launches so far
