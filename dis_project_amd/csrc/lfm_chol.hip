@@ -100,6 +100,30 @@ __device__ __forceinline__ double row_bcast(double v, int src) {
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // ---------------------------------------------------------------- potrf
+// Two doubles; COH: device-coherent loads (agent-scope relaxed atomics bypass the XCD's L2,
+// which may hold stale lines of data another XCD wrote in the same launch).
+template <bool COH>
+__device__ __forceinline__ double2 ld2(const double* p) {
+  if (COH) {
+    double2 v;
+    v.x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v.y = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v;
+  }
+  return *reinterpret_cast<const double2*>(p);
+}
+// One double, write-through (COH) or plain.
+template <bool COH>
+__device__ __forceinline__ void st1(double* p, double v) {
+  if (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+template <bool COH>
+__device__ __forceinline__ double ld1(const double* p) {
+  if (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return *p;
+}
+
 // 1/sqrt(x) to ~1 ulp: v_rsq_f64 estimate + two Newton steps (a pivot and its inverse
 // come from one estimate instead of a correctly rounded sqrt followed by a divide).
 // One Newton step: the pivot's relative error stays far below the 1e-9 MLL tolerance (a
@@ -124,7 +148,8 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 // After the loop the eight 16x16 diagonal inverses (dinv, for trsm_kernel) are built by
 // the four waves, and logdet / the first failing pivot are reduced.
 // PH (diagnostics only, lfm_probe_potrf): bit 0 = phase 1, bit 1 = phase 2, bit 2 = phase 3,
-// bit 3 = global load / store of the block. The product path always runs PH = 15.
+// bit 3 = global load / store of the block. The product path always runs PH = 15, with bit 4
+// (device-coherent block loads) in the chain's light mode.
 // only the 36 lower 16x16 blocks of the 128x128 block, each 16 x 17 (padded) doubles:
 // 78 KB, so the kernel fits on a CU beside one SYRK workgroup (look-ahead overlap)
 constexpr int MB_DOUBLES = (NB / IB) * (NB / IB + 1) / 2 * IB * (IB + 1);
@@ -135,7 +160,13 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
                                             double* __restrict__ dinv,
                                             double* __restrict__ parts, int k,
                                             int* __restrict__ status,
-                                            double* __restrict__ Li = nullptr) {
+                                            double* __restrict__ Li = nullptr,
+                                            unsigned long long* __restrict__ pst = nullptr) {
+  // pst (diagnostics, NULL: off): s_memrealtime after the load (pst[0]) and after each panel
+  // iteration ib < 7 (pst[1 + ib])
+  auto pstamp = [&](int p) {
+    if (pst && threadIdx.x == 0) pst[p] = __builtin_amdgcn_s_memrealtime();
+  };
   __shared__ double pvs[NB];  // unscaled pivots
   __shared__ double ipv[NB];  // 1 / L_cc
   __shared__ double red[4];
@@ -154,7 +185,7 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
     for (int u = 0; u < 16; ++u) {
       const int idx = tid + 256 * (u + 16 * hb), r = idx >> 6, c2 = idx & 63;
       if ((2 * c2) >> 4 <= r >> 4)
-        v[u] = (PH & 8) ? *reinterpret_cast<const double2*>(&A[(kb + r) * lda + kb + 2 * c2])
+        v[u] = (PH & 8) ? ld2<(PH & 16) != 0>(&A[(kb + r) * lda + kb + 2 * c2])
                         : double2{(r == 2 * c2) ? 2.0 : 0.0, (r == 2 * c2 + 1) ? 2.0 : 0.0};
     }
 #pragma unroll
@@ -252,6 +283,7 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
   };
   if ((PH & 1) && w == 0) leaf(0);
   __syncthreads();
+  pstamp(0);
 #pragma unroll 1
   for (int ib = 0; ib < NB / IB; ++ib) {
     const int c0 = ib * IB;
@@ -306,6 +338,7 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
         for (int J = w - 2; J < ib - 1; J += 2) linv_block(ib - 1, J);
     }
     __syncthreads();
+    pstamp(1 + ib);
   }
   if (Li) {
     // remaining: Dinv_7 with block row 6, then block row 7
@@ -378,6 +411,7 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
 
 // out[k][j] = Linv[j][k] (the transposed inverse of the factored block: upper triangular,
 // zeros below the diagonal), ld ldo, from Li (packed 16x16 blocks, built by potrf_block).
+template <bool COH = false>
 __device__ __forceinline__ void store_inverse_t(const double* __restrict__ Li,
                                                 double* __restrict__ out, int64_t ldo) {
 #define LI(r, q) Li[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * (IB * (IB + 1)) + \
@@ -388,7 +422,12 @@ __device__ __forceinline__ void store_inverse_t(const double* __restrict__ Li,
     double2 v;
     v.x = j >= k ? LI(j, k) : 0.0;
     v.y = j + 1 >= k ? LI(j + 1, k) : 0.0;
-    *reinterpret_cast<double2*>(&out[k * ldo + j]) = v;
+    if (COH) {
+      st1<true>(&out[k * ldo + j], v.x);
+      st1<true>(&out[k * ldo + j + 1], v.y);
+    } else {
+      *reinterpret_cast<double2*>(&out[k * ldo + j]) = v;
+    }
   }
 #undef LI
 }
@@ -608,18 +647,6 @@ __global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, in
 // acc (negated once at load / store instead of per fragment). sP: LDS staging, (TR + ST) rows
 // of KB + 1 doubles: rows [0, TR) panel i, rows [TR, TR + ST) panel j (j-major).
 // Every thread of the (256-thread) workgroup must call it.
-// Two doubles; COH: device-coherent loads (agent-scope relaxed atomics bypass the XCD's L2,
-// which may hold stale lines of data another XCD wrote in the same launch).
-template <bool COH>
-__device__ __forceinline__ double2 ld2(const double* p) {
-  if (COH) {
-    double2 v;
-    v.x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    v.y = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return v;
-  }
-  return *reinterpret_cast<const double2*>(p);
-}
 
 // KS: depth of one LDS stage (16 in the bulk kernels; 64 where one workgroup per CU has no
 // neighbours to hide the global-load latency behind — the side stream's chain kernel).
@@ -1152,6 +1179,7 @@ struct ChainArgs {
   int64_t K0p;             // first column of super-panel s - 1
   const double* Bdp;       // Bd_{s-1}: kd x kd, ld kd
   double* xd;              // W x kd scratch
+  int small;               // bit 0: PX, bit 1: P0 in 32 x 32 tiles (gemm32)
 };
 
 // dynamic LDS of chain_kernel: the factor block and its inverse (packed 16x16 blocks)
@@ -1183,8 +1211,122 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, int* s
   return ok;
 }
 
+// Light grid barrier: no cache maintenance. Valid when every value another workgroup wrote
+// before the barrier was stored write-through (agent-scope relaxed stores) and is read after it
+// with device-coherent loads: the s_waitcnt orders this thread's stores before the arrival.
+__device__ __forceinline__ bool grid_sync_light(unsigned* bar, unsigned target, int* status) {
+  __shared__ int ok;
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned it = 0;
+    bool good = true;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (++it >= (1u << 24) ||
+          __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == PANEL_TIMEOUT) {
+        good = false;
+        atomicMin(status, PANEL_TIMEOUT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    ok = good;
+  }
+  __syncthreads();
+  return ok;
+}
+
+
 constexpr int CKS = 64;  // chain kernel GEMM stage depth
 static_assert(2 * MB_DOUBLES >= (64 + ST) * (CKS + 1), "chain LDS union");
+
+// Small-tile GEMM for the chain's latency-bound phases: one 32 x 32 output tile per
+// workgroup, so a 128-row block spreads over 16 workgroups instead of two 64 x 128 units
+// (one CU's fp64 MFMA rate is 1/256 of the chip's: a 64 x 128 x 128 unit alone is ~7 us).
+//   v[q] = sum_{k < kd} P[r][k] Q[k][c],  element (r, c) = ((tid + 256 q) >> 5, & 31)
+// P: row-major, k contiguous (row r at pi + r ldi). Q: BT, K-major (element (k, c) at
+// pj[k ldj + c]); !BT, j-major (element (k, c) at pj[c ldj + k]). kd: multiple of 128.
+// Stages of 128 k are loaded with 16 coalesced 16-B loads per thread (the next stage is
+// prefetched into registers while the current one is multiplied); the four waves each take
+// 32 k of a stage and their partial tiles are summed through LDS at the end.
+// LDS: smem[0, 2 * 32 * G32K) (operands) and then [0, 4 * 32 * 33) (partials, aliased).
+constexpr int G32K = 129;  // LDS row stride of a 128-deep operand row
+static_assert(2 * MB_DOUBLES >= 2 * 32 * G32K && 2 * MB_DOUBLES >= 4 * 32 * 33, "gemm32 LDS");
+template <bool BT, bool COH = false>
+__device__ __forceinline__ void gemm32(const double* __restrict__ pi, int64_t ldi,
+                                       const double* __restrict__ pj, int64_t ldj, int kd,
+                                       double (&v)[4], double* __restrict__ smem) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 15, lk = lane >> 4, l3 = lane & 3;
+  double* sA = smem;             // [32][G32K]: P rows
+  double* sB = smem + 32 * G32K;  // [32][G32K]: Q columns (j-major)
+  double acc[8][2];
+#pragma unroll
+  for (int ir = 0; ir < 8; ++ir) acc[ir][0] = acc[ir][1] = 0.0;
+  double2 pre[16];
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = tid + 256 * u;
+      pre[u] = ld2<COH>(pi + (idx >> 6) * ldi + k0 + 2 * (idx & 63));
+      pre[8 + u] = BT ? ld2<COH>(pj + (int64_t)(k0 + (idx >> 4)) * ldj + 2 * (idx & 15))
+                      : ld2<COH>(pj + (idx >> 6) * ldj + k0 + 2 * (idx & 63));
+    }
+  };
+  if (kd > 0) gload(0);
+  for (int k0 = 0; k0 < kd; k0 += 128) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int idx = tid + 256 * u;
+      double* d = sA + (idx >> 6) * G32K + 2 * (idx & 63);
+      d[0] = pre[u].x;
+      d[1] = pre[u].y;
+      if (BT) {
+        const int kr = idx >> 4, c = 2 * (idx & 15);
+        sB[c * G32K + kr] = pre[8 + u].x;
+        sB[(c + 1) * G32K + kr] = pre[8 + u].y;
+      } else {
+        double* e = sB + (idx >> 6) * G32K + 2 * (idx & 63);
+        e[0] = pre[8 + u].x;
+        e[1] = pre[8 + u].y;
+      }
+    }
+    __syncthreads();
+    if (k0 + 128 < kd) gload(k0 + 128);
+#pragma unroll
+    for (int kk = 32 * w; kk < 32 * w + 32; kk += 4) {
+      const double b0 = sB[li * G32K + kk + lk], b1 = sB[(16 + li) * G32K + kk + lk];
+      double a[8];
+#pragma unroll
+      for (int ir = 0; ir < 8; ++ir) a[ir] = sA[(ir * 4 + l3) * G32K + kk + lk];
+#pragma unroll
+      for (int ir = 0; ir < 8; ++ir) {
+        acc[ir][0] = mfma4(a[ir], b0, acc[ir][0]);
+        acc[ir][1] = mfma4(a[ir], b1, acc[ir][1]);
+      }
+    }
+  }
+  __syncthreads();  // operand reads done: the partials alias them
+  double* red = smem;  // [4][32][33]
+#pragma unroll
+  for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+    for (int jr = 0; jr < 2; ++jr) red[(w * 32 + ir * 4 + lk) * 33 + jr * 16 + li] = acc[ir][jr];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int e = tid + 256 * q, r = e >> 5, c = e & 31;
+    v[q] = red[r * 33 + c] + red[(32 + r) * 33 + c] + red[(64 + r) * 33 + c] +
+           red[(96 + r) * 33 + c];
+  }
+  __syncthreads();  // partials read: smem is free for the next call
+}
+// LIGHT (w = 1 with both small-tile phases): every value one workgroup hands to another is
+// stored write-through and loaded device-coherently, so the barriers, the input wait and the
+// completion flag need no cache maintenance (an agent-scope fence costs ~1.7-3.5 us).
+template <bool LIGHT>
 __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double (*sP)[CKS + 1] = reinterpret_cast<double (*)[CKS + 1]>(smem);
@@ -1201,16 +1343,32 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     __shared__ int okx;
     if (tid == 0) okx = spin_until<false>(g.xready, g.xtarget);
     __syncthreads();
-    // one agent-scope acquire (L2 invalidate) so the inputs below come through plain, cached
-    // loads: the chain starts once per super-panel, the bulk units lose little
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // one agent-scope acquire so the inputs below come through plain, cached loads (LIGHT:
+    // device-coherent loads instead)
+    if (!LIGHT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (!okx) {
       if (tid == 0) atomicMin(g.status, PANEL_TIMEOUT);
       return;
     }
   }
   stamp(14);
-  if (g.kd > 0) {
+  if (g.kd > 0 && (g.small & 1)) {
+    // PX in 32 x 32 tiles (K = 32 (cb + 1) rounded up to 128: Bd is upper triangular)
+    const int nc = g.kd / 32, nu = (W / 32) * nc;
+    for (int u = wg; u < nu; u += G) {
+      const int cb = u % nc, rb = u / nc;
+      const int kd = min(g.kd, (32 * (cb + 1) + 127) / 128 * 128);
+      double v[4];
+      gemm32<true, LIGHT>(g.A + (g.Kc + 32 * rb) * g.lda + g.K0p, g.lda, g.Bdp + 32 * cb, g.kd,
+                          kd, v, smem);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = tid + 256 * q;
+        st1<LIGHT>(&g.xd[(int64_t)(32 * rb + (e >> 5)) * g.kd + 32 * cb + (e & 31)], v[q]);
+      }
+    }
+    if (!(LIGHT ? grid_sync_light : grid_sync)(g.bar, G * ++nbar, g.status)) return;
+  } else if (g.kd > 0) {
     // PX: X_{s-1} rows of the block, 64-row x 128-column units (K = 128 (cb + 1), Bd upper)
     const int wp = g.kd / NB;
     const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64, li = lane & 15, lk = lane >> 4;
@@ -1237,7 +1395,26 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
   // P0: pending update of the block into the workspace (lower 128-tiles, 2 slabs each)
   {
     const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64, li = lane & 15, lk = lane >> 4;
-    const int nunit = g.w * (g.w + 1);
+    const int nunit = (g.small & 2) ? 0 : g.w * (g.w + 1);
+    if (g.small & 2) {
+      // 32 x 32 lower tiles: Wk[D] = A[D] - X X^T
+      const int nt = W / 32, ntile = nt * (nt + 1) / 2;
+      for (int u = wg; u < ntile; u += G) {
+        int ti = 0;
+        while ((ti + 1) * (ti + 2) / 2 <= u) ++ti;
+        const int tj = u - ti * (ti + 1) / 2;
+        double v[4] = {0.0, 0.0, 0.0, 0.0};
+        if (g.kd > 0)
+          gemm32<false, LIGHT>(g.xd + (int64_t)32 * ti * g.kd, g.kd, g.xd + (int64_t)32 * tj * g.kd,
+                               g.kd, g.kd, v, smem);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = tid + 256 * q;
+          const int64_t i = g.Kc + 32 * ti + (e >> 5), j = g.Kc + 32 * tj + (e & 31);
+          st1<LIGHT>(&Aw[i * W + j], ld1<LIGHT>(&g.A[i * g.lda + j]) - v[q]);
+        }
+      }
+    }
     for (int u = wg; u < nunit; u += G) {
       const int t = u >> 1, sub = u & 1;
       int ti = 0;
@@ -1261,7 +1438,9 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
         for (int jr = 0; jr < 4; ++jr) Cd[(ir * 4) * W + jr * 16] = -acc[ir][jr];
       __syncthreads();
     }
-    for (int64_t idx = (int64_t)wg * 256 + tid; idx < (int64_t)W * W / 2; idx += (int64_t)G * 256) {
+    // identity border (w = 1: Bd overwrites it whole, nothing reads it)
+    for (int64_t idx = (int64_t)wg * 256 + tid; idx < (LIGHT ? 0 : (int64_t)W * W / 2);
+         idx += (int64_t)G * 256) {
       const int r = (int)(idx / (W / 2)), c = 2 * (int)(idx % (W / 2));
       double2 v;
       v.x = (r == c) ? 1.0 : 0.0;
@@ -1270,7 +1449,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     }
   }
   stamp(1);
-  bool ok = grid_sync(g.bar, G * ++nbar, g.status);
+  bool ok = (LIGHT ? grid_sync_light : grid_sync)(g.bar, G * ++nbar, g.status);
   stamp(2);
   for (int c = 0; c < g.w && ok; ++c) {
     const int64_t kb = g.Kc + (int64_t)c * NB, r0 = kb + NB;
@@ -1278,9 +1457,10 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     // the only block (w = 1: Bd = L11^{-T}), else into linv for the panel solve below
     if (wg == 0) {
       double* Li = smem + MB_DOUBLES;
-      potrf_block<15>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB), g.status, Li);
+      potrf_block<LIGHT ? 31 : 15>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB),
+                                   g.status, Li, g.stamps && g.w == 1 ? g.stamps + 5 : nullptr);
       stamp(3 + 3 * c);
-      store_inverse_t(Li, g.w == 1 ? g.Wk + (int64_t)W * W : g.linv, g.w == 1 ? W : NB);
+      store_inverse_t<LIGHT>(Li, g.w == 1 ? g.Wk + (int64_t)W * W : g.linv, g.w == 1 ? W : NB);
       stamp(4 + 3 * c);
     }
     if (g.w == 1) break;
@@ -1321,10 +1501,15 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
   if (wg == 0) {
     if (g.n >= g.Kc && g.n < g.Kc + W)
       for (int c = tid; c < W; c += 256) g.zvec[g.Kc + c] = g.Wk[(g.n - g.Kc) * W + c];
-    __threadfence();
+    // LIGHT: Bd went out write-through and its readers load it device-coherently; zvec, parts
+    // and status are read by later launches only
+    if (LIGHT) __builtin_amdgcn_s_waitcnt(0);
+    else __threadfence();
     __syncthreads();
     stamp(15);
-    if (tid == 0) __hip_atomic_store(g.done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0)
+      __hip_atomic_store(g.done, 1u, LIGHT ? __ATOMIC_RELAXED : __ATOMIC_RELEASE,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -1726,7 +1911,9 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     hipFuncSetAttribute(reinterpret_cast<const void*>(&potrf_diag_kernel<15>),
                         hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)(MB_DOUBLES * sizeof(double)));
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_kernel),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_kernel<false>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_kernel<true>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS);
     attr = true;
   }
@@ -1829,6 +2016,11 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       const int ws = steps[s].second;
       return (unsigned)(ws * (ws + 1) + 2 * ws * steps[s - 1].second);
     };
+    // the chain's PX / P0 phases in 32 x 32 tiles (bit 0 / bit 1), for w = 1 and wider chains
+    const int chain_small1 = env_int("LFM_CHAIN_SMALL", 3);
+    const int chain_small4 = env_int("LFM_CHAIN_SMALL4", 0);
+    // w = 1 chains with both small phases: fence-free hand-offs (chain_kernel<true>)
+    const bool chain_light = env_int("LFM_CHAIN_LIGHT", 1) != 0;
     // chain(s): factor block s on the side stream's CUs (one launch, see chain_kernel)
     auto chain = [&](int s, bool dev_wait = true) {
       ChainArgs c{};
@@ -1847,6 +2039,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         c.Bdp = wkbuf(s - 1) + (int64_t)c.kd * c.kd;
         c.xd = ctx->xd;
       }
+      c.small = c.w == 1 ? chain_small1 : chain_small4;
       c.n = n;
       c.dinv = ctx->linvT;
       c.linv = ctx->linv_full;
@@ -1858,7 +2051,12 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       c.stamps = ctx->dbg_stamps ? ctx->dbg_stamps + 16 * (size_t)std::min(s, 255) : nullptr;
       hipEvent_t pe;
       prof_begin(ctx, K_POTRF, &pe, side);
-      hipLaunchKernelGGL(chain_kernel, dim3((unsigned)ctx->side_cus), dim3(256), CHAIN_LDS, side, c);
+      if (c.w == 1 && (c.small & 3) == 3 && chain_light)
+        hipLaunchKernelGGL(chain_kernel<true>, dim3((unsigned)ctx->side_cus), dim3(256), CHAIN_LDS,
+                           side, c);
+      else
+        hipLaunchKernelGGL(chain_kernel<false>, dim3((unsigned)ctx->side_cus), dim3(256), CHAIN_LDS,
+                           side, c);
       const double W = c.w * NB;
       prof_end(ctx, K_POTRF, pe, W * W * W / 3.0 + W * W * W, 0, side);
     };
