@@ -95,19 +95,58 @@ __device__ __forceinline__ double row_bcast(double v, int src) {
   }
 }
 
+// As row_bcast with one v_mov_b64_dpp (gfx90a+ 64-bit DPP, row_newbcast) instead of two
+// 32-bit moves; the compiler keeps the DPP hazards.
+template <int SRC>
+__device__ __forceinline__ double row_bcast64_t(double v) {
+  return __builtin_amdgcn_mov_dpp(v, 0x150 + SRC, 0xf, 0xf, false);
+}
+__device__ __forceinline__ double row_bcast64(double v, int src) {
+  switch (src) {
+    case 0: return row_bcast64_t<0>(v);
+    case 1: return row_bcast64_t<1>(v);
+    case 2: return row_bcast64_t<2>(v);
+    case 3: return row_bcast64_t<3>(v);
+    case 4: return row_bcast64_t<4>(v);
+    case 5: return row_bcast64_t<5>(v);
+    case 6: return row_bcast64_t<6>(v);
+    case 7: return row_bcast64_t<7>(v);
+    case 8: return row_bcast64_t<8>(v);
+    case 9: return row_bcast64_t<9>(v);
+    case 10: return row_bcast64_t<10>(v);
+    case 11: return row_bcast64_t<11>(v);
+    case 12: return row_bcast64_t<12>(v);
+    case 13: return row_bcast64_t<13>(v);
+    case 14: return row_bcast64_t<14>(v);
+    default: return row_bcast64_t<15>(v);
+  }
+}
+
 // Orders one wave's LDS writes before its following LDS reads (and vice versa): LDS
 // operations of a wave complete in order; the asm keeps the compiler from reordering.
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // ---------------------------------------------------------------- potrf
-// Two doubles; COH: device-coherent loads (agent-scope relaxed atomics bypass the XCD's L2,
-// which may hold stale lines of data another XCD wrote in the same launch).
+// Two doubles; COH: device-coherent loads that bypass the CU's vector L1, which may hold stale
+// lines of data another CU wrote (write-through) in the same launch. LFM_COH_NT (default):
+// one 16-B nontemporal load (global_load_dwordx4 nt, L2-served like sc1); else two 8-B
+// agent-scope relaxed atomic loads (sc1).
+#ifndef LFM_COH_NT
+#define LFM_COH_NT 1
+#endif
+typedef double double2v __attribute__((ext_vector_type(2)));
 template <bool COH>
 __device__ __forceinline__ double2 ld2(const double* p) {
   if (COH) {
     double2 v;
+#if LFM_COH_NT
+    const double2v t = __builtin_nontemporal_load(reinterpret_cast<const double2v*>(p));
+    v.x = t.x;
+    v.y = t.y;
+#else
     v.x = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     v.y = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
     return v;
   }
   return *reinterpret_cast<const double2*>(p);
@@ -148,8 +187,9 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 // After the loop the eight 16x16 diagonal inverses (dinv, for trsm_kernel) are built by
 // the four waves, and logdet / the first failing pivot are reduced.
 // PH (diagnostics only, lfm_probe_potrf): bit 0 = phase 1, bit 1 = phase 2, bit 2 = phase 3,
-// bit 3 = global load / store of the block. The product path always runs PH = 15, with bit 4
-// (device-coherent block loads) in the chain's light mode.
+// bit 3 = global load / store of the block. The product path always runs PH = 15, in the
+// chain kernel with bit 5 (the block load in one batch), in its light mode also bit 4
+// (device-coherent block loads) and bit 6 (no block store: nothing reads it but row n).
 // only the 36 lower 16x16 blocks of the 128x128 block, each 16 x 17 (padded) doubles:
 // 78 KB, so the kernel fits on a CU beside one SYRK workgroup (look-ahead overlap)
 constexpr int MB_DOUBLES = (NB / IB) * (NB / IB + 1) / 2 * IB * (IB + 1);
@@ -162,11 +202,17 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
                                             int* __restrict__ status,
                                             double* __restrict__ Li = nullptr,
                                             unsigned long long* __restrict__ pst = nullptr) {
-  // pst (diagnostics, NULL: off): s_memrealtime after the load (pst[0]) and after each panel
-  // iteration ib < 7 (pst[1 + ib])
+  // pst (diagnostics, NULL: off): s_memrealtime after the load (0), panel iterations 0, 3, 6
+  // (1-3), the loop (4), inverse block row 6 (5) and 7 (6), the block store (7)
   auto pstamp = [&](int p) {
     if (pst && threadIdx.x == 0) pst[p] = __builtin_amdgcn_s_memrealtime();
   };
+#ifdef LFM_PSTAMP_WAVES
+  // diagnostics: iteration 3 by wave (lane 0 of each wave)
+  auto wstamp = [&](int p) {
+    if (pst && (threadIdx.x & 63) == 0) pst[p] = __builtin_amdgcn_s_memrealtime();
+  };
+#endif
   __shared__ double pvs[NB];  // unscaled pivots
   __shared__ double ipv[NB];  // 1 / L_cc
   __shared__ double red[4];
@@ -178,19 +224,21 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
 
   // block load: row r, 16-B chunks of the lower 16x16 blocks; two batches of 16 loads per
   // thread in flight (64 VGPRs), so the kernel fits in one bulk-SYRK workgroup's registers
+  // (PH bit 5, the chain kernel with one workgroup per CU: all 32 at once)
+  constexpr int LB = (PH & 32) ? 32 : 16;
 #pragma unroll
-  for (int hb = 0; hb < 2; ++hb) {
-    double2 v[16];
+  for (int hb = 0; hb < 32 / LB; ++hb) {
+    double2 v[LB];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int idx = tid + 256 * (u + 16 * hb), r = idx >> 6, c2 = idx & 63;
+    for (int u = 0; u < LB; ++u) {
+      const int idx = tid + 256 * (u + LB * hb), r = idx >> 6, c2 = idx & 63;
       if ((2 * c2) >> 4 <= r >> 4)
         v[u] = (PH & 8) ? ld2<(PH & 16) != 0>(&A[(kb + r) * lda + kb + 2 * c2])
                         : double2{(r == 2 * c2) ? 2.0 : 0.0, (r == 2 * c2 + 1) ? 2.0 : 0.0};
     }
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int idx = tid + 256 * (u + 16 * hb), r = idx >> 6, c2 = idx & 63;
+    for (int u = 0; u < LB; ++u) {
+      const int idx = tid + 256 * (u + LB * hb), r = idx >> 6, c2 = idx & 63;
       if ((2 * c2) >> 4 <= r >> 4) {
         MS(r, 2 * c2) = v[u].x;
         MS(r, 2 * c2 + 1) = v[u].y;
@@ -208,16 +256,19 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
     double d[IB], pv[IB], yv[IB];
 #pragma unroll
     for (int q = 0; q < IB; ++q) d[q] = (lane < IB && q <= lane) ? MS(c0 + li, c0 + q) : 0.0;
+    // PH bit 7: 64-bit DPP moves (v_mov_b64_dpp, one instruction per broadcast) instead of
+    // two 32-bit ones
 #pragma unroll
     for (int c = 0; c < IB; ++c) {
-      double dc = row_bcast(d[c], c);
+      double dc = (PH & 128) ? row_bcast64(d[c], c) : row_bcast(d[c], c);
       if (kb + c0 + c >= npiv) dc = 1.0;
       const double y = rsqrt_1nr(dc);
       pv[c] = dc;
       yv[c] = y;
       d[c] = (lane == c) ? dc * y : d[c] * y;
 #pragma unroll
-      for (int q = c + 1; q < IB; ++q) d[q] = fma(-d[c], row_bcast(d[c], q), d[q]);
+      for (int q = c + 1; q < IB; ++q)
+        d[q] = fma(-d[c], (PH & 128) ? row_bcast64(d[c], q) : row_bcast(d[c], q), d[q]);
     }
     if (lane < IB) {
 #pragma unroll
@@ -308,6 +359,9 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
       }
     }
     __syncthreads();
+#ifdef LFM_PSTAMP_WAVES
+    if (ib == 3) pstamp(1);
+#endif
     if (nr == 0) break;
     // (3) wave 0: next diagonal block, then its leaf; waves 1-3: the other trailing tiles
     const int nrb = nr / IB;
@@ -337,9 +391,21 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
       else
         for (int J = w - 2; J < ib - 1; J += 2) linv_block(ib - 1, J);
     }
+#ifdef LFM_PSTAMP_WAVES
+    if (ib == 3) wstamp(2 + w);
+    if (ib == 2) pstamp(0);
+#endif
     __syncthreads();
-    pstamp(1 + ib);
+#ifdef LFM_PSTAMP_WAVES
+    if (ib == 3) pstamp(6);
+    if (ib == 4) pstamp(7);
+#else
+    if (ib == 0 || ib == 3 || ib == 6) pstamp(ib == 0 ? 1 : ib == 3 ? 2 : 3);
+#endif
   }
+#ifndef LFM_PSTAMP_WAVES
+  pstamp(4);
+#endif
   if (Li) {
     // remaining: Dinv_7 with block row 6, then block row 7
     constexpr int L7 = NB / IB - 1;
@@ -347,7 +413,13 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
     else
       for (int J = w - 1; J < L7 - 1; J += 3) linv_block(L7 - 1, J);
     __syncthreads();
+#ifndef LFM_PSTAMP_WAVES
+    pstamp(5);
+#endif
     for (int J = w; J < L7; J += 4) linv_block(L7, J);
+#ifndef LFM_PSTAMP_WAVES
+    pstamp(6);
+#endif
   }
 #undef LI
   // inverses of the eight 16x16 diagonal blocks: wave w builds blocks w and w + 4,
@@ -372,7 +444,7 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
     }
   }
   // block store (lower triangle incl. diagonal)
-  if (PH & 8) {
+  if ((PH & 8) && !(PH & 64)) {
 #pragma unroll 8
     for (int u = 0; u < 32; ++u) {
       const int idx = tid + 256 * u, r = idx >> 6, c2 = idx & 63;
@@ -384,6 +456,9 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
       }
     }
   }
+#ifndef LFM_PSTAMP_WAVES
+  pstamp(7);
+#endif
   // logdet partial = 1/2 sum log(pivot) over real pivots; first non-positive pivot
   double lg = 0.0;
   int bad = STATUS_NONE;
@@ -417,7 +492,9 @@ __device__ __forceinline__ void store_inverse_t(const double* __restrict__ Li,
 #define LI(r, q) Li[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * (IB * (IB + 1)) + \
                     ((r) & 15) * (IB + 1) + ((q) & 15)]
   __syncthreads();
-  for (int idx = threadIdx.x; idx < NB * (NB / 2); idx += 256) {
+#pragma unroll 8
+  for (int u = 0; u < NB * (NB / 2) / 256; ++u) {
+    const int idx = threadIdx.x + 256 * u;
     const int k = idx / (NB / 2), j = 2 * (idx % (NB / 2));
     double2 v;
     v.x = j >= k ? LI(j, k) : 0.0;
@@ -1326,7 +1403,7 @@ __device__ __forceinline__ void gemm32(const double* __restrict__ pi, int64_t ld
 // LIGHT (w = 1 with both small-tile phases): every value one workgroup hands to another is
 // stored write-through and loaded device-coherently, so the barriers, the input wait and the
 // completion flag need no cache maintenance (an agent-scope fence costs ~1.7-3.5 us).
-template <bool LIGHT>
+template <bool LIGHT, bool LEAF>
 __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double (*sP)[CKS + 1] = reinterpret_cast<double (*)[CKS + 1]>(smem);
@@ -1457,7 +1534,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     // the only block (w = 1: Bd = L11^{-T}), else into linv for the panel solve below
     if (wg == 0) {
       double* Li = smem + MB_DOUBLES;
-      potrf_block<LIGHT ? 31 : 15>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB),
+      potrf_block<(LIGHT ? 127 : 47) | (LEAF ? 128 : 0)>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB),
                                    g.status, Li, g.stamps && g.w == 1 ? g.stamps + 5 : nullptr);
       stamp(3 + 3 * c);
       store_inverse_t<LIGHT>(Li, g.w == 1 ? g.Wk + (int64_t)W * W : g.linv, g.w == 1 ? W : NB);
@@ -1499,8 +1576,15 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     ok = grid_sync(g.bar, G * ++nbar, g.status);
   }
   if (wg == 0) {
-    if (g.n >= g.Kc && g.n < g.Kc + W)
-      for (int c = tid; c < W; c += 256) g.zvec[g.Kc + c] = g.Wk[(g.n - g.Kc) * W + c];
+    if (g.n >= g.Kc && g.n < g.Kc + W) {
+      const int r = (int)(g.n - g.Kc);
+      // LIGHT (w = 1): row n of the factor from LDS (the block was not stored back)
+      for (int c = tid; c < W; c += 256)
+        g.zvec[g.Kc + c] = !LIGHT ? g.Wk[(int64_t)r * W + c]
+                           : c <= r ? smem[(((r >> 4) * ((r >> 4) + 1) / 2) + (c >> 4)) *
+                                               (IB * (IB + 1)) + (r & 15) * (IB + 1) + (c & 15)]
+                                    : 0.0;
+    }
     // LIGHT: Bd went out write-through and its readers load it device-coherently; zvec, parts
     // and status are read by later launches only
     if (LIGHT) __builtin_amdgcn_s_waitcnt(0);
@@ -1911,10 +1995,12 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     hipFuncSetAttribute(reinterpret_cast<const void*>(&potrf_diag_kernel<15>),
                         hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)(MB_DOUBLES * sizeof(double)));
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_kernel<false>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&chain_kernel<true>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS);
+    const void* chains[4] = {reinterpret_cast<const void*>(&chain_kernel<false, false>),
+                             reinterpret_cast<const void*>(&chain_kernel<false, true>),
+                             reinterpret_cast<const void*>(&chain_kernel<true, false>),
+                             reinterpret_cast<const void*>(&chain_kernel<true, true>)};
+    for (const void* f : chains)
+      hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS);
     attr = true;
   }
   // CHOL_MLL: factor the Mp x Mp augmented matrix (block columns holding pivots only).
@@ -2021,6 +2107,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     const int chain_small4 = env_int("LFM_CHAIN_SMALL4", 0);
     // w = 1 chains with both small phases: fence-free hand-offs (chain_kernel<true>)
     const bool chain_light = env_int("LFM_CHAIN_LIGHT", 1) != 0;
+    // the diagonal factor's serial leaf with 64-bit DPP broadcasts (potrf_block PH bit 7)
+    const bool leaf_asm = env_int("LFM_LEAF_ASM", 1) != 0;
     // chain(s): factor block s on the side stream's CUs (one launch, see chain_kernel)
     auto chain = [&](int s, bool dev_wait = true) {
       ChainArgs c{};
@@ -2051,12 +2139,10 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       c.stamps = ctx->dbg_stamps ? ctx->dbg_stamps + 16 * (size_t)std::min(s, 255) : nullptr;
       hipEvent_t pe;
       prof_begin(ctx, K_POTRF, &pe, side);
-      if (c.w == 1 && (c.small & 3) == 3 && chain_light)
-        hipLaunchKernelGGL(chain_kernel<true>, dim3((unsigned)ctx->side_cus), dim3(256), CHAIN_LDS,
-                           side, c);
-      else
-        hipLaunchKernelGGL(chain_kernel<false>, dim3((unsigned)ctx->side_cus), dim3(256), CHAIN_LDS,
-                           side, c);
+      const bool light = c.w == 1 && (c.small & 3) == 3 && chain_light;
+      auto kern = light ? (leaf_asm ? chain_kernel<true, true> : chain_kernel<true, false>)
+                        : (leaf_asm ? chain_kernel<false, true> : chain_kernel<false, false>);
+      hipLaunchKernelGGL(kern, dim3((unsigned)ctx->side_cus), dim3(256), CHAIN_LDS, side, c);
       const double W = c.w * NB;
       prof_end(ctx, K_POTRF, pe, W * W * W / 3.0 + W * W * W, 0, side);
     };
