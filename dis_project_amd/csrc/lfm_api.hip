@@ -463,6 +463,16 @@ hipError_t create_streams(lfm_ctx* ctx) {
       is_side[c] = 1;
       c = (c + stride) % ncu;
     }
+    // mask bit c lives on XCD c % 8 (observed: LFM_SIDE_STRIDE=8 puts every side CU on one XCD
+    // and the main stream's workgroups dealt to that XCD never run). Every XCD keeps the same
+    // number of main CUs, or the partition is refused.
+    {
+      std::vector<int> per_xcd(8, 0);
+      for (int c = 0; c < ncu; ++c) per_xcd[c % 8] += is_side[c] ? 0 : 1;
+      if (*std::min_element(per_xcd.begin(), per_xcd.end()) !=
+          *std::max_element(per_xcd.begin(), per_xcd.end()))
+        continue;
+    }
     std::vector<uint32_t> mside((ncu + 31) / 32, 0u), mmain((ncu + 31) / 32, 0u);
     for (int c = 0; c < ncu; ++c) (is_side[c] ? mside : mmain)[c / 32] |= 1u << (c % 32);
     e = hipExtStreamCreateWithCUMask(&ctx->m3, (uint32_t)mmain.size(), mmain.data());
