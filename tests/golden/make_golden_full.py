@@ -1,0 +1,93 @@
+"""Full-size golden values for BASELINE.json configs[1] / configs[2] from the CPU oracle.
+
+    python tests/golden/make_golden_full.py     # writes tests/golden/full_n16384.npz
+
+The inputs are not stored: configs.grid_workload / configs.c3_restarts rebuild them
+bit-identically from their seeds on any machine. Stored per case (C2 base hyperparameters and
+C3 restarts 0 and 1): the oracle's MLL (oracle/lfm_oracle.py: gram per model.py:372-414,
+Sigma per objectives.py:71-73, scipy Cholesky log-density per gpjax log_prob), its logdet and
+quadratic form, and (C2 only) the oracle gram on 16 sampled rows (row index, full row) with the
+cancellation-aware error scale for each entry (oracle.gram_error_scale). Takes a few minutes
+on 8 cores (the N^2 erf gram dominates; the Cholesky is LAPACK).
+"""
+
+from __future__ import annotations
+
+import math
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import scipy.linalg
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from dis_project_amd import configs  # noqa: E402
+from oracle import lfm_oracle as O  # noqa: E402
+
+THREADS = int(os.environ.get("GOLDEN_THREADS", str(os.cpu_count() or 8)))
+ROWS = 16
+
+
+def gram_threaded(x, D, S, l, rows=None):
+    """Oracle cross_covariance(x[rows], x) in row slabs over a thread pool."""
+    idx = np.arange(x.shape[0]) if rows is None else np.asarray(rows)
+    slabs = np.array_split(idx, max(1, len(idx) // 256))
+    out = np.empty((len(idx), x.shape[0]))
+    offs = np.cumsum([0] + [len(s) for s in slabs])
+
+    def work(i):
+        out[offs[i]:offs[i + 1]] = O.cross_covariance(x[slabs[i]], x, D, S, l, chunk=64)
+
+    with ThreadPoolExecutor(THREADS) as ex:
+        list(ex.map(work, range(len(slabs))))
+    return out
+
+
+def case(tag, model, data, rows=None):
+    t0 = time.perf_counter()
+    x = np.ascontiguousarray(data.X)
+    y = np.ascontiguousarray(data.y.reshape(-1))
+    D, S, B = (np.asarray(v, np.float64) for v in (model.true_d, model.true_s, model.true_b))
+    n = x.shape[0]
+    K = gram_threaded(x, D, S, model.l)
+    K[np.diag_indices(n)] += model.jitter + model.obs_stddev ** 2  # objectives.py:71-73
+    m = O.mean_function(x, D, B, model.num_genes).reshape(-1)
+    r = y - m
+    c, low = scipy.linalg.cho_factor(K, lower=True, overwrite_a=True, check_finite=False)
+    logdet = 2.0 * float(np.sum(np.log(np.diag(c))))
+    z = scipy.linalg.solve_triangular(c, r, lower=True, check_finite=False)
+    quad = float(z @ z)
+    mll = -0.5 * (n * math.log(2 * math.pi) + logdet + quad)
+    del K, c
+    print(f"{tag}: n={n} mll={mll!r} logdet={logdet!r} quad={quad!r} "
+          f"({time.perf_counter() - t0:.1f} s)", flush=True)
+    res = {f"{tag}_mll": np.float64(mll), f"{tag}_logdet": np.float64(logdet),
+           f"{tag}_quad": np.float64(quad)}
+    if rows is not None:
+        res[f"{tag}_rows"] = np.asarray(rows, np.int64)
+        res[f"{tag}_krows"] = gram_threaded(x, D, S, model.l, rows)
+        # a tolerance scale: fp32 is plenty
+        res[f"{tag}_kscale"] = np.concatenate(
+            [O.gram_error_scale(x[[i]], x, D, S, model.l) for i in rows]).astype(np.float32)
+    return res
+
+
+def main():
+    base = configs.c2()
+    rng = np.random.default_rng(2024)
+    rows = np.sort(np.concatenate([[0, 127, 128, 8191, base.n - 1],
+                                   rng.choice(base.n, ROWS - 5, replace=False)]))
+    out = {}
+    out.update(case("c2", base.model, base.data, rows))
+    for r in (0, 1):
+        out.update(case(f"c3_r{r}", configs.c3_restarts(base, 2)[r], base.data))
+    np.savez_compressed(os.path.join(HERE, "full_n16384.npz"), **out)
+
+
+if __name__ == "__main__":
+    main()

@@ -192,3 +192,22 @@ def test_predictor_oracle_identities():
     lm2, lv2 = O.latent_predict(x, y, v, g["t_lat"], D, S, B, l, float(g["jitter"]))
     np.testing.assert_array_equal(lm2, g["lat_mean"])
     np.testing.assert_array_equal(lv2, g["lat_var"])
+
+
+def test_full_size_golden_rows_regenerate():
+    """tests/golden/full_n16384.npz (make_golden_full.py): the stored C2 gram rows regenerate
+    bit-exactly from the seeded inputs, and the stored MLL is consistent with its logdet /
+    quadratic-form parts."""
+    from dis_project_amd import configs
+
+    g = load_golden("full_n16384")
+    work = configs.c2()
+    x = np.ascontiguousarray(work.data.X)
+    m = work.model
+    for i in (0, len(g["c2_rows"]) - 1):
+        row = O.cross_covariance(x[[int(g["c2_rows"][i])]], x, m.true_d, m.true_s, m.l, chunk=64)
+        np.testing.assert_array_equal(row[0], g["c2_krows"][i])
+    for tag in ("c2", "c3_r0", "c3_r1"):
+        n = x.shape[0]
+        mll = -0.5 * (n * math.log(2 * math.pi) + float(g[tag + "_logdet"]) + float(g[tag + "_quad"]))
+        assert mll == pytest.approx(float(g[tag + "_mll"]), rel=1e-15)
