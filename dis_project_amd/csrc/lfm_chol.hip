@@ -188,8 +188,9 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 // the four waves, and logdet / the first failing pivot are reduced.
 // PH (diagnostics only, lfm_probe_potrf): bit 0 = phase 1, bit 1 = phase 2, bit 2 = phase 3,
 // bit 3 = global load / store of the block. The product path always runs PH = 15, in the
-// chain kernel with bit 5 (the block load in one batch), in its light mode also bit 4
-// (device-coherent block loads) and bit 6 (no block store: nothing reads it but row n).
+// chain kernel with bit 5 (the block load in one batch) and bit 7 (64-bit DPP broadcasts in
+// the leaf), in its light mode also bit 4 (device-coherent block loads) and bit 6 (no block
+// store: nothing reads it but row n).
 // only the 36 lower 16x16 blocks of the 128x128 block, each 16 x 17 (padded) doubles:
 // 78 KB, so the kernel fits on a CU beside one SYRK workgroup (look-ahead overlap)
 constexpr int MB_DOUBLES = (NB / IB) * (NB / IB + 1) / 2 * IB * (IB + 1);
@@ -207,12 +208,6 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
   auto pstamp = [&](int p) {
     if (pst && threadIdx.x == 0) pst[p] = __builtin_amdgcn_s_memrealtime();
   };
-#ifdef LFM_PSTAMP_WAVES
-  // diagnostics: iteration 3 by wave (lane 0 of each wave)
-  auto wstamp = [&](int p) {
-    if (pst && (threadIdx.x & 63) == 0) pst[p] = __builtin_amdgcn_s_memrealtime();
-  };
-#endif
   __shared__ double pvs[NB];  // unscaled pivots
   __shared__ double ipv[NB];  // 1 / L_cc
   __shared__ double red[4];
@@ -359,9 +354,6 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
       }
     }
     __syncthreads();
-#ifdef LFM_PSTAMP_WAVES
-    if (ib == 3) pstamp(1);
-#endif
     if (nr == 0) break;
     // (3) wave 0: next diagonal block, then its leaf; waves 1-3: the other trailing tiles
     const int nrb = nr / IB;
@@ -391,21 +383,10 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
       else
         for (int J = w - 2; J < ib - 1; J += 2) linv_block(ib - 1, J);
     }
-#ifdef LFM_PSTAMP_WAVES
-    if (ib == 3) wstamp(2 + w);
-    if (ib == 2) pstamp(0);
-#endif
     __syncthreads();
-#ifdef LFM_PSTAMP_WAVES
-    if (ib == 3) pstamp(6);
-    if (ib == 4) pstamp(7);
-#else
     if (ib == 0 || ib == 3 || ib == 6) pstamp(ib == 0 ? 1 : ib == 3 ? 2 : 3);
-#endif
   }
-#ifndef LFM_PSTAMP_WAVES
   pstamp(4);
-#endif
   if (Li) {
     // remaining: Dinv_7 with block row 6, then block row 7
     constexpr int L7 = NB / IB - 1;
@@ -413,13 +394,9 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
     else
       for (int J = w - 1; J < L7 - 1; J += 3) linv_block(L7 - 1, J);
     __syncthreads();
-#ifndef LFM_PSTAMP_WAVES
     pstamp(5);
-#endif
     for (int J = w; J < L7; J += 4) linv_block(L7, J);
-#ifndef LFM_PSTAMP_WAVES
     pstamp(6);
-#endif
   }
 #undef LI
   // inverses of the eight 16x16 diagonal blocks: wave w builds blocks w and w + 4,
@@ -456,9 +433,7 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
       }
     }
   }
-#ifndef LFM_PSTAMP_WAVES
   pstamp(7);
-#endif
   // logdet partial = 1/2 sum log(pivot) over real pivots; first non-positive pivot
   double lg = 0.0;
   int bad = STATUS_NONE;
@@ -1403,7 +1378,7 @@ __device__ __forceinline__ void gemm32(const double* __restrict__ pi, int64_t ld
 // LIGHT (w = 1 with both small-tile phases): every value one workgroup hands to another is
 // stored write-through and loaded device-coherently, so the barriers, the input wait and the
 // completion flag need no cache maintenance (an agent-scope fence costs ~1.7-3.5 us).
-template <bool LIGHT, bool LEAF>
+template <bool LIGHT>
 __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double (*sP)[CKS + 1] = reinterpret_cast<double (*)[CKS + 1]>(smem);
@@ -1534,7 +1509,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     // the only block (w = 1: Bd = L11^{-T}), else into linv for the panel solve below
     if (wg == 0) {
       double* Li = smem + MB_DOUBLES;
-      potrf_block<(LIGHT ? 127 : 47) | (LEAF ? 128 : 0)>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB),
+      potrf_block<(LIGHT ? 127 : 47) | 128>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB),
                                    g.status, Li, g.stamps && g.w == 1 ? g.stamps + 5 : nullptr);
       stamp(3 + 3 * c);
       store_inverse_t<LIGHT>(Li, g.w == 1 ? g.Wk + (int64_t)W * W : g.linv, g.w == 1 ? W : NB);
@@ -1995,10 +1970,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     hipFuncSetAttribute(reinterpret_cast<const void*>(&potrf_diag_kernel<15>),
                         hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)(MB_DOUBLES * sizeof(double)));
-    const void* chains[4] = {reinterpret_cast<const void*>(&chain_kernel<false, false>),
-                             reinterpret_cast<const void*>(&chain_kernel<false, true>),
-                             reinterpret_cast<const void*>(&chain_kernel<true, false>),
-                             reinterpret_cast<const void*>(&chain_kernel<true, true>)};
+    const void* chains[2] = {reinterpret_cast<const void*>(&chain_kernel<false>),
+                             reinterpret_cast<const void*>(&chain_kernel<true>)};
     for (const void* f : chains)
       hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS);
     attr = true;
@@ -2107,8 +2080,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     const int chain_small4 = env_int("LFM_CHAIN_SMALL4", 0);
     // w = 1 chains with both small phases: fence-free hand-offs (chain_kernel<true>)
     const bool chain_light = env_int("LFM_CHAIN_LIGHT", 1) != 0;
-    // the diagonal factor's serial leaf with 64-bit DPP broadcasts (potrf_block PH bit 7)
-    const bool leaf_asm = env_int("LFM_LEAF_ASM", 1) != 0;
     // chain(s): factor block s on the side stream's CUs (one launch, see chain_kernel)
     auto chain = [&](int s, bool dev_wait = true) {
       ChainArgs c{};
@@ -2140,8 +2111,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       hipEvent_t pe;
       prof_begin(ctx, K_POTRF, &pe, side);
       const bool light = c.w == 1 && (c.small & 3) == 3 && chain_light;
-      auto kern = light ? (leaf_asm ? chain_kernel<true, true> : chain_kernel<true, false>)
-                        : (leaf_asm ? chain_kernel<false, true> : chain_kernel<false, false>);
+      auto kern = light ? chain_kernel<true> : chain_kernel<false>;
       hipLaunchKernelGGL(kern, dim3((unsigned)ctx->side_cus), dim3(256), CHAIN_LDS, side, c);
       const double W = c.w * NB;
       prof_end(ctx, K_POTRF, pe, W * W * W / 3.0 + W * W * W, 0, side);
