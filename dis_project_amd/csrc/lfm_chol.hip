@@ -1901,7 +1901,15 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   else
     hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8, ctx->stream);
   const unsigned tiles = (unsigned)((int64_t)T * (T + 1) / 2);
-  hipStream_t st = ctx->stream;
+  // cio bit 4: on schedule 3's CU-masked main stream (the bulk's CUs) instead of every CU
+  hipStream_t st = (cio & 16) && ctx->m3 ? ctx->m3 : ctx->stream;
+  if (st != ctx->stream) {
+    hipEvent_t f;
+    hipEventCreate(&f);
+    hipEventRecord(f, ctx->stream);
+    hipStreamWaitEvent(st, f, 0);
+    hipEventDestroy(f);
+  }
   const Panel pan{ctx->A, n, 0};
   auto go = [&]() {
     if (cio & 4) {  // 64-row slabs, C I/O
