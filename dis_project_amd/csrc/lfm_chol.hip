@@ -1892,6 +1892,20 @@ __global__ void fill_hash_kernel(double* a, int64_t cnt) {
   }
 }
 
+// Diagnostic load for probe_syrk (cio bit 5): one workgroup per side CU issuing fp64 MFMAs on
+// register operands for `iters` rounds, as an upper bound of the chain's power draw.
+__global__ __launch_bounds__(256) void mfma_burn_kernel(double* out, int iters) {
+  double a = 1.0 + threadIdx.x * 1e-3, b = 1.0 - threadIdx.x * 1e-3;
+  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int i = 0; i < iters; ++i)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] = mfma4(a + u, b, acc[u]);
+  double t = 0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) t += acc[u];
+  if (t == 1.2345e300) out[0] = t;
+}
+
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const int64_t n = (int64_t)T * ST + 512;
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
@@ -1928,6 +1942,16 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
+  if ((cio & 32) && ctx->s3) {
+    hipEvent_t f;
+    hipEventCreate(&f);
+    hipEventRecord(f, st);
+    hipStreamWaitEvent(ctx->s3, f, 0);
+    hipEventDestroy(f);
+    // ~ (reps + 1) x the probe's duration of MFMA issue on the side CUs
+    hipLaunchKernelGGL(mfma_burn_kernel, dim3((unsigned)ctx->side_cus), dim3(256), 0, ctx->s3,
+                       ctx->A, 400000 * (reps + 1));
+  }
   hipEventRecord(a, st);
   for (int i = 0; i < reps; ++i) go();
   hipEventRecord(b, st);
@@ -1936,6 +1960,7 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   hipEventElapsedTime(&ms, a, b);
   hipEventDestroy(a);
   hipEventDestroy(b);
+  if ((cio & 32) && ctx->s3) hipStreamSynchronize(ctx->s3);
   *us = ms * 1e3 / reps;
   return hip_fail(ctx, e, "probe_syrk");
 }
