@@ -112,6 +112,9 @@ SIGNATURES = [
     ("lfm_memcpy_h2d", c_int, [_c_ctx, c_void_p, c_void_p, c_size_t]),
     ("lfm_memcpy_d2h", c_int, [_c_ctx, c_void_p, c_void_p, c_size_t]),
     ("lfm_mll_f64_dev", c_int, [_c_ctx, c_void_p, c_void_p, c_int64, POINTER(LfmHyp), c_int, _dptr]),
+    ("lfm_data_create", c_int, [_c_ctx, c_void_p, c_void_p, c_int64, POINTER(c_void_p)]),
+    ("lfm_data_destroy", c_int, [c_void_p]),
+    ("lfm_mll_f64_data", c_int, [_c_ctx, c_void_p, POINTER(LfmHyp), c_int, _dptr]),
     ("lfm_gram_f64_dev", c_int,
      [_c_ctx, c_void_p, c_int64, POINTER(LfmHyp), c_double, c_int, c_void_p, c_int64]),
     ("lfm_gram_f32_dev", c_int,

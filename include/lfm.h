@@ -156,6 +156,17 @@ int lfm_memcpy_d2h(lfm_ctx* ctx, void* dst, const void* src, size_t bytes);
 /* As lfm_mll_f64 with x / y already on the ctx's device. */
 int lfm_mll_f64_dev(lfm_ctx* ctx, const double* d_x, const double* d_y, int64_t n,
                     const lfm_hyp* hyp, int negative, double* out);
+/* A device-resident dataset evaluated many times (training steps, random restarts): x (and y
+ * when n is small) is read back and analysed once, here, instead of on every call. The caller
+ * keeps d_x / d_y allocated and unmodified until lfm_data_destroy — the reference's Dataset is
+ * an immutable JAX array pair (gpjax Dataset, objectives.py:21 / trainer.py:126) likewise. */
+typedef struct lfm_data lfm_data;
+int lfm_data_create(lfm_ctx* ctx, const double* d_x, const double* d_y, int64_t n,
+                    lfm_data** out);
+int lfm_data_destroy(lfm_data* data);
+/* As lfm_mll_f64_dev on a dataset handle. */
+int lfm_mll_f64_data(lfm_ctx* ctx, lfm_data* data, const lfm_hyp* hyp, int negative,
+                     double* out);
 /* As lfm_gram_f64 / _f32 with x and out on the device. */
 int lfm_gram_f64_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* hyp,
                      double diag_add, int uplo, double* d_out, int64_t ldo);

@@ -119,3 +119,42 @@ def test_gram_rows_n16384_vs_golden(full, c2_dev):
     err = np.abs(got - ref)
     tol = 16 * np.finfo(np.float64).eps * scale
     assert np.all(err <= tol), (err / tol).max()
+
+
+def test_dataset_handle_matches_per_call_path(c2_dev):
+    """lfm_mll_f64_data (layout analysed once per dataset) returns exactly what
+    lfm_mll_f64_dev returns, for two hyperparameter sets and for a small (fused-kernel) n."""
+    from dis_project_amd import _lib, configs
+
+    ctx, work, dx, dy = c2_dev
+    lib, h = ctx.lib, ctx.handle
+    data = _lib.c_void_p()
+    ctx.check(lib.lfm_data_create(h, dx, dy, work.n, _lib.ctypes.byref(data)))
+    try:
+        for model in (work.model, configs.c3_restarts(work, 1)[0]):
+            hp = model.hyp()
+            a, b = np.empty(1), np.empty(1)
+            ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, work.n, hp.ref, 1, _lib.dptr(a)))
+            ctx.check(lib.lfm_mll_f64_data(h, data, hp.ref, 1, _lib.dptr(b)))
+            assert a[0] == b[0], (a[0], b[0])
+    finally:
+        lib.lfm_data_destroy(data)
+    small = configs.c1_p53()
+    x = np.ascontiguousarray(small.data.X)
+    y = np.ascontiguousarray(small.data.y.reshape(-1))
+    sx, sy = _lib.c_void_p(), _lib.c_void_p()
+    ctx.check(lib.lfm_dev_alloc(h, x.nbytes, _lib.ctypes.byref(sx)))
+    ctx.check(lib.lfm_dev_alloc(h, y.nbytes, _lib.ctypes.byref(sy)))
+    try:
+        ctx.check(lib.lfm_memcpy_h2d(h, sx, x.ctypes.data, x.nbytes))
+        ctx.check(lib.lfm_memcpy_h2d(h, sy, y.ctypes.data, y.nbytes))
+        ctx.check(lib.lfm_data_create(h, sx, sy, x.shape[0], _lib.ctypes.byref(data)))
+        hp = small.model.hyp()
+        a, b = np.empty(1), np.empty(1)
+        ctx.check(lib.lfm_mll_f64(h, _lib.dptr(x), _lib.dptr(y), x.shape[0], hp.ref, 1, _lib.dptr(a)))
+        ctx.check(lib.lfm_mll_f64_data(h, data, hp.ref, 1, _lib.dptr(b)))
+        lib.lfm_data_destroy(data)
+        assert a[0] == b[0], (a[0], b[0])
+    finally:
+        lib.lfm_dev_free(h, sx)
+        lib.lfm_dev_free(h, sy)
