@@ -797,7 +797,8 @@ struct Panel {
 // index in the enumeration below.
 // Returns whether the unit's tile lies in the leading coh_lim x coh_lim tiles of the trailing
 // matrix (stores then write through to memory: device-coherent, for an in-flight reader).
-template <bool CIO, int TR, bool COH = false, int KS = KB>
+// LDCOH: C and panel loads device-coherent too (a reader of data written in the same launch).
+template <bool CIO, int TR, bool COH = false, int KS = KB, bool LDCOH = false>
 __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, int64_t s, Panel P,
                                           int kd, int T, int tj_lo, int tj_hi, int64_t b, int ti0,
                                           double (*__restrict__ sP)[KS + 1], int coh_lim = 0,
@@ -841,8 +842,8 @@ __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, i
 #pragma unroll
   for (int ir = 0; ir < IRN; ++ir)
 #pragma unroll
-    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = CIO ? -Cb[ir * ld4 + jr * 16] : 0.0;
-  gemm_accumulate<TR, false, false, KS>(P.p + (i0 - P.r0) * P.ld, P.ld, P.p + (j0 - P.r0) * P.ld,
+    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = CIO ? -ld1<LDCOH>(&Cb[ir * ld4 + jr * 16]) : 0.0;
+  gemm_accumulate<TR, false, LDCOH, KS>(P.p + (i0 - P.r0) * P.ld, P.ld, P.p + (j0 - P.r0) * P.ld,
                                         P.ld, kd, acc, sP);
 
   int ld4s = ld4;
@@ -1906,6 +1907,17 @@ __global__ __launch_bounds__(256) void mfma_burn_kernel(double* out, int iters) 
   if (t == 1.2345e300) out[0] = t;
 }
 
+// probe_syrk cio bit 6: every store write-through and every load device-coherent (the cost
+// of streaming consecutive steps through one launch)
+__global__ __launch_bounds__(256, LFM_SLAB_WGS) void syrk_coh_kernel(double* __restrict__ A,
+                                                                    int64_t lda, int64_t s,
+                                                                    Panel P, int kd, int T) {
+  __shared__ double sP[64 + ST][KB + 1];
+  int64_t lo, hi;
+  xcd_range(gridDim.x, (int)(blockIdx.x % 8), &lo, &hi);
+  syrk_unit<true, 64, true, KB, true>(A, lda, s, P, kd, T, 0, T, lo + blockIdx.x / 8, 0, sP);
+}
+
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const int64_t n = (int64_t)T * ST + 512;
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
@@ -1926,6 +1938,11 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   }
   const Panel pan{ctx->A, n, 0};
   auto go = [&]() {
+    if (cio & 64) {
+      hipLaunchKernelGGL(syrk_coh_kernel, dim3(2 * tiles), dim3(256), 0, st, ctx->A, n,
+                         (int64_t)512, pan, kd, T);
+      return;
+    }
     if (cio & 4) {  // 64-row slabs, C I/O
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(2 * tiles), dim3(256), 0, st, ctx->A, n,
                          (int64_t)512, pan, kd, T, 0, T, 0, ctx->xcd_remap, 0, (int64_t)0);
