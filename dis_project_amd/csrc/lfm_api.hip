@@ -419,6 +419,10 @@ static int gram_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* h
 }
 
 namespace {
+int env_int_api(const char* name, int def) {
+  const char* v = std::getenv(name);
+  return v ? std::atoi(v) : def;
+}
 // Main + high-priority side stream (every CU), and for schedule 3 a CU-partitioned pair:
 // LFM_SIDE_CUS (default 32) CUs for the factor chain, the rest for the bulk
 // (hipExtStreamCreateWithCUMask). LFM_LOOKAHEAD=0 serialises on one stream.
@@ -460,9 +464,14 @@ hipError_t create_streams(lfm_ctx* ctx) {
   // (one per CU) resident at once: checked here, halving the reservation until it holds.
   const char* sst = std::getenv("LFM_SIDE_STRIDE");
   const int stride = sst ? std::max(1, std::atoi(sst)) : 1;
+  // two contexts evaluating concurrently on one GPU (scripts/c3_pipe.py): LFM_SIDE_FIRST = the
+  // first side CU bit, LFM_MAIN_SKIP = CU bits [0, skip) kept off the main stream as well (the
+  // other context's chain CUs)
+  const int side_first = std::max(0, env_int_api("LFM_SIDE_FIRST", 0)) % std::max(1, ncu);
+  const int main_skip = std::max(0, env_int_api("LFM_MAIN_SKIP", 0));
   for (int cus = side_cus; cus >= 4; cus /= 2) {
     std::vector<char> is_side(ncu, 0);
-    for (int j = 0, c = 0; j < cus; ++j) {
+    for (int j = 0, c = side_first; j < cus; ++j) {
       while (is_side[c]) c = (c + 1) % ncu;
       is_side[c] = 1;
       c = (c + stride) % ncu;
@@ -472,13 +481,16 @@ hipError_t create_streams(lfm_ctx* ctx) {
     // number of main CUs, or the partition is refused.
     {
       std::vector<int> per_xcd(8, 0);
-      for (int c = 0; c < ncu; ++c) per_xcd[c % 8] += is_side[c] ? 0 : 1;
+      for (int c = 0; c < ncu; ++c) per_xcd[c % 8] += (is_side[c] || c < main_skip) ? 0 : 1;
       if (*std::min_element(per_xcd.begin(), per_xcd.end()) !=
           *std::max_element(per_xcd.begin(), per_xcd.end()))
         continue;
     }
     std::vector<uint32_t> mside((ncu + 31) / 32, 0u), mmain((ncu + 31) / 32, 0u);
-    for (int c = 0; c < ncu; ++c) (is_side[c] ? mside : mmain)[c / 32] |= 1u << (c % 32);
+    for (int c = 0; c < ncu; ++c) {
+      if (is_side[c]) mside[c / 32] |= 1u << (c % 32);
+      else if (c >= main_skip) mmain[c / 32] |= 1u << (c % 32);
+    }
     e = hipExtStreamCreateWithCUMask(&ctx->m3, (uint32_t)mmain.size(), mmain.data());
     if (e == hipSuccess)
       e = hipExtStreamCreateWithCUMask(&ctx->s3, (uint32_t)mside.size(), mside.data());
