@@ -167,8 +167,21 @@ __global__ __launch_bounds__(256) void gram_grid_aligned_kernel(
   constexpr int R = 64, C = 256, WIN = C + R - 1;
   __shared__ T sWk[WIN], sXk[WIN], sWj[WIN], sXj[WIN];
   __shared__ T sPk[R], sEj[R], sQj[R];
-  const int64_t c0 = (int64_t)blockIdx.x * C, r0 = (int64_t)blockIdx.y * R;
-  if (lower && c0 > r0 + R - 1) return;
+  int64_t c0, r0;
+  if (lower) {
+    // 1-D grid over the lower tiles only: 64-row tile row rb = 4 q + r holds q + 1 tiles of
+    // 256 columns, so tile rows 4q .. 4q + 3 start at tile index 2 q (q + 1)
+    const int64_t b = blockIdx.x;
+    int64_t q = (int64_t)((sqrt(2.0 * (double)b + 1.0) - 1.0) * 0.5);
+    while (2 * (q + 1) * (q + 2) <= b) ++q;
+    while (2 * q * (q + 1) > b) --q;
+    const int64_t off = b - 2 * q * (q + 1);
+    r0 = (4 * q + off / (q + 1)) * R;
+    c0 = (off % (q + 1)) * C;
+  } else {
+    c0 = (int64_t)blockIdx.x * C;
+    r0 = (int64_t)blockIdx.y * R;
+  }
   const int tid = threadIdx.x;
   const int W = 2 * Tn - 1;
   const T* Wt = tab;
@@ -242,7 +255,9 @@ int launch_gram_grid(lfm_ctx* ctx, const HypDev& h, const GridLayout& lay, const
   hipEvent_t ev;
   prof_begin(ctx, K_GRAM_GRID, &ev);
   if (lay.T % 256 == 0) {
-    dim3 grid((unsigned)(n / 256), (unsigned)(n / 64));
+    // lower: only the lower tiles are launched (2 Q (Q + 1) of them, Q = n / 256)
+    const int64_t Q = n / 256;
+    dim3 grid = lower ? dim3((unsigned)(2 * Q * (Q + 1))) : dim3((unsigned)(n / 256), (unsigned)(n / 64));
     hipLaunchKernelGGL((gram_grid_aligned_kernel<OutT>), grid, dim3(256), 0, ctx->stream, tabT,
                        h.G, lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out, ldo);
   } else {
