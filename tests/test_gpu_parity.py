@@ -284,11 +284,12 @@ def test_pivot_rsqrt_one_newton_step(lfm):
 @pytest.mark.parametrize("env", [{"LFM_SCHED": "3"}, {"LFM_SCHED": "3", "LFM_S3_EVENTS": "1"},
                                  {"LFM_SCHED": "3", "LFM_W4_MIN": "1024"},
                                  {"LFM_SCHED": "3", "LFM_W4_MIN": "1024", "LFM_S3_EVENTS": "1"},
+                                 {"LFM_SCHED": "3", "LFM_W4_MIN": "1073741824", "LFM_W2_MIN": "1024"},
                                  {"LFM_SCHED": "1"}, {"LFM_SCHED": "3", "LFM_SIDE_CUS": "8"}])
 def test_mll_schedules_agree(lfm, env, monkeypatch):
     """N = 2560 (10 genes x 256): schedule 3 device-ordered (default), schedule 3 event-ordered
-    (profiling mode), both with w = 4 super-panels (LFM_W4_MIN=1024), schedule 1 and a smaller
-    chain partition all match the oracle to 1e-9."""
+    (profiling mode), both with w = 4 super-panels (LFM_W4_MIN=1024), w = 2 super-panels,
+    schedule 1 and a smaller chain partition all match the oracle to 1e-9."""
     from dis_project_amd import _lib, configs
 
     for k, v in env.items():
