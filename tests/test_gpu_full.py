@@ -158,3 +158,28 @@ def test_dataset_handle_matches_per_call_path(c2_dev):
     finally:
         lib.lfm_dev_free(h, sx)
         lib.lfm_dev_free(h, sy)
+
+
+@pytest.mark.parametrize("env", [{"LFM_SCHED": "1"}, {"LFM_SCHED": "3", "LFM_S3_EVENTS": "1"},
+                                 {"LFM_SCHED": "3", "LFM_CHAIN_LIGHT": "0", "LFM_CHAIN_SMALL": "0"}])
+def test_mll_n16384_other_schedules_vs_golden(full, env, monkeypatch):
+    """The full-size C2 MLL through schedule 1 (potrf / trsm / SYRK launches), schedule 3 in
+    its event-ordered profiling mode, and schedule 3 with the w = 1 chain's fenced 64 x 128
+    PX / P0 phases — each against the golden value at 1e-9."""
+    from dis_project_amd import _lib, configs
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    work = configs.c2()
+    x = np.ascontiguousarray(work.data.X)
+    y = np.ascontiguousarray(work.data.y.reshape(-1))
+    ctx = _lib.Context(0)  # schedule knobs are read when a context is created / per call
+    try:
+        out = np.empty(1)
+        hp = work.model.hyp()
+        ctx.check(ctx.lib.lfm_mll_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0], hp.ref,
+                                      0, _lib.dptr(out)))
+        ref = float(full["c2_mll"])
+        assert abs(out[0] - ref) <= MLL_RTOL * abs(ref), (env, out[0], ref)
+    finally:
+        ctx.close()
