@@ -212,7 +212,9 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
   __shared__ double ipv[NB];  // 1 / L_cc
   __shared__ double red[4];
   __shared__ int redi[4];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // opaque: the callers' loops do not hoist and hold its index math
+  const int lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lk = lane >> 4;
 #define MS(r, q) Mb[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * (IB * (IB + 1)) + \
                     ((r) & 15) * (IB + 1) + ((q) & 15)]
@@ -1232,7 +1234,8 @@ struct ChainArgs {
   int64_t K0p;             // first column of super-panel s - 1
   const double* Bdp;       // Bd_{s-1}: kd x kd, ld kd
   double* xd;              // W x kd scratch
-  int small;               // bit 0: PX, bit 1: P0 in 32 x 32 tiles (gemm32)
+  int small;               // bit 0: PX, bit 1: P0, bit 2: in-chain panel solve and band
+                           // update (w > 1) in 32 x 32 tiles (gemm32)
 };
 
 // dynamic LDS of chain_kernel: the factor block and its inverse (packed 16x16 blocks)
@@ -1305,12 +1308,15 @@ static_assert(2 * MB_DOUBLES >= (64 + ST) * (CKS + 1), "chain LDS union");
 // 32 k of a stage and their partial tiles are summed through LDS at the end.
 // LDS: smem[0, 2 * 32 * G32K) (operands) and then [0, 4 * 32 * 33) (partials, aliased).
 constexpr int G32K = 129;  // LDS row stride of a 128-deep operand row
-static_assert(2 * MB_DOUBLES >= 2 * 32 * G32K && 2 * MB_DOUBLES >= 4 * 32 * 33, "gemm32 LDS");
+static_assert(2 * MB_DOUBLES >= 2 * 32 * G32K + 4 * 1024 && 2 * MB_DOUBLES >= 4 * 32 * 33,
+              "gemm32 LDS (+ the in-chain solve's parked output tiles)");
 template <bool BT, bool COH = false>
 __device__ __forceinline__ void gemm32(const double* __restrict__ pi, int64_t ldi,
                                        const double* __restrict__ pj, int64_t ldj, int kd,
                                        double (&v)[4], double* __restrict__ smem) {
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // opaque: index math is redone per call, not hoisted and held
+  const int lane = tid & 63, w = tid >> 6;
   const int li = lane & 15, lk = lane >> 4, l3 = lane & 3;
   double* sA = smem;             // [32][G32K]: P rows
   double* sB = smem + 32 * G32K;  // [32][G32K]: Q columns (j-major)
@@ -1521,7 +1527,30 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     if (!ok) break;
     // panel solve of every workspace row below block c as a GEMM: X = A_c Linv_c^T
     const int64_t rows = g.Kc + 2 * W - r0;
-    {
+    if (g.small & 4) {
+      // 32-row units, one workgroup each (the solve is in place: a unit owns its rows), the
+      // four 32-column output tiles parked in LDS past gemm32's operands until all are formed
+      double* park = smem + 2 * 32 * G32K;
+      for (int64_t u = wg; u < rows / 32; u += G) {
+        const int64_t ra = r0 + 32 * u;
+#pragma unroll 1
+        for (int jc = 0; jc < 4; ++jc) {
+          double v[4];
+          gemm32<true>(Aw + ra * W + kb, W, g.linv + 32 * jc, NB, NB, v, smem);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) park[jc * 1024 + tid + 256 * q] = v[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int jc = 0; jc < 4; ++jc)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q;
+            Aw[(ra + (e >> 5)) * W + kb + 32 * jc + (e & 31)] = park[jc * 1024 + e];
+          }
+        __syncthreads();
+      }
+    } else {
       const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64, li = lane & 15, lk = lane >> 4;
       for (int64_t u = wg; u < rows / 64; u += G) {
         const int64_t ra = r0 + 64 * u;
@@ -1543,11 +1572,35 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     stamp(5 + 3 * c);
     if (!ok || c + 1 == g.w) break;
     const int T = (int)(rows / ST), hi = g.w - 1 - c;
-    int64_t nunit = 0;
-    for (int tj = 0; tj < hi; ++tj) nunit += 2 * (T - tj);
-    for (int64_t u = wg; u < nunit; u += G) {
-      syrk_unit<true, 64, false, CKS>(Aw, W, r0, Panel{Aw + kb, W, 0}, NB, T, 0, hi, u, 0, sP);
-      __syncthreads();
+    if (g.small & 4) {
+      // band update in 32 x 32 tiles: columns r0 .. r0 + 128 hi, every row below (diagonal
+      // tiles whole: their upper part is never read)
+      const int R32 = (int)(rows / 32), J32 = 4 * hi;
+      int nt = 0;
+      for (int jt = 0; jt < J32; ++jt) nt += R32 - jt;
+      for (int u = wg; u < nt; u += G) {
+        int jt = 0, rem = u;
+        while (rem >= R32 - jt) {
+          rem -= R32 - jt;
+          ++jt;
+        }
+        const int it = jt + rem;
+        const int64_t ra = r0 + 32 * it, ca = r0 + 32 * jt;
+        double v[4];
+        gemm32<false>(Aw + ra * W + kb, W, Aw + ca * W + kb, W, NB, v, smem);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = tid + 256 * q;
+          Aw[(ra + (e >> 5)) * W + ca + (e & 31)] -= v[q];
+        }
+      }
+    } else {
+      int64_t nunit = 0;
+      for (int tj = 0; tj < hi; ++tj) nunit += 2 * (T - tj);
+      for (int64_t u = wg; u < nunit; u += G) {
+        syrk_unit<true, 64, false, CKS>(Aw, W, r0, Panel{Aw + kb, W, 0}, NB, T, 0, hi, u, 0, sP);
+        __syncthreads();
+      }
     }
     ok = grid_sync(g.bar, G * ++nbar, g.status);
   }
@@ -2128,7 +2181,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     };
     // the chain's PX / P0 phases in 32 x 32 tiles (bit 0 / bit 1), for w = 1 and wider chains
     const int chain_small1 = env_int("LFM_CHAIN_SMALL", 3);
-    const int chain_small4 = env_int("LFM_CHAIN_SMALL4", 0);
+    const int chain_small4 = env_int("LFM_CHAIN_SMALL4", 7);  // bit 2: in-chain solve / band
     // w = 1 chains with both small phases: fence-free hand-offs (chain_kernel<true>)
     const bool chain_light = env_int("LFM_CHAIN_LIGHT", 1) != 0;
     // chain(s): factor block s on the side stream's CUs (one launch, see chain_kernel)
