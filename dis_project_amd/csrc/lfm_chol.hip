@@ -285,15 +285,30 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
     }
   };
   // one 16x16 tile (i0, j0) -= panel c0 rows i0 x rows j0 (fp64 MFMA), in LDS
+  // (block offsets from wave-uniform block indices: scalar address math; the lane parts
+  // (lk + 4 r) * 17 + li and li * 17 + 4 ks + lk are fixed per lane)
   auto tile_update = [&](int i0, int j0, int c0) {
+    const int bi = __builtin_amdgcn_readfirstlane(i0 >> 4);
+    const int bj = __builtin_amdgcn_readfirstlane(j0 >> 4);
+    const int bc = __builtin_amdgcn_readfirstlane(c0 >> 4);
+    double* C = Mb + (bi * (bi + 1) / 2 + bj) * (IB * (IB + 1));
+    const double* Pa = Mb + (bi * (bi + 1) / 2 + bc) * (IB * (IB + 1));
+    const double* Pb = Mb + (bj * (bj + 1) / 2 + bc) * (IB * (IB + 1));
     double4v acc;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) acc[r] = MS(i0 + lk + 4 * r, j0 + li);
+    for (int r = 0; r < 4; ++r) acc[r] = C[(lk + 4 * r) * (IB + 1) + li];
 #pragma unroll
     for (int ks = 0; ks < IB / 4; ++ks)
-      acc = mfma16(-MS(i0 + li, c0 + ks * 4 + lk), MS(j0 + li, c0 + ks * 4 + lk), acc);
+      acc = mfma16(-Pa[li * (IB + 1) + ks * 4 + lk], Pb[li * (IB + 1) + ks * 4 + lk], acc);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) MS(i0 + lk + 4 * r, j0 + li) = acc[r];
+    for (int r = 0; r < 4; ++r) C[(lk + 4 * r) * (IB + 1) + li] = acc[r];
+  };
+  // lower 16x16 tiles of a triangle of side nrb, enumerated row by row: tile t -> (row, column)
+  auto tri_tile = [](int t, int* ti, int* tj) {
+    int r = 0;
+    while ((r + 1) * (r + 2) / 2 <= t) ++r;
+    *ti = r;
+    *tj = t - r * (r + 1) / 2;
   };
   // With Li (the full inverse is wanted), waves 1-3 build it in the time the look-ahead leaves
   // them: Dinv_I (16x16 inverse of L_II, forward substitution, lane = column) and the blocks
@@ -317,17 +332,24 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
     }
   };
   auto linv_block = [&](int I, int J) {
+    I = __builtin_amdgcn_readfirstlane(I);  // wave-uniform block indices: scalar offsets
+    J = __builtin_amdgcn_readfirstlane(J);
+    auto blk = [&](int bi, int bj) { return (bi * (bi + 1) / 2 + bj) * (IB * (IB + 1)); };
     double4v sacc = {0, 0, 0, 0};
-    for (int K = J; K < I; ++K)
+    for (int K = J; K < I; ++K) {
+      const double* a = Mb + blk(I, K);
+      const double* b = Li + blk(K, J);
 #pragma unroll
       for (int ks = 0; ks < IB / 4; ++ks)
-        sacc = mfma16(MS(I * IB + li, K * IB + 4 * ks + lk), LI(K * IB + 4 * ks + lk, J * IB + li),
-                      sacc);
+        sacc = mfma16(a[li * (IB + 1) + 4 * ks + lk], b[(4 * ks + lk) * (IB + 1) + li], sacc);
+    }
+    const double* d = Li + blk(I, I);
     double4v o = {0, 0, 0, 0};
 #pragma unroll
-    for (int ks = 0; ks < IB / 4; ++ks) o = mfma16(LI(I * IB + li, I * IB + 4 * ks + lk), sacc[ks], o);
+    for (int ks = 0; ks < IB / 4; ++ks) o = mfma16(d[li * (IB + 1) + 4 * ks + lk], sacc[ks], o);
+    double* out = Li + blk(I, J);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) LI(I * IB + lk + 4 * r, J * IB + li) = -o[r];
+    for (int r = 0; r < 4; ++r) out[(lk + 4 * r) * (IB + 1) + li] = -o[r];
   };
   if ((PH & 1) && w == 0) leaf(0);
   __syncthreads();
@@ -367,15 +389,15 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
       if (PH & 1) leaf(ib + 1);
     } else if (PH & 4) {
       const int ntiles = nrb * (nrb + 1) / 2;
-      for (int t = w; t < ntiles; t += 6) {
+      const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform: scalar tile walk
+      for (int t = wu; t < ntiles; t += 6) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int tc = t + 3 * u;
           if (tc >= ntiles) break;
-          int ti = (int)((sqrtf(8.0f * tc + 1.0f) - 1.0f) * 0.5f);
-          while ((ti + 1) * (ti + 2) / 2 <= tc) ++ti;
-          while (ti * (ti + 1) / 2 > tc) --ti;
-          tile_update(c0 + IB + ti * IB, c0 + IB + (tc - ti * (ti + 1) / 2) * IB, c0);
+          int ti, tj;
+          tri_tile(tc, &ti, &tj);
+          tile_update(c0 + IB + ti * IB, c0 + IB + tj * IB, c0);
         }
       }
     }
