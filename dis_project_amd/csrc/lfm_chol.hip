@@ -318,13 +318,18 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
                     ((r) & 15) * (IB + 1) + ((q) & 15)]
   auto dinv_block = [&](int I) {
     const int c0 = I * IB;
+    const int bd = __builtin_amdgcn_readfirstlane(I);
+    const double* Ld = Mb + (bd * (bd + 1) / 2 + bd) * (IB * (IB + 1));
     double x[IB];
 #pragma unroll
-    for (int r = 0; r < IB; ++r) {
-      double sacc = (li == r) ? 1.0 : 0.0;
+    for (int r = 0; r < IB; ++r) x[r] = (li == r) ? 1.0 : 0.0;
+    // right-looking (the same terms in the same order per element as the left-looking sum,
+    // one dependent FMA + multiply per step instead of r)
 #pragma unroll
-      for (int q = 0; q < r; ++q) sacc = fma(-MS(c0 + r, c0 + q), x[q], sacc);
-      x[r] = sacc * ipv[c0 + r];
+    for (int r = 0; r < IB; ++r) {
+      x[r] = x[r] * ipv[c0 + r];
+#pragma unroll
+      for (int q = r + 1; q < IB; ++q) x[q] = fma(-Ld[q * (IB + 1) + r], x[r], x[q]);
     }
     if (lane < IB) {
 #pragma unroll
@@ -357,7 +362,10 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
 #pragma unroll 1
   for (int ib = 0; ib < NB / IB; ++ib) {
     const int c0 = ib * IB;
-    // (2) rows below: x_c = (p_c - sum_{q<c} x_q L[c][q]) / L_cc
+    // (2) rows below: x_c = (p_c - sum_{q<c} x_q L[c][q]) / L_cc, swept right-looking: once
+    // x_c is known it is subtracted from every later p_q at once. Each p_q still accumulates
+    // its terms in increasing c (bit-identical to the left-looking sum), but the dependent
+    // chain per column is one FMA and one multiply instead of c FMAs.
     const int nr = NB - c0 - IB;
     if ((PH & 2) && w * 64 < nr) {
       const bool act = tid < nr;
@@ -365,12 +373,13 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
       double p[IB];
 #pragma unroll
       for (int q = 0; q < IB; ++q) p[q] = MS(row, c0 + q);
+      const int bd = __builtin_amdgcn_readfirstlane(c0 >> 4);
+      const double* Ld = Mb + (bd * (bd + 1) / 2 + bd) * (IB * (IB + 1));  // L[c0.., c0..]
 #pragma unroll
       for (int c = 0; c < IB; ++c) {
-        double sacc = p[c];
+        p[c] = p[c] * ipv[c0 + c];
 #pragma unroll
-        for (int q = 0; q < c; ++q) sacc = fma(-p[q], MS(c0 + c, c0 + q), sacc);
-        p[c] = sacc * ipv[c0 + c];
+        for (int q = c + 1; q < IB; ++q) p[q] = fma(-p[c], Ld[q * (IB + 1) + c], p[q]);
       }
       if (act) {
 #pragma unroll
