@@ -126,6 +126,16 @@ __device__ __forceinline__ double row_bcast64(double v, int src) {
 // operations of a wave complete in order; the asm keeps the compiler from reordering.
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// Pins 16 register values at this point of the instruction stream (no instructions): the
+// updates before it are issued before the ones after it. Keeps a right-looking sweep
+// right-looking (the scheduler otherwise regroups the FMAs per element, a dependent chain of
+// c FMAs for element c).
+__device__ __forceinline__ void pin16(double (&p)[16]) {
+  asm volatile("" : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3]), "+v"(p[4]), "+v"(p[5]),
+               "+v"(p[6]), "+v"(p[7]), "+v"(p[8]), "+v"(p[9]), "+v"(p[10]), "+v"(p[11]),
+               "+v"(p[12]), "+v"(p[13]), "+v"(p[14]), "+v"(p[15]));
+}
+
 // ---------------------------------------------------------------- potrf
 // Two doubles; COH: device-coherent loads that bypass the CU's vector L1, which may hold stale
 // lines of data another CU wrote (write-through) in the same launch. LFM_COH_NT (default):
@@ -206,7 +216,15 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
   // pst (diagnostics, NULL: off): s_memrealtime after the load (0), panel iterations 0, 3, 6
   // (1-3), the loop (4), inverse block row 6 (5) and 7 (6), the block store (7)
   auto pstamp = [&](int p) {
+#ifndef LFM_PSTAMP_LEAF
     if (pst && threadIdx.x == 0) pst[p] = __builtin_amdgcn_s_memrealtime();
+#endif
+  };
+  // diagnostics build (-DLFM_PSTAMP_LEAF): panel iteration 3 by phase and wave instead
+  auto lstamp = [&](int ib, int p, int wv) {
+#ifdef LFM_PSTAMP_LEAF
+    if (pst && ib == 3 && threadIdx.x == 64 * wv) pst[p] = __builtin_amdgcn_s_memrealtime();
+#endif
   };
   __shared__ double pvs[NB];  // unscaled pivots
   __shared__ double ipv[NB];  // 1 / L_cc
@@ -316,6 +334,29 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
   // accumulator layout is the B-operand layout of the next product).
 #define LI(r, q) Li[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * (IB * (IB + 1)) + \
                     ((r) & 15) * (IB + 1) + ((q) & 15)]
+  // PH bit 9: p <- p L^-T (16 columns, right-looking), pinned column by column, column c + 1
+  // of L (and its 1 / L_cc) loaded while column c is applied (the pins are scheduling
+  // boundaries). Ld: the 16x16 block (row stride 17), y: 1 / L_cc.
+  auto sweep_pinned = [](double (&p)[IB], const double* Ld, const double* y) {
+    double lc[IB], ln[IB], yc = y[0], yn = 0.0;
+#pragma unroll
+    for (int q = 1; q < IB; ++q) lc[q] = Ld[q * (IB + 1)];
+#pragma unroll
+    for (int c = 0; c < IB; ++c) {
+      if (c + 1 < IB) {
+        yn = y[c + 1];
+#pragma unroll
+        for (int q = c + 2; q < IB; ++q) ln[q] = Ld[q * (IB + 1) + c + 1];
+      }
+      p[c] = p[c] * yc;
+#pragma unroll
+      for (int q = c + 1; q < IB; ++q) p[q] = fma(-p[c], lc[q], p[q]);
+      pin16(p);
+      yc = yn;
+#pragma unroll
+      for (int q = c + 2; q < IB; ++q) lc[q] = ln[q];
+    }
+  };
   auto dinv_block = [&](int I) {
     const int c0 = I * IB;
     const int bd = __builtin_amdgcn_readfirstlane(I);
@@ -325,11 +366,15 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
     for (int r = 0; r < IB; ++r) x[r] = (li == r) ? 1.0 : 0.0;
     // right-looking (the same terms in the same order per element as the left-looking sum,
     // one dependent FMA + multiply per step instead of r)
+    if constexpr ((PH & 512) != 0) {
+      sweep_pinned(x, Ld, ipv + c0);
+    } else {
 #pragma unroll
-    for (int r = 0; r < IB; ++r) {
-      x[r] = x[r] * ipv[c0 + r];
+      for (int r = 0; r < IB; ++r) {
+        x[r] = x[r] * ipv[c0 + r];
 #pragma unroll
-      for (int q = r + 1; q < IB; ++q) x[q] = fma(-Ld[q * (IB + 1) + r], x[r], x[q]);
+        for (int q = r + 1; q < IB; ++q) x[q] = fma(-Ld[q * (IB + 1) + r], x[r], x[q]);
+      }
     }
     if (lane < IB) {
 #pragma unroll
@@ -362,6 +407,7 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
 #pragma unroll 1
   for (int ib = 0; ib < NB / IB; ++ib) {
     const int c0 = ib * IB;
+    lstamp(ib, 0, 0);
     // (2) rows below: x_c = (p_c - sum_{q<c} x_q L[c][q]) / L_cc, swept right-looking: once
     // x_c is known it is subtracted from every later p_q at once. Each p_q still accumulates
     // its terms in increasing c (bit-identical to the left-looking sum), but the dependent
@@ -375,18 +421,24 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
       for (int q = 0; q < IB; ++q) p[q] = MS(row, c0 + q);
       const int bd = __builtin_amdgcn_readfirstlane(c0 >> 4);
       const double* Ld = Mb + (bd * (bd + 1) / 2 + bd) * (IB * (IB + 1));  // L[c0.., c0..]
+      if constexpr ((PH & 512) != 0) {
+        sweep_pinned(p, Ld, ipv + c0);
+      } else {
 #pragma unroll
-      for (int c = 0; c < IB; ++c) {
-        p[c] = p[c] * ipv[c0 + c];
+        for (int c = 0; c < IB; ++c) {
+          p[c] = p[c] * ipv[c0 + c];
 #pragma unroll
-        for (int q = c + 1; q < IB; ++q) p[q] = fma(-p[c], Ld[q * (IB + 1) + c], p[q]);
+          for (int q = c + 1; q < IB; ++q) p[q] = fma(-p[c], Ld[q * (IB + 1) + c], p[q]);
+        }
       }
       if (act) {
 #pragma unroll
         for (int q = 0; q < IB; ++q) MS(row, c0 + q) = p[q];
       }
     }
+    lstamp(ib, 1, 0);
     __syncthreads();
+    lstamp(ib, 2, 0);
     if (nr == 0) break;
     // (3) wave 0: next diagonal block, then its leaf; waves 1-3: the other trailing tiles
     const int nrb = nr / IB;
@@ -395,7 +447,9 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
         tile_update(c0 + IB, c0 + IB, c0);
         wave_lds_fence();
       }
+      lstamp(ib, 3, 0);
       if (PH & 1) leaf(ib + 1);
+      lstamp(ib, 4, 0);
     } else if (PH & 4) {
       const int ntiles = nrb * (nrb + 1) / 2;
       const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform: scalar tile walk
@@ -416,7 +470,10 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
       else
         for (int J = w - 2; J < ib - 1; J += 2) linv_block(ib - 1, J);
     }
+    lstamp(ib, 5, 1);
+    lstamp(ib, 6, 3);
     __syncthreads();
+    lstamp(ib, 7, 0);
     if (ib == 0 || ib == 3 || ib == 6) pstamp(ib == 0 ? 1 : ib == 3 ? 2 : 3);
   }
   pstamp(4);
@@ -1416,7 +1473,7 @@ __device__ __forceinline__ void gemm32(const double* __restrict__ pi, int64_t ld
 // LIGHT (w = 1 with both small-tile phases): every value one workgroup hands to another is
 // stored write-through and loaded device-coherently, so the barriers, the input wait and the
 // completion flag need no cache maintenance (an agent-scope fence costs ~1.7-3.5 us).
-template <bool LIGHT>
+template <bool LIGHT, int XPH>
 __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   double (*sP)[CKS + 1] = reinterpret_cast<double (*)[CKS + 1]>(smem);
@@ -1547,7 +1604,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     // the only block (w = 1: Bd = L11^{-T}), else into linv for the panel solve below
     if (wg == 0) {
       double* Li = smem + MB_DOUBLES;
-      potrf_block<(LIGHT ? 127 : 47) | 128>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB),
+      potrf_block<(LIGHT ? 127 : 47) | 128 | XPH>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB),
                                    g.status, Li, g.stamps && g.w == 1 ? g.stamps + 5 : nullptr);
       stamp(3 + 3 * c);
       store_inverse_t<LIGHT>(Li, g.w == 1 ? g.Wk + (int64_t)W * W : g.linv, g.w == 1 ? W : NB);
@@ -2104,8 +2161,10 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     hipFuncSetAttribute(reinterpret_cast<const void*>(&potrf_diag_kernel<15>),
                         hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)(MB_DOUBLES * sizeof(double)));
-    const void* chains[2] = {reinterpret_cast<const void*>(&chain_kernel<false>),
-                             reinterpret_cast<const void*>(&chain_kernel<true>)};
+    const void* chains[4] = {reinterpret_cast<const void*>(&chain_kernel<false, 0>),
+                             reinterpret_cast<const void*>(&chain_kernel<true, 0>),
+                             reinterpret_cast<const void*>(&chain_kernel<false, 512>),
+                             reinterpret_cast<const void*>(&chain_kernel<true, 512>)};
     for (const void* f : chains)
       hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS);
     attr = true;
@@ -2215,6 +2274,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     const int chain_small4 = env_int("LFM_CHAIN_SMALL4", 7);  // bit 2: in-chain solve / band
     // w = 1 chains with both small phases: fence-free hand-offs (chain_kernel<true>)
     const bool chain_light = env_int("LFM_CHAIN_LIGHT", 1) != 0;
+    // the diagonal factor's panel solve pinned column by column (potrf_block PH bit 9)
+    const bool solve_pin = env_int("LFM_SOLVE_PIN", 1) != 0;
     // chain(s): factor block s on the side stream's CUs (one launch, see chain_kernel)
     auto chain = [&](int s, bool dev_wait = true) {
       ChainArgs c{};
@@ -2246,7 +2307,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       hipEvent_t pe;
       prof_begin(ctx, K_POTRF, &pe, side);
       const bool light = c.w == 1 && (c.small & 3) == 3 && chain_light;
-      auto kern = light ? chain_kernel<true> : chain_kernel<false>;
+      auto kern = light ? (solve_pin ? chain_kernel<true, 512> : chain_kernel<true, 0>)
+                        : (solve_pin ? chain_kernel<false, 512> : chain_kernel<false, 0>);
       hipLaunchKernelGGL(kern, dim3((unsigned)ctx->side_cus), dim3(256), CHAIN_LDS, side, c);
       const double W = c.w * NB;
       prof_end(ctx, K_POTRF, pe, W * W * W / 3.0 + W * W * W, 0, side);
