@@ -167,6 +167,16 @@ __device__ __forceinline__ void st1(double* p, double v) {
   if (COH) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   else *p = v;
 }
+// Two doubles at base + off (bytes, 16-B aligned) in one 16-B write-through (sc1) vector store:
+// the wide form of st1<true> (an 8-B sc1 store is one fabric write, ≈2.7x the 16-B time per
+// byte, MI355X_MICROARCH.md). base must be wave-uniform (a kernel argument or derived from one):
+// it becomes the buffer resource.
+typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st2_wt(double* base, unsigned off, double a, double b) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
+  const double2v v = {a, b};
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), r, off, 0, 16 /* sc1 */);
+}
 template <bool COH>
 __device__ __forceinline__ double ld1(const double* p) {
   if (COH) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -565,8 +575,7 @@ __device__ __forceinline__ void store_inverse_t(const double* __restrict__ Li,
     v.x = j >= k ? LI(j, k) : 0.0;
     v.y = j + 1 >= k ? LI(j + 1, k) : 0.0;
     if (COH) {
-      st1<true>(&out[k * ldo + j], v.x);
-      st1<true>(&out[k * ldo + j + 1], v.y);
+      st2_wt(out, (unsigned)((k * ldo + j) * 8), v.x, v.y);
     } else {
       *reinterpret_cast<double2*>(&out[k * ldo + j]) = v;
     }
@@ -1398,7 +1407,7 @@ static_assert(2 * MB_DOUBLES >= (64 + ST) * (CKS + 1), "chain LDS union");
 constexpr int G32K = 129;  // LDS row stride of a 128-deep operand row
 static_assert(2 * MB_DOUBLES >= 2 * 32 * G32K + 4 * 1024 && 2 * MB_DOUBLES >= 4 * 32 * 33,
               "gemm32 LDS (+ the in-chain solve's parked output tiles)");
-template <bool BT, bool COH = false>
+template <bool BT, bool COH = false, bool PAIR = false>
 __device__ __forceinline__ void gemm32(const double* __restrict__ pi, int64_t ldi,
                                        const double* __restrict__ pj, int64_t ldj, int kd,
                                        double (&v)[4], double* __restrict__ smem) {
@@ -1464,7 +1473,8 @@ __device__ __forceinline__ void gemm32(const double* __restrict__ pi, int64_t ld
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    const int e = tid + 256 * q, r = e >> 5, c = e & 31;
+    // PAIR: v[2h], v[2h + 1] = elements e, e + 1 with e = 2 tid + 512 h (one 16-B store each)
+    const int e = PAIR ? 2 * tid + 512 * (q >> 1) + (q & 1) : tid + 256 * q, r = e >> 5, c = e & 31;
     v[q] = red[r * 33 + c] + red[(32 + r) * 33 + c] + red[(64 + r) * 33 + c] +
            red[(96 + r) * 33 + c];
   }
@@ -1506,12 +1516,22 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
       const int cb = u % nc, rb = u / nc;
       const int kd = min(g.kd, (32 * (cb + 1) + 127) / 128 * 128);
       double v[4];
-      gemm32<true, LIGHT>(g.A + (g.Kc + 32 * rb) * g.lda + g.K0p, g.lda, g.Bdp + 32 * cb, g.kd,
-                          kd, v, smem);
+      gemm32<true, LIGHT, LIGHT>(g.A + (g.Kc + 32 * rb) * g.lda + g.K0p, g.lda, g.Bdp + 32 * cb,
+                                 g.kd, kd, v, smem);
+      if (LIGHT) {
+        // element pairs, one 16-B write-through store each
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int e = tid + 256 * q;
-        st1<LIGHT>(&g.xd[(int64_t)(32 * rb + (e >> 5)) * g.kd + 32 * cb + (e & 31)], v[q]);
+        for (int h = 0; h < 2; ++h) {
+          const int e = 2 * tid + 512 * h;
+          st2_wt(g.xd, (unsigned)(((32 * rb + (e >> 5)) * g.kd + 32 * cb + (e & 31)) * 8), v[2 * h],
+                 v[2 * h + 1]);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int e = tid + 256 * q;
+          g.xd[(int64_t)(32 * rb + (e >> 5)) * g.kd + 32 * cb + (e & 31)] = v[q];
+        }
       }
     }
     if (!(LIGHT ? grid_sync_light : grid_sync)(g.bar, G * ++nbar, g.status)) return;
@@ -1552,13 +1572,24 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
         const int tj = u - ti * (ti + 1) / 2;
         double v[4] = {0.0, 0.0, 0.0, 0.0};
         if (g.kd > 0)
-          gemm32<false, LIGHT>(g.xd + (int64_t)32 * ti * g.kd, g.kd, g.xd + (int64_t)32 * tj * g.kd,
-                               g.kd, g.kd, v, smem);
+          gemm32<false, LIGHT, LIGHT>(g.xd + (int64_t)32 * ti * g.kd, g.kd,
+                                      g.xd + (int64_t)32 * tj * g.kd, g.kd, g.kd, v, smem);
+        if (LIGHT) {
+          // element pairs: one 16-B device-coherent load and one 16-B write-through store each
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int e = tid + 256 * q;
-          const int64_t i = g.Kc + 32 * ti + (e >> 5), j = g.Kc + 32 * tj + (e & 31);
-          st1<LIGHT>(&Aw[i * W + j], ld1<LIGHT>(&g.A[i * g.lda + j]) - v[q]);
+          for (int h = 0; h < 2; ++h) {
+            const int e = 2 * tid + 512 * h;
+            const int il = 32 * ti + (e >> 5), jl = 32 * tj + (e & 31);
+            const double2 a = ld2<true>(&g.A[(g.Kc + il) * g.lda + g.Kc + jl]);
+            st2_wt(g.Wk, (unsigned)((il * W + jl) * 8), a.x - v[2 * h], a.y - v[2 * h + 1]);
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q;
+            const int64_t i = g.Kc + 32 * ti + (e >> 5), j = g.Kc + 32 * tj + (e & 31);
+            Aw[i * W + j] = g.A[i * g.lda + j] - v[q];
+          }
         }
       }
     }
