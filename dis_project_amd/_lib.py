@@ -29,6 +29,8 @@ LFM_E_NOT_PD = 3
 LFM_E_OOM = 4
 LFM_E_RCCL = 5
 LFM_E_STATE = 6
+LFM_E_TIMEOUT = 7
+ABI_VERSION = 2
 
 LFM_UPLO_FULL = 0
 LFM_UPLO_LOWER = 1
@@ -40,6 +42,7 @@ _ERR_NAMES = {
     LFM_E_OOM: "LFM_E_OOM",
     LFM_E_RCCL: "LFM_E_RCCL",
     LFM_E_STATE: "LFM_E_STATE",
+    LFM_E_TIMEOUT: "LFM_E_TIMEOUT",
 }
 
 _dptr = POINTER(c_double)
@@ -76,12 +79,13 @@ class LfmKstat(ctypes.Structure):
         ("total_ms", c_double),
         ("flops", c_double),
         ("bytes", c_double),
+        ("issued_flops", c_double),
     ]
 
 
 # (name, restype, argtypes) — every entry point of include/lfm.h
 _c_ctx = c_void_p
-SIGNATURES = [
+PRODUCT_SIGNATURES = [
     ("lfm_abi_version", c_int, []),
     ("lfm_device_count", c_int, [POINTER(c_int)]),
     ("lfm_ctx_create", c_int, [c_int, POINTER(c_void_p)]),
@@ -111,6 +115,7 @@ SIGNATURES = [
     ("lfm_dev_free", c_int, [_c_ctx, c_void_p]),
     ("lfm_memcpy_h2d", c_int, [_c_ctx, c_void_p, c_void_p, c_size_t]),
     ("lfm_memcpy_d2h", c_int, [_c_ctx, c_void_p, c_void_p, c_size_t]),
+    ("lfm_memset_dev", c_int, [_c_ctx, c_void_p, c_int, c_size_t]),
     ("lfm_mll_f64_dev", c_int, [_c_ctx, c_void_p, c_void_p, c_int64, POINTER(LfmHyp), c_int, _dptr]),
     ("lfm_data_create", c_int, [_c_ctx, c_void_p, c_void_p, c_int64, POINTER(c_void_p)]),
     ("lfm_data_destroy", c_int, [c_void_p]),
@@ -123,21 +128,25 @@ SIGNATURES = [
     ("lfm_profile_classes", c_int, [_c_ctx, ctypes.c_uint]),
     ("lfm_profile_reset", c_int, [_c_ctx]),
     ("lfm_profile_read", c_int, [_c_ctx, POINTER(LfmKstat), c_int, POINTER(c_int)]),
-    ("lfm_debug_stamps", c_int, [_c_ctx, c_int, POINTER(ctypes.c_ulonglong), c_int]),
-    ("lfm_probe_rsq", c_int, [_c_ctx, c_void_p, c_int64, c_void_p]),
     ("lfm_farm_unique_id", c_int, [_c_ctx, POINTER(ctypes.c_ubyte)]),
     ("lfm_farm_init", c_int, [_c_ctx, POINTER(ctypes.c_ubyte), c_int, c_int]),
     ("lfm_farm_allgather_f64", c_int, [_c_ctx, _dptr, c_int64, _dptr]),
     ("lfm_farm_destroy", c_int, [_c_ctx]),
-    ("lfm_probe_mfma_f64", c_int, [_c_ctx, c_int, c_int, _dptr, _dptr]),
-    ("lfm_probe_mfma_f64_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr]),
-    ("lfm_probe_potrf", c_int, [_c_ctx, c_int, c_int, _dptr]),
-    ("lfm_probe_trsm", c_int, [_c_ctx, c_int, c_int, c_int, _dptr]),
-    ("lfm_probe_syrk", c_int, [_c_ctx, c_int, c_int, c_int, c_int, _dptr]),
-    ("lfm_probe_rate", c_int, [_c_ctx, c_int, c_int, c_int, _dptr]),
-    ("lfm_probe_mfma4_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr, _dptr]),
-    ("lfm_probe_mfma_f64_cycles", c_int, [_c_ctx, c_int, c_int, _dptr, _dptr]),
 ]
+
+# include/lfm_diag.h: probes and phase stamps (measurement / known-answer tests only)
+DIAG_SIGNATURES = [
+    ("lfm_debug_stamps", c_int, [_c_ctx, c_int, POINTER(ctypes.c_ulonglong), c_int]),
+    ("lfm_probe_rsq", c_int, [_c_ctx, c_void_p, c_int64, c_void_p]),
+    ("lfm_probe_mfma_f64_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr]),
+    ("lfm_probe_mfma4_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr, _dptr]),
+    ("lfm_probe_mfma_f64", c_int, [_c_ctx, c_int, c_int, _dptr, _dptr]),
+    ("lfm_probe_mfma_f64_cycles", c_int, [_c_ctx, c_int, c_int, _dptr, _dptr]),
+    ("lfm_probe_rate", c_int, [_c_ctx, c_int, c_int, c_int, _dptr]),
+    ("lfm_probe_syrk", c_int, [_c_ctx, c_int, c_int, c_int, c_int, _dptr]),
+]
+
+SIGNATURES = PRODUCT_SIGNATURES + DIAG_SIGNATURES
 
 # kernel classes in lfm_profile_read order (lfm_internal.h KClass)
 KCLASSES = ["tables", "gram_grid", "gram_direct", "augment", "potrf", "trsm", "syrk",
@@ -165,7 +174,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.lfm_abi_version() != 1:
+        if lib.lfm_abi_version() != ABI_VERSION:
             raise LfmError(LFM_E_STATE, "liblfm ABI version mismatch")
         if path is None:
             _lib = lib
@@ -219,6 +228,9 @@ class Context:
 
     # -- error plumbing
     def check(self, rc: int, allow_not_pd: bool = False) -> int:
+        """Raise LfmError unless rc is LFM_OK (or LFM_E_NOT_PD with allow_not_pd: JAX's NaN
+        on a failed Cholesky). LFM_E_TIMEOUT always raises: a stalled device-side hand-off is
+        not a property of the input and must never read as a NaN likelihood."""
         if rc == LFM_OK or (allow_not_pd and rc == LFM_E_NOT_PD):
             return rc
         msg = self.lib.lfm_last_error(self.handle)
@@ -258,11 +270,14 @@ class Context:
         for i in range(min(cnt.value, 32)):
             s = arr[i]
             out[s.name.decode()] = dict(launches=s.launches, total_ms=s.total_ms,
-                                        flops=s.flops, bytes=s.bytes)
+                                        flops=s.flops, bytes=s.bytes,
+                                        issued_flops=s.issued_flops)
         return out
 
 
-_contexts: dict[int, Context] = {}
+# one context per (host thread, device): a context's workspace, pinned buffer and streams are
+# not thread-safe (include/lfm.h), so threads never share one
+_tls = threading.local()
 
 
 def default_device() -> int:
@@ -274,11 +289,15 @@ def default_device() -> int:
 
 
 def get_context(device: int | None = None) -> Context:
+    """The calling thread's context on `device` (created on first use)."""
     dev = default_device() if device is None else int(device)
-    ctx = _contexts.get(dev)
+    cache = getattr(_tls, "contexts", None)
+    if cache is None:
+        cache = _tls.contexts = {}
+    ctx = cache.get(dev)
     if ctx is None:
         ctx = Context(dev)
-        _contexts[dev] = ctx
+        cache[dev] = ctx
     return ctx
 
 

@@ -29,6 +29,17 @@ int set_err(lfm_ctx* ctx, int code, const std::string& msg) {
   return code;
 }
 
+int status_code(lfm_ctx* ctx, double st) {
+  const long long v = (long long)st;
+  if (v == INT_MAX) return LFM_OK;
+  if (v == STATUS_TIMEOUT)
+    return set_err(ctx, LFM_E_TIMEOUT,
+                   "device-side wait timed out (a cross-stream hand-off of the factorisation "
+                   "stalled): the result is invalid, not a property of the input");
+  return set_err(ctx, LFM_E_NOT_PD,
+                 "Cholesky failed: non-positive pivot at index " + std::to_string(v));
+}
+
 int hip_fail(lfm_ctx* ctx, hipError_t e, const char* what) {
   if (e == hipSuccess) return LFM_OK;
   const int code = (e == hipErrorOutOfMemory) ? LFM_E_OOM : LFM_E_HIP;
@@ -93,7 +104,8 @@ void prof_begin(lfm_ctx* ctx, int cls, hipEvent_t* a, hipStream_t st) {
   hipEventRecord(*a, st);
 }
 
-void prof_end(lfm_ctx* ctx, int cls, hipEvent_t a, double flops, double bytes, hipStream_t st) {
+void prof_end(lfm_ctx* ctx, int cls, hipEvent_t a, double flops, double bytes, hipStream_t st,
+              double issued) {
   if (!ctx->prof || !a) return;
   if (!st) st = ctx->stream;
   if (ctx->pool.empty()) {
@@ -104,7 +116,7 @@ void prof_end(lfm_ctx* ctx, int cls, hipEvent_t a, double flops, double bytes, h
   hipEvent_t b = ctx->pool.back();
   ctx->pool.pop_back();
   hipEventRecord(b, st);
-  ctx->pending.push_back(ProfEvent{cls, a, b, flops, bytes});
+  ctx->pending.push_back(ProfEvent{cls, a, b, flops, bytes, issued < 0 ? flops : issued});
 }
 
 int prof_flush(lfm_ctx* ctx) {
@@ -116,6 +128,7 @@ int prof_flush(lfm_ctx* ctx) {
     s.total_ms += ms;
     s.flops += p.flops;
     s.bytes += p.bytes;
+    s.issued_flops += p.issued;
     ctx->pool.push_back(p.a);
     ctx->pool.push_back(p.b);
   }
@@ -258,14 +271,9 @@ int mll_blocked(lfm_ctx* ctx, const Staged& st, const double* d_x, const double*
   r = finish(ctx);
   if (r) return r;
   *out = hres[0];
-  if ((int)hres[3] != INT_MAX) {
-    const double nan = std::nan("");
-    *out = nan;
-    return set_err(ctx, LFM_E_NOT_PD,
-                   "Cholesky failed: non-positive pivot at index " +
-                       std::to_string((long long)hres[3]));
-  }
-  return LFM_OK;
+  r = status_code(ctx, hres[3]);
+  if (r) *out = std::nan("");
+  return r;
 }
 
 int validate_x(lfm_ctx* ctx, const void* x, int64_t n) {
@@ -425,32 +433,19 @@ int env_int_api(const char* name, int def) {
 }
 // Main + high-priority side stream (every CU), and for schedule 3 a CU-partitioned pair:
 // LFM_SIDE_CUS (default 32) CUs for the factor chain, the rest for the bulk
-// (hipExtStreamCreateWithCUMask). LFM_LOOKAHEAD=0 serialises on one stream.
+// (hipExtStreamCreateWithCUMask). The documented knobs read here:
+//   LFM_SCHED            3 (default) or 1: the look-ahead schedule of the MLL factorisation
+//   LFM_SIDE_CUS         CUs reserved for the schedule-3 factor chain (0: schedule 1 only)
+//   LFM_S3_EVENTS        1: schedule 3 ordered by stream events (for rocprofv3 --pmc)
+//   LFM_DEBUG_SPIN_LIMIT poll bound of every device-side wait (tests force timeouts with 0)
 hipError_t create_streams(lfm_ctx* ctx) {
-  const char* pk = std::getenv("LFM_SYRK_PAD_KB");
-  ctx->syrk_pad_kb = pk ? std::atoi(pk) : 0;
-  const char* xr = std::getenv("LFM_XCD_REMAP");
-  ctx->xcd_remap = xr ? std::atoi(xr) : 1;
-  const char* bp = std::getenv("LFM_BAND_PRIO");
-  ctx->prio_mask = bp ? std::atoi(bp) : 1;
-  const char* sv = std::getenv("LFM_SCHED");
-  ctx->sched = sv ? std::atoi(sv) : 3;
-  const char* fv = std::getenv("LFM_FUSED");
-  ctx->fused = fv ? std::atoi(fv) : 1;
-  const char* trv = std::getenv("LFM_SYRK_TR");
-  // LFM_SYRK_TR: 64 / 128 force the triangle's row height, -1 = choose by round count
-  ctx->syrk_tr = trv ? std::atoi(trv) : 0;
-  if (ctx->syrk_tr != 64 && ctx->syrk_tr != 128 && ctx->syrk_tr != -1) ctx->syrk_tr = 0;
-  const char* scv = std::getenv("LFM_SLAB_COST");
-  if (scv) ctx->slab_cost = std::atof(scv);
-  const char* tv = std::getenv("LFM_TRSM");
-  if (tv) ctx->trsm_variant = std::atoi(tv);
-  const char* la = std::getenv("LFM_LOOKAHEAD");
-  ctx->lookahead = !(la && std::atoi(la) == 0);
+  ctx->sched = env_int_api("LFM_SCHED", 3) == 1 ? 1 : 3;
+  ctx->s3_events = env_int_api("LFM_S3_EVENTS", 0) != 0;
+  if (const char* sl = std::getenv("LFM_DEBUG_SPIN_LIMIT"))
+    ctx->spin_limit = (unsigned)std::strtoul(sl, nullptr, 10);
   int least = 0, greatest = 0;
   hipDeviceGetStreamPriorityRange(&least, &greatest);
-  const char* sc = std::getenv("LFM_SIDE_CUS");
-  const int side_cus = sc ? std::atoi(sc) : 32;
+  const int side_cus = env_int_api("LFM_SIDE_CUS", 32);
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, ctx->device);
   const int ncu = prop.multiProcessorCount;
@@ -458,39 +453,20 @@ hipError_t create_streams(lfm_ctx* ctx) {
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e == hipSuccess) e = hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest);
   if (e != hipSuccess || side_cus <= 0 || side_cus >= ncu) return e;
-  // Schedule 3 stream pair: side CUs j * stride (mod ncu), j < side_cus, for the factor chain
-  // (LFM_SIDE_STRIDE = 1: consecutive mask bits, which the hardware spreads over the XCDs),
-  // every other CU for the main (bulk) stream. The chain kernel needs all of its workgroups
-  // (one per CU) resident at once: checked here, halving the reservation until it holds.
-  const char* sst = std::getenv("LFM_SIDE_STRIDE");
-  const int stride = sst ? std::max(1, std::atoi(sst)) : 1;
-  // two contexts evaluating concurrently on one GPU (scripts/c3_pipe.py): LFM_SIDE_FIRST = the
-  // first side CU bit, LFM_MAIN_SKIP = CU bits [0, skip) kept off the main stream as well (the
-  // other context's chain CUs)
-  const int side_first = std::max(0, env_int_api("LFM_SIDE_FIRST", 0)) % std::max(1, ncu);
-  const int main_skip = std::max(0, env_int_api("LFM_MAIN_SKIP", 0));
+  // Schedule 3 stream pair: CU mask bits [0, cus) for the factor chain (consecutive bits,
+  // which the hardware spreads over the XCDs: bit c lives on XCD c % 8), every other CU for the
+  // main (bulk) stream. The chain kernel needs all of its workgroups (one per CU) resident at
+  // once: checked here, halving the reservation until it holds.
   for (int cus = side_cus; cus >= 4; cus /= 2) {
-    std::vector<char> is_side(ncu, 0);
-    for (int j = 0, c = side_first; j < cus; ++j) {
-      while (is_side[c]) c = (c + 1) % ncu;
-      is_side[c] = 1;
-      c = (c + stride) % ncu;
-    }
-    // mask bit c lives on XCD c % 8 (observed: LFM_SIDE_STRIDE=8 puts every side CU on one XCD
-    // and the main stream's workgroups dealt to that XCD never run). Every XCD keeps the same
-    // number of main CUs, or the partition is refused.
-    {
-      std::vector<int> per_xcd(8, 0);
-      for (int c = 0; c < ncu; ++c) per_xcd[c % 8] += (is_side[c] || c < main_skip) ? 0 : 1;
-      if (*std::min_element(per_xcd.begin(), per_xcd.end()) !=
-          *std::max_element(per_xcd.begin(), per_xcd.end()))
-        continue;
-    }
+    // every XCD keeps the same number of main CUs, or the partition is refused (measured:
+    // an XCD left without main CUs never ran the main launch's workgroups dealt to it)
+    std::vector<int> per_xcd(8, 0);
+    for (int c = cus; c < ncu; ++c) per_xcd[c % 8] += 1;
+    if (*std::min_element(per_xcd.begin(), per_xcd.end()) !=
+        *std::max_element(per_xcd.begin(), per_xcd.end()))
+      continue;
     std::vector<uint32_t> mside((ncu + 31) / 32, 0u), mmain((ncu + 31) / 32, 0u);
-    for (int c = 0; c < ncu; ++c) {
-      if (is_side[c]) mside[c / 32] |= 1u << (c % 32);
-      else if (c >= main_skip) mmain[c / 32] |= 1u << (c % 32);
-    }
+    for (int c = 0; c < ncu; ++c) (c < cus ? mside : mmain)[c / 32] |= 1u << (c % 32);
     e = hipExtStreamCreateWithCUMask(&ctx->m3, (uint32_t)mmain.size(), mmain.data());
     if (e == hipSuccess)
       e = hipExtStreamCreateWithCUMask(&ctx->s3, (uint32_t)mside.size(), mside.data());
@@ -774,11 +750,12 @@ int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
   if (r) return r;
   *value = hres[0];
   std::memcpy(grad, hres + 8, ng * sizeof(double));
-  if ((int)hres[3] != INT_MAX)
-    return set_err(ctx, LFM_E_NOT_PD,
-                   "Cholesky failed: non-positive pivot at index " +
-                       std::to_string((long long)hres[3]));
-  return LFM_OK;
+  r = status_code(ctx, hres[3]);
+  if (r) {
+    *value = std::nan("");
+    for (size_t i = 0; i < ng; ++i) grad[i] = std::nan("");
+  }
+  return r;
 }
 
 int lfm_posterior_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
@@ -825,15 +802,13 @@ int lfm_posterior_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
   hipMemcpyAsync(cov, d_cov, (size_t)m * m * 8, hipMemcpyDeviceToHost, ctx->stream);
   r = finish(ctx);
   if (r) return r;
-  if ((int)hres[3] != INT_MAX) {
+  r = status_code(ctx, hres[3]);
+  if (r) {
     const double nan = std::nan("");
     for (int64_t i = 0; i < m; ++i) mean[i] = nan;
     for (int64_t i = 0; i < m * m; ++i) cov[i] = nan;
-    return set_err(ctx, LFM_E_NOT_PD,
-                   "Cholesky failed: non-positive pivot at index " +
-                       std::to_string((long long)hres[3]));
   }
-  return LFM_OK;
+  return r;
 }
 
 int lfm_mll_f64_dev(lfm_ctx* ctx, const double* d_x, const double* d_y, int64_t n,
@@ -950,7 +925,7 @@ int lfm_mll_batch_f64(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, int
   for (int64_t q : big) {
     int r = lfm_mll_f64(ctx, probs[q].x, probs[q].y, probs[q].n, &probs[q].hyp, negative, &out[q]);
     if (status) status[q] = r;
-    if (r && r != LFM_E_NOT_PD) return r;
+    if (r && r != LFM_E_NOT_PD) return r;  // LFM_E_TIMEOUT included: never a NaN slot
   }
   if (status)
     for (int64_t q = 0; q < nprob; ++q)
@@ -986,13 +961,9 @@ int lfm_log_prob_f64(lfm_ctx* ctx, const double* loc, const double* scale, int64
   r = finish(ctx);
   if (r) return r;
   *out = hres[0];
-  if ((int)hres[3] != INT_MAX) {
-    *out = std::nan("");
-    return set_err(ctx, LFM_E_NOT_PD,
-                   "Cholesky failed: non-positive pivot at index " +
-                       std::to_string((long long)hres[3]));
-  }
-  return LFM_OK;
+  r = status_code(ctx, hres[3]);
+  if (r) *out = std::nan("");
+  return r;
 }
 
 int lfm_dev_alloc(lfm_ctx* ctx, size_t bytes, void** out) {
@@ -1025,6 +996,14 @@ int lfm_memcpy_d2h(lfm_ctx* ctx, void* dst, const void* src, size_t bytes) {
   return finish(ctx);
 }
 
+int lfm_memset_dev(lfm_ctx* ctx, void* dst, int value, size_t bytes) {
+  if (!ctx || (!dst && bytes)) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  hipError_t e = hipMemsetAsync(dst, value, bytes, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "memset");
+  return finish(ctx);
+}
+
 int lfm_profile_enable(lfm_ctx* ctx, int on) {
   if (!ctx) return LFM_E_ARG;
   ctx->prof = on != 0;
@@ -1047,6 +1026,7 @@ int lfm_profile_reset(lfm_ctx* ctx) {
     ctx->stats[i].total_ms = 0;
     ctx->stats[i].flops = 0;
     ctx->stats[i].bytes = 0;
+    ctx->stats[i].issued_flops = 0;
   }
   return LFM_OK;
 }
@@ -1214,18 +1194,6 @@ int lfm_probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   if (!ctx || !us || T < 1 || reps < 1 || kd < 16 || kd > 2048 || kd % 16) return LFM_E_ARG;
   DeviceGuard g(ctx->device);
   return probe_syrk(ctx, T, kd, cio, reps, us);
-}
-
-int lfm_probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us) {
-  if (!ctx || !us || rows < 64 || rows % 64 || reps < 1) return LFM_E_ARG;
-  DeviceGuard g(ctx->device);
-  return probe_trsm(ctx, variant, rows, reps, us);
-}
-
-int lfm_probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us) {
-  if (!ctx || !us || reps < 1) return LFM_E_ARG;
-  DeviceGuard g(ctx->device);
-  return probe_potrf(ctx, mask, reps, us);
 }
 
 int lfm_probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d) {

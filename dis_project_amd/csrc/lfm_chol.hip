@@ -43,7 +43,7 @@ static constexpr int IB = 16;        // inner block of the diagonal factor / pan
 static constexpr int ST = 128;       // SYRK output tile edge
 static constexpr int KB = 16;        // SYRK K-step staged through LDS
 static constexpr int STATUS_NONE = INT_MAX;
-constexpr int PANEL_TIMEOUT = -2;  // status: a bounded device-side wait ran out
+constexpr int PANEL_TIMEOUT = STATUS_TIMEOUT;  // status: a bounded device-side wait ran out
 
 __device__ __forceinline__ double4v mfma16(double a, double b, double4v c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -206,8 +206,8 @@ __device__ __forceinline__ double rsqrt_nr(double x) {
 //  (3) the rank-16 update of the trailing lower triangle on fp64 MFMA.
 // After the loop the eight 16x16 diagonal inverses (dinv, for trsm_kernel) are built by
 // the four waves, and logdet / the first failing pivot are reduced.
-// PH (diagnostics only, lfm_probe_potrf): bit 0 = phase 1, bit 1 = phase 2, bit 2 = phase 3,
-// bit 3 = global load / store of the block. The product path always runs PH = 15, in the
+// PH: bit 0 = phase 1, bit 1 = phase 2, bit 2 = phase 3, bit 3 = global load / store of
+// the block. The product path always runs PH = 15, in the
 // chain kernel with bit 5 (the block load in one batch) and bit 7 (64-bit DPP broadcasts in
 // the leaf), in its light mode also bit 4 (device-coherent block loads) and bit 6 (no block
 // store: nothing reads it but row n).
@@ -597,101 +597,6 @@ __global__ __launch_bounds__(256, 4) void potrf_diag_kernel(double* __restrict__
   potrf_block<PH>(Mb, A, lda, kb, npiv, dinv, parts, k, status);
 }
 
-// ----------------------------------------------------------------- trsm
-// Rows [s, Mp) of block column kb, 32 rows per workgroup (2 waves x 16 rows):
-//   X_cb = (A_cb - sum_{q < cb} X_q L_{cb,q}^T) * Dinv_cb^T,  cb = 0..7 (16 columns each).
-// The factored diagonal block (its 36 lower 16x16 blocks) and the rows are staged in LDS
-// once (111 KB: fits beside one SYRK workgroup); the products run on
-// v_mfma_f64_4x4x4_4b_f64 with A replicated over the 4 blocks, so the 16x16 accumulator
-// acc[ir] holds X[ir*4 + (lane >> 4)][lane & 15] — the 16x16 MFMA layout — as four
-// independent chains.
-__global__ __launch_bounds__(128) void trsm_kernel_v3(double* __restrict__ A, int64_t lda, int64_t s,
-                                                   int64_t kb, const double* __restrict__ dinv) {
-  constexpr int RW = 32;                               // rows per workgroup
-  constexpr int BS = IB * (IB + 1);                    // one padded 16x16 block
-  __shared__ double sA[RW][NB + 1];
-  __shared__ double Lb[(NB / IB) * (NB / IB + 1) / 2 * BS];
-#define LS(r, q) Lb[((((r) >> 4) * (((r) >> 4) + 1) / 2) + ((q) >> 4)) * BS + ((r) & 15) * (IB + 1) + ((q) & 15)]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int li = lane & 15, lk = lane >> 4, l3 = lane & 3;
-  const int64_t r0 = s + (int64_t)blockIdx.x * RW;
-  // rows: 32 x 64 double2 = 16 per thread; diagonal block: the 36 lower 16x16 blocks
-  {
-    double2 v[16];
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int idx = tid + 128 * u, r = idx >> 6, c2 = idx & 63;
-      v[u] = *reinterpret_cast<const double2*>(&A[(r0 + r) * lda + kb + 2 * c2]);
-    }
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int idx = tid + 128 * u, r = idx >> 6, c2 = idx & 63;
-      sA[r][2 * c2] = v[u].x;
-      sA[r][2 * c2 + 1] = v[u].y;
-    }
-  }
-  for (int half = 0; half < 2; ++half) {
-    double2 v[32];
-#pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      const int idx = tid + 128 * (u + 32 * half), r = idx >> 6, c2 = idx & 63;
-      if ((2 * c2) >> 4 <= r >> 4) v[u] = *reinterpret_cast<const double2*>(&A[(kb + r) * lda + kb + 2 * c2]);
-    }
-#pragma unroll
-    for (int u = 0; u < 32; ++u) {
-      const int idx = tid + 128 * (u + 32 * half), r = idx >> 6, c2 = idx & 63;
-      if ((2 * c2) >> 4 <= r >> 4) {
-        LS(r, 2 * c2) = v[u].x;
-        LS(r, 2 * c2 + 1) = v[u].y;
-      }
-    }
-  }
-  // Dinv_cb fragments for the Z = acc Dinv^T step: B[k][j] = Dinv[j][k], lane: j = li, k = lk
-  double dv[NB / IB][IB / 4];
-#pragma unroll
-  for (int cb = 0; cb < NB / IB; ++cb)
-#pragma unroll
-    for (int ks = 0; ks < IB / 4; ++ks) dv[cb][ks] = dinv[cb * IB * IB + li * IB + ks * 4 + lk];
-  __syncthreads();
-
-  const int wr = w * IB;
-#pragma unroll
-  for (int cb = 0; cb < NB / IB; ++cb) {
-    double acc[4];
-#pragma unroll
-    for (int ir = 0; ir < 4; ++ir) acc[ir] = sA[wr + ir * 4 + lk][cb * IB + li];
-#pragma unroll 4
-    for (int q0 = 0; q0 < cb * IB; q0 += 4) {
-      const double b = LS(cb * IB + li, q0 + lk);
-#pragma unroll
-      for (int ir = 0; ir < 4; ++ir) acc[ir] = mfma4(-sA[wr + ir * 4 + l3][q0 + lk], b, acc[ir]);
-    }
-    // Z = acc * Dinv_cb^T: acc goes through the wave's own LDS rows to become the A operand
-#pragma unroll
-    for (int ir = 0; ir < 4; ++ir) sA[wr + ir * 4 + lk][cb * IB + li] = acc[ir];
-    wave_lds_fence();
-    double z[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int ks = 0; ks < IB / 4; ++ks)
-#pragma unroll
-      for (int ir = 0; ir < 4; ++ir)
-        z[ir] = mfma4(sA[wr + ir * 4 + l3][cb * IB + ks * 4 + lk], dv[cb][ks], z[ir]);
-    wave_lds_fence();
-#pragma unroll
-    for (int ir = 0; ir < 4; ++ir) sA[wr + ir * 4 + lk][cb * IB + li] = z[ir];
-    wave_lds_fence();
-  }
-  // the wave's 16 rows back to HBM
-  for (int idx = lane; idx < IB * (NB / 2); idx += 64) {
-    const int r = idx / (NB / 2), q2 = idx - r * (NB / 2);
-    double2 v;
-    v.x = sA[wr + r][2 * q2];
-    v.y = sA[wr + r][2 * q2 + 1];
-    *reinterpret_cast<double2*>(&A[(r0 + wr + r) * lda + kb + 2 * q2]) = v;
-  }
-#undef LS
-}
-
 // ------------------------------------------------------------ trsm (v2)
 // Rows [s, Mp) of block column kb, 64 rows per workgroup, 16 rows per wave:
 //   X_cb = (A_cb - sum_{q < cb} X_q L_{cb,q}^T) * Dinv_cb^T,  cb = 0..7 (16 columns each).
@@ -991,91 +896,17 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
   syrk_unit<CIO, TR>(A, lda, s, P, kd, T, tj_lo, tj_hi, b + skip, ti0, sP);
 }
 
-// ------------------------------------------------------------ tall panel solve as a GEMM
-// Schedule 3: X = A21 L11^{-T} for the rows [r0, r0 + rows) below a super-panel of width
-// W = 128 w starting at column K0, given Bd = L11^{-T} (W x W, upper triangular, row-major,
-// ld W; the identity border of the chain factorisation). Unit (64-row slab rb, column block
-// cb): X[i][128 cb + j] = sum_{q < 128 (cb + 1)} A[i][K0 + q] Bd[q][128 cb + j]. X goes to a
-// separate buffer (ld W, row r0 first) — the A columns are still read by other units — and
-// row n of X (z = L^{-1} r) also to zvec[K0 + c].
-__global__ __launch_bounds__(256, LFM_SLAB_WGS) void tall_kernel(
-    const double* __restrict__ A, int64_t lda, int64_t K0, int64_t r0, int w,
-    const double* __restrict__ Bd, double* __restrict__ X, int64_t n, double* __restrict__ zvec) {
-  __shared__ double sP[64 + ST][KB + 1];
-  const int W = w * NB;
-  int64_t b = blockIdx.x;
-  {
-    int64_t lo, hi;
-    xcd_range(gridDim.x, (int)(b % 8), &lo, &hi);
-    b = lo + b / 8;
-  }
-  const int cb = (int)(b % w);
-  const int64_t i0 = r0 + (b / w) * 64;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64;
-  const int li = lane & 15, lk = lane >> 4;
-  double acc[8][4];
-#pragma unroll
-  for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = 0.0;
-  gemm_accumulate<64, true>(A + i0 * lda + K0, lda, Bd + cb * NB, W, NB * (cb + 1), acc, sP);
-  double* Xb = X + (i0 - r0 + wr + lk) * W + cb * NB + wc + li;
-#pragma unroll
-  for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-    for (int jr = 0; jr < 4; ++jr) {
-      Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
-      if (i0 + wr + ir * 4 + lk == n) zvec[K0 + cb * NB + wc + jr * 16 + li] = acc[ir][jr];
-    }
-}
-
-// Schedule 3 chain workspace Wk (2W x W, ld W): rows [0, W) the diagonal block
-// A[K1 .. K1 + W, K1 .. K1 + W] (lower part), rows [W, 2W) the identity. Factoring its W
-// columns leaves L11 in the top and L11^{-T} in the bottom. With wait != NULL the copy starts
-// once *wait >= target (the main stream's update of the block has landed).
+// Bounded relaxed / acquire spin on a device counter: true once *p >= target, false after
+// `limit` polls (the caller records PANEL_TIMEOUT). limit = 0 fails at once (the
+// LFM_DEBUG_SPIN_LIMIT test knob).
 template <bool ACQ = true>
-__device__ __forceinline__ bool spin_until(const unsigned* p, unsigned target) {
+__device__ __forceinline__ bool spin_until(const unsigned* p, unsigned target, unsigned limit) {
   unsigned it = 0;
   while (__hip_atomic_load(p, ACQ ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
              target &&
-         ++it < (1u << 26))
+         ++it < limit)
     __builtin_amdgcn_s_sleep(2);
-  return it < (1u << 26);
-}
-
-__global__ __launch_bounds__(256) void chain_init_kernel(const double* __restrict__ A, int64_t lda,
-                                                         int64_t K1, int W, double* __restrict__ Wk,
-                                                         const unsigned* wait, unsigned target,
-                                                         int* __restrict__ status) {
-  if (wait) {
-    __shared__ int ok;
-    if (threadIdx.x == 0) ok = spin_until(wait, target);
-    __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (!ok) {
-      if (threadIdx.x == 0) atomicMin(status, PANEL_TIMEOUT);
-      return;
-    }
-  }
-  const int64_t cells = (int64_t)W * W;  // 2W rows of W/2 double2
-  for (int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x; idx < cells;
-       idx += (int64_t)gridDim.x * 256) {
-    const int r = (int)(idx / (W / 2)), c = 2 * (int)(idx % (W / 2));
-    double2 v;
-    if (r < W) {
-      v = *reinterpret_cast<const double2*>(&A[(K1 + r) * lda + K1 + c]);
-    } else {
-      v.x = (r - W == c) ? 1.0 : 0.0;
-      v.y = (r - W == c + 1) ? 1.0 : 0.0;
-    }
-    *reinterpret_cast<double2*>(&Wk[(int64_t)r * W + c]) = v;
-  }
-}
-
-// Sets *flag = 1 (release) once every earlier kernel of the stream has completed.
-__global__ void signal_kernel(unsigned* flag) {
-  __hip_atomic_store(flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  return it < limit;
 }
 
 // One main-stream launch per super-panel step s (schedule 3): step s's trailing update from
@@ -1096,8 +927,6 @@ struct StepArgs {
   Panel px;       // X_s (rows from s0)
   int kd, T, wn;  // depth W_s, trailing 128-tiles, next width in tiles
   int na, nr, nt;  // units per role
-  int nr1;        // rest units dispatched before the tall units
-  int exp;        // experiments: bit 0 = no ahead -> tall ordering (wrong results; timing only)
   int64_t tr0;    // tall: first row (K1 of step s + 1), W_{s+1} = tw * 128, K0_{s+1} = tk0
   int64_t tk0;
   int tw;
@@ -1113,6 +942,7 @@ struct StepArgs {
   // rows < wn + lead) write through to memory and bump *xready when done
   unsigned* xready;  // NULL: no chain waits on this launch
   int lead;
+  unsigned spin;     // poll bound of every device-side wait (PANEL_TIMEOUT past it)
 };
 
 __device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
@@ -1126,21 +956,19 @@ __device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
 __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
   __shared__ double sP[64 + ST][KB + 1];
   const int64_t b = blockIdx.x;
-  // segments in blockIdx order: ahead, rest [0, nr1), tall, rest [nr1, nr)
-  const int cnt[4] = {g.na, g.nr1, g.nt, g.nr - g.nr1};
-  const int role_of[4] = {1, 2, 3, 2};
+  // roles in blockIdx order: ahead (1), rest (2), tall (3), each padded to a multiple of 8
+  const int cnt[3] = {g.na, g.nr, g.nt};
   int seg = 0;
   int64_t base = 0;
-  while (seg < 3 && b >= base + (cnt[seg] + 7) / 8 * 8) {
+  while (seg < 2 && b >= base + (cnt[seg] + 7) / 8 * 8) {
     base += (cnt[seg] + 7) / 8 * 8;
     ++seg;
   }
   int64_t lo, hi;
   xcd_range(cnt[seg], (int)(b % 8), &lo, &hi);
-  int64_t u = lo + (b - base) / 8;
+  const int64_t u = lo + (b - base) / 8;
   if (u >= hi) return;
-  const int role = role_of[seg];
-  if (seg == 3) u += g.nr1;
+  const int role = seg + 1;
   if (role == 1) {
     // device-coherent stores + a counter bump once they have completed: the tall units read
     // these rows with device-coherent loads (no L2 writeback / invalidate on either side)
@@ -1148,7 +976,7 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     const int trow = g.wn + (int)(u % (2 * (g.T - g.wn))) / 2;  // 128-tile row of the unit
-    if (threadIdx.x == 0 && g.a_done && !(g.exp & 1))
+    if (threadIdx.x == 0 && g.a_done)
       __hip_atomic_fetch_add(&g.a_done[trow], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0 && g.xready && trow < g.wn + g.lead)
       __hip_atomic_fetch_add(g.xready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1171,9 +999,9 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
     // relaxed polling and device-coherent operand loads below instead of an acquire fence:
     // an agent-scope acquire invalidates this XCD's L2 under the running bulk units
     if (threadIdx.x == 0) {
-      bool good = !g.chain_done || spin_until<false>(g.chain_done, 1u);
-      if (good && g.a_done && !(g.exp & 1))
-        good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], 2u * g.wn);
+      bool good = !g.chain_done || spin_until<false>(g.chain_done, 1u, g.spin);
+      if (good && g.a_done)
+        good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], 2u * g.wn, g.spin);
       ok = good;
     }
     __syncthreads();
@@ -1203,12 +1031,6 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
     }
 }
 
-// Row n of the chain workspace (n inside the super-panel's diagonal block) into zvec.
-__global__ void zrow_kernel(const double* __restrict__ Wk, int W, int64_t rloc, int64_t K0,
-                            double* __restrict__ zvec) {
-  for (int c = threadIdx.x; c < W; c += blockDim.x) zvec[K0 + c] = Wk[rloc * W + c];
-}
-
 // ---------------------------------------------------------- fused panel
 // One block column of the look-ahead chain in one launch (w = 1 steps):
 //   workgroups 0, 1   apply the pending rank-pkd update (panel columns pkb .. pkb + pkd) to the
@@ -1224,15 +1046,9 @@ __global__ void zrow_kernel(const double* __restrict__ Wk, int W, int64_t rloc, 
 constexpr size_t PANEL_LDS = (size_t)MB_DOUBLES * sizeof(double);
 static_assert(MB_DOUBLES >= 64 * (NB + 1) && MB_DOUBLES >= (64 + ST) * (KB + 1), "LDS union");
 
-__device__ __forceinline__ bool wait_counter(unsigned* p, unsigned target) {
+__device__ __forceinline__ bool wait_counter(unsigned* p, unsigned target, unsigned limit) {
   __shared__ int ok;
-  if (threadIdx.x == 0) {
-    unsigned it = 0;
-    while (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target &&
-           ++it < (1u << 26))
-      __builtin_amdgcn_s_sleep(2);
-    ok = it < (1u << 26);
-  }
+  if (threadIdx.x == 0) ok = spin_until<true>(p, target, limit);
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return ok;
@@ -1243,7 +1059,8 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
                                                     int64_t npiv, double* __restrict__ dinv,
                                                     double* __restrict__ parts, int k,
                                                     int* __restrict__ status,
-                                                    unsigned* __restrict__ sync, unsigned epoch) {
+                                                    unsigned* __restrict__ sync, unsigned epoch,
+                                                    unsigned spin) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __builtin_amdgcn_s_setprio(3);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1271,7 +1088,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     if (b == 1) return;
-    if (!wait_counter(&sync[1], 2u * epoch)) {
+    if (!wait_counter(&sync[1], 2u * epoch, spin)) {
       if (tid == 0) {
         atomicMin(status, PANEL_TIMEOUT);
         __hip_atomic_store(&sync[0], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -1291,7 +1108,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
   for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) sA[wr + ir * 4 + lk][wc + jr * 16 + li] = -acc[ir][jr];
-  if (!wait_counter(&sync[0], epoch)) {
+  if (!wait_counter(&sync[0], epoch, spin)) {
     if (tid == 0) atomicMin(status, PANEL_TIMEOUT);
     return;
   }
@@ -1331,8 +1148,7 @@ struct ChainArgs {
   int64_t K0p;             // first column of super-panel s - 1
   const double* Bdp;       // Bd_{s-1}: kd x kd, ld kd
   double* xd;              // W x kd scratch
-  int small;               // bit 0: PX, bit 1: P0, bit 2: in-chain panel solve and band
-                           // update (w > 1) in 32 x 32 tiles (gemm32)
+  unsigned spin;           // poll bound of the input wait (grid barriers: spin / 4)
 };
 
 // dynamic LDS of chain_kernel: the factor block and its inverse (packed 16x16 blocks)
@@ -1340,7 +1156,8 @@ constexpr size_t CHAIN_LDS = 2 * (size_t)MB_DOUBLES * sizeof(double);
 
 // Grid barrier over the chain kernel's co-resident workgroups: release, count, acquire.
 // Bounded: on timeout (or a timeout already recorded in *status) it returns false at once.
-__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, int* status) {
+__device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, int* status,
+                                          unsigned limit) {
   __shared__ int ok;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1349,7 +1166,7 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, int* s
     unsigned it = 0;
     bool good = true;
     while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (++it >= (1u << 24) ||
+      if (++it >= limit ||
           __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == PANEL_TIMEOUT) {
         good = false;
         atomicMin(status, PANEL_TIMEOUT);
@@ -1367,7 +1184,8 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, int* s
 // Light grid barrier: no cache maintenance. Valid when every value another workgroup wrote
 // before the barrier was stored write-through (agent-scope relaxed stores) and is read after it
 // with device-coherent loads: the s_waitcnt orders this thread's stores before the arrival.
-__device__ __forceinline__ bool grid_sync_light(unsigned* bar, unsigned target, int* status) {
+__device__ __forceinline__ bool grid_sync_light(unsigned* bar, unsigned target, int* status,
+                                                unsigned limit) {
   __shared__ int ok;
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
@@ -1376,7 +1194,7 @@ __device__ __forceinline__ bool grid_sync_light(unsigned* bar, unsigned target, 
     unsigned it = 0;
     bool good = true;
     while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (++it >= (1u << 24) ||
+      if (++it >= limit ||
           __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == PANEL_TIMEOUT) {
         good = false;
         atomicMin(status, PANEL_TIMEOUT);
@@ -1480,25 +1298,29 @@ __device__ __forceinline__ void gemm32(const double* __restrict__ pi, int64_t ld
   }
   __syncthreads();  // partials read: smem is free for the next call
 }
-// LIGHT (w = 1 with both small-tile phases): every value one workgroup hands to another is
-// stored write-through and loaded device-coherently, so the barriers, the input wait and the
-// completion flag need no cache maintenance (an agent-scope fence costs ~1.7-3.5 us).
-template <bool LIGHT, int XPH>
+// Every phase runs in 32 x 32 output tiles (gemm32) over all gridDim.x workgroups: one CU's
+// fp64 rate is 1/256 of the chip's, so the latency-bound chain spreads each product thin.
+// LIGHT (w = 1): every value one workgroup hands to another is stored write-through and
+// loaded device-coherently, so the barriers, the input wait and the completion flag need no
+// cache maintenance (an agent-scope fence costs ~1.7-3.5 us).
+template <bool LIGHT>
 __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
-  double (*sP)[CKS + 1] = reinterpret_cast<double (*)[CKS + 1]>(smem);
-  const int G = gridDim.x, wg = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int G = gridDim.x, wg = blockIdx.x, tid = threadIdx.x;
   const int W = g.w * NB;
   double* Aw = g.Wk - (g.Kc * W + g.Kc);  // the workspace with the matrix's row / column numbers
   unsigned nbar = 0;
   auto stamp = [&](int p) {
     if (g.stamps && wg == 0 && tid == 0 && p < 16) g.stamps[p] = __builtin_amdgcn_s_memrealtime();
   };
+  auto sync = [&]() {
+    return (LIGHT ? grid_sync_light : grid_sync)(g.bar, G * ++nbar, g.status, g.spin >> 2);
+  };
   stamp(0);
   // the block's inputs come from the main stream's launch in flight: wait for its count
   if (g.xready) {
     __shared__ int okx;
-    if (tid == 0) okx = spin_until<false>(g.xready, g.xtarget);
+    if (tid == 0) okx = spin_until<false>(g.xready, g.xtarget, g.spin);
     __syncthreads();
     // one agent-scope acquire so the inputs below come through plain, cached loads (LIGHT:
     // device-coherent loads instead)
@@ -1509,7 +1331,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     }
   }
   stamp(14);
-  if (g.kd > 0 && (g.small & 1)) {
+  if (g.kd > 0) {
     // PX in 32 x 32 tiles (K = 32 (cb + 1) rounded up to 128: Bd is upper triangular)
     const int nc = g.kd / 32, nu = (W / 32) * nc;
     for (int u = wg; u < nu; u += G) {
@@ -1519,7 +1341,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
       gemm32<true, LIGHT, LIGHT>(g.A + (g.Kc + 32 * rb) * g.lda + g.K0p, g.lda, g.Bdp + 32 * cb,
                                  g.kd, kd, v, smem);
       if (LIGHT) {
-        // element pairs, one 16-B write-through store each
+        // element pairs, one 16-B write-through store each (xd: W x kd doubles, < 2^31 B)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int e = 2 * tid + 512 * h;
@@ -1534,87 +1356,38 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
         }
       }
     }
-    if (!(LIGHT ? grid_sync_light : grid_sync)(g.bar, G * ++nbar, g.status)) return;
-  } else if (g.kd > 0) {
-    // PX: X_{s-1} rows of the block, 64-row x 128-column units (K = 128 (cb + 1), Bd upper)
-    const int wp = g.kd / NB;
-    const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64, li = lane & 15, lk = lane >> 4;
-    for (int u = wg; u < 2 * g.w * wp; u += G) {
-      const int cb = u % wp, rb = u / wp;
-      const int64_t i0 = g.Kc + 64 * rb;
-      double acc[8][4];
-#pragma unroll
-      for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-        for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = 0.0;
-      gemm_accumulate<64, true, false, CKS>(g.A + i0 * g.lda + g.K0p, g.lda, g.Bdp + cb * NB, g.kd,
-                                            NB * (cb + 1), acc, sP);
-      double* Xb = g.xd + (64 * rb + wr + lk) * g.kd + cb * NB + wc + li;
-#pragma unroll
-      for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-        for (int jr = 0; jr < 4; ++jr) Xb[(ir * 4) * g.kd + jr * 16] = acc[ir][jr];
-      __syncthreads();
-    }
-    if (!grid_sync(g.bar, G * ++nbar, g.status)) return;
+    if (!sync()) return;
   }
   stamp(13);
-  // P0: pending update of the block into the workspace (lower 128-tiles, 2 slabs each)
+  // P0: pending update of the block into the workspace, 32 x 32 lower tiles:
+  // Wk[D] = A[D] - X X^T
   {
-    const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64, li = lane & 15, lk = lane >> 4;
-    const int nunit = (g.small & 2) ? 0 : g.w * (g.w + 1);
-    if (g.small & 2) {
-      // 32 x 32 lower tiles: Wk[D] = A[D] - X X^T
-      const int nt = W / 32, ntile = nt * (nt + 1) / 2;
-      for (int u = wg; u < ntile; u += G) {
-        int ti = 0;
-        while ((ti + 1) * (ti + 2) / 2 <= u) ++ti;
-        const int tj = u - ti * (ti + 1) / 2;
-        double v[4] = {0.0, 0.0, 0.0, 0.0};
-        if (g.kd > 0)
-          gemm32<false, LIGHT, LIGHT>(g.xd + (int64_t)32 * ti * g.kd, g.kd,
-                                      g.xd + (int64_t)32 * tj * g.kd, g.kd, g.kd, v, smem);
-        if (LIGHT) {
-          // element pairs: one 16-B device-coherent load and one 16-B write-through store each
+    const int nt = W / 32, ntile = nt * (nt + 1) / 2;
+    for (int u = wg; u < ntile; u += G) {
+      int ti = 0;
+      while ((ti + 1) * (ti + 2) / 2 <= u) ++ti;
+      const int tj = u - ti * (ti + 1) / 2;
+      double v[4] = {0.0, 0.0, 0.0, 0.0};
+      if (g.kd > 0)
+        gemm32<false, LIGHT, LIGHT>(g.xd + (int64_t)32 * ti * g.kd, g.kd,
+                                    g.xd + (int64_t)32 * tj * g.kd, g.kd, g.kd, v, smem);
+      if (LIGHT) {
+        // element pairs: one 16-B device-coherent load and one 16-B write-through store each
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int e = 2 * tid + 512 * h;
-            const int il = 32 * ti + (e >> 5), jl = 32 * tj + (e & 31);
-            const double2 a = ld2<true>(&g.A[(g.Kc + il) * g.lda + g.Kc + jl]);
-            st2_wt(g.Wk, (unsigned)((il * W + jl) * 8), a.x - v[2 * h], a.y - v[2 * h + 1]);
-          }
-        } else {
+        for (int h = 0; h < 2; ++h) {
+          const int e = 2 * tid + 512 * h;
+          const int il = 32 * ti + (e >> 5), jl = 32 * tj + (e & 31);
+          const double2 a = ld2<true>(&g.A[(g.Kc + il) * g.lda + g.Kc + jl]);
+          st2_wt(g.Wk, (unsigned)((il * W + jl) * 8), a.x - v[2 * h], a.y - v[2 * h + 1]);
+        }
+      } else {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int e = tid + 256 * q;
-            const int64_t i = g.Kc + 32 * ti + (e >> 5), j = g.Kc + 32 * tj + (e & 31);
-            Aw[i * W + j] = g.A[i * g.lda + j] - v[q];
-          }
+        for (int q = 0; q < 4; ++q) {
+          const int e = tid + 256 * q;
+          const int64_t i = g.Kc + 32 * ti + (e >> 5), j = g.Kc + 32 * tj + (e & 31);
+          Aw[i * W + j] = g.A[i * g.lda + j] - v[q];
         }
       }
-    }
-    for (int u = wg; u < nunit; u += G) {
-      const int t = u >> 1, sub = u & 1;
-      int ti = 0;
-      while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-      const int tj = t - ti * (ti + 1) / 2;
-      const int64_t i0 = g.Kc + ti * NB + sub * 64, j0 = g.Kc + tj * NB;
-      const double* Cs = g.A + (i0 + wr + lk) * g.lda + j0 + wc + li;
-      double acc[8][4];
-#pragma unroll
-      for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-        for (int jr = 0; jr < 4; ++jr)
-          acc[ir][jr] = -Cs[(ir * 4) * g.lda + jr * 16];
-      if (g.kd > 0)
-        gemm_accumulate<64, false, false, CKS>(g.xd + (i0 - g.Kc) * g.kd, g.kd,
-                                               g.xd + (j0 - g.Kc) * g.kd, g.kd, g.kd, acc, sP);
-      double* Cd = Aw + (i0 + wr + lk) * W + j0 + wc + li;
-#pragma unroll
-      for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-        for (int jr = 0; jr < 4; ++jr) Cd[(ir * 4) * W + jr * 16] = -acc[ir][jr];
-      __syncthreads();
     }
     // identity border (w = 1: Bd overwrites it whole, nothing reads it)
     for (int64_t idx = (int64_t)wg * 256 + tid; idx < (LIGHT ? 0 : (int64_t)W * W / 2);
@@ -1627,7 +1400,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     }
   }
   stamp(1);
-  bool ok = (LIGHT ? grid_sync_light : grid_sync)(g.bar, G * ++nbar, g.status);
+  bool ok = sync();
   stamp(2);
   for (int c = 0; c < g.w && ok; ++c) {
     const int64_t kb = g.Kc + (int64_t)c * NB, r0 = kb + NB;
@@ -1635,18 +1408,19 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
     // the only block (w = 1: Bd = L11^{-T}), else into linv for the panel solve below
     if (wg == 0) {
       double* Li = smem + MB_DOUBLES;
-      potrf_block<(LIGHT ? 127 : 47) | 128 | XPH>(smem, Aw, W, kb, g.n, g.dinv, g.parts, (int)(kb / NB),
-                                   g.status, Li, g.stamps && g.w == 1 ? g.stamps + 5 : nullptr);
+      potrf_block<(LIGHT ? 127 : 47) | 128 | 512>(smem, Aw, W, kb, g.n, g.dinv, g.parts,
+                                                  (int)(kb / NB), g.status, Li,
+                                                  g.stamps && g.w == 1 ? g.stamps + 5 : nullptr);
       stamp(3 + 3 * c);
       store_inverse_t<LIGHT>(Li, g.w == 1 ? g.Wk + (int64_t)W * W : g.linv, g.w == 1 ? W : NB);
       stamp(4 + 3 * c);
     }
     if (g.w == 1) break;
-    ok = grid_sync(g.bar, G * ++nbar, g.status);
+    ok = sync();
     if (!ok) break;
     // panel solve of every workspace row below block c as a GEMM: X = A_c Linv_c^T
     const int64_t rows = g.Kc + 2 * W - r0;
-    if (g.small & 4) {
+    {
       // 32-row units, one workgroup each (the solve is in place: a unit owns its rows), the
       // four 32-column output tiles parked in LDS past gemm32's operands until all are formed
       double* park = smem + 2 * 32 * G32K;
@@ -1669,29 +1443,12 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
           }
         __syncthreads();
       }
-    } else {
-      const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64, li = lane & 15, lk = lane >> 4;
-      for (int64_t u = wg; u < rows / 64; u += G) {
-        const int64_t ra = r0 + 64 * u;
-        double acc[8][4];
-#pragma unroll
-        for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-          for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = 0.0;
-        gemm_accumulate<64, true, false, CKS>(Aw + ra * W + kb, W, g.linv, NB, NB, acc, sP);
-        __syncthreads();  // every wave's operand reads of these rows are done
-        double* Xb = Aw + (ra + wr + lk) * W + kb + wc + li;
-#pragma unroll
-        for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-          for (int jr = 0; jr < 4; ++jr) Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
-      }
     }
-    ok = grid_sync(g.bar, G * ++nbar, g.status);
+    ok = sync();
     stamp(5 + 3 * c);
     if (!ok || c + 1 == g.w) break;
-    const int T = (int)(rows / ST), hi = g.w - 1 - c;
-    if (g.small & 4) {
+    const int hi = g.w - 1 - c;
+    {
       // band update in 32 x 32 tiles: columns r0 .. r0 + 128 hi, every row below (diagonal
       // tiles whole: their upper part is never read)
       const int R32 = (int)(rows / 32), J32 = 4 * hi;
@@ -1713,15 +1470,8 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
           Aw[(ra + (e >> 5)) * W + ca + (e & 31)] -= v[q];
         }
       }
-    } else {
-      int64_t nunit = 0;
-      for (int tj = 0; tj < hi; ++tj) nunit += 2 * (T - tj);
-      for (int64_t u = wg; u < nunit; u += G) {
-        syrk_unit<true, 64, false, CKS>(Aw, W, r0, Panel{Aw + kb, W, 0}, NB, T, 0, hi, u, 0, sP);
-        __syncthreads();
-      }
     }
-    ok = grid_sync(g.bar, G * ++nbar, g.status);
+    ok = sync();
   }
   if (wg == 0) {
     if (g.n >= g.Kc && g.n < g.Kc + W) {
@@ -1834,88 +1584,42 @@ struct Launcher {
   int64_t Mp;   // rows of the (augmented) matrix being factored
   int64_t win;  // 0: trailing rows run to Mp; > 0: rows [s, s + win) only (bordered inverse)
   int64_t end(int64_t s) const { return win ? s + win : Mp; }
-  void potrf(hipStream_t st, int64_t k, int64_t n, double* dinv = nullptr) {
+  void potrf(hipStream_t st, int64_t k, int64_t n) {
     hipEvent_t ev;
     prof_begin(ctx, K_POTRF, &ev, st);
     hipLaunchKernelGGL(potrf_diag_kernel<15>, dim3(1), dim3(256), MB_DOUBLES * sizeof(double), st,
-                       A, lda, k * NB, n, dinv ? dinv : ctx->linvT, ctx->parts, (int)k,
-                       ctx->status);
+                       A, lda, k * NB, n, ctx->linvT, ctx->parts, (int)k, ctx->status);
     prof_end(ctx, K_POTRF, ev, (double)NB * NB * NB / 3.0, 0, st);
   }
-  // Panel solve of block column k over rows [r0, r0 + rows) with the diagonal inverses dinv.
-  void trsm_rows(hipStream_t st, int64_t k, int64_t r0, int64_t rows, const double* dinv) {
-    if (rows <= 0) return;
-    hipEvent_t ev;
-    prof_begin(ctx, K_TRSM, &ev, st);
-    hipLaunchKernelGGL(trsm_kernel_v2, dim3((unsigned)(rows / 64)), dim3(256), 0, st, A, lda, r0,
-                       k * NB, dinv);
-    prof_end(ctx, K_TRSM, ev, (double)rows * NB * NB, 2.0 * rows * NB * 8, st);
-  }
+  // Panel solve of block column k over the rows below it, with the diagonal inverses.
   void trsm(hipStream_t st, int64_t k) {
     const int64_t s = (k + 1) * NB;
     const int64_t rows = end(s) - s;
     if (rows <= 0) return;
     hipEvent_t ev;
     prof_begin(ctx, K_TRSM, &ev, st);
-    if (ctx->trsm_variant == 3)
-      hipLaunchKernelGGL(trsm_kernel_v3, dim3((unsigned)(rows / 32)), dim3(128), 0, st, A, lda, s,
-                         k * NB, ctx->linvT);
-    else
-      hipLaunchKernelGGL(trsm_kernel_v2, dim3((unsigned)(rows / 64)), dim3(256), 0, st, A, lda, s,
-                         k * NB, ctx->linvT);
+    hipLaunchKernelGGL(trsm_kernel_v2, dim3((unsigned)(rows / 64)), dim3(256), 0, st, A, lda, s,
+                       k * NB, ctx->linvT);
     prof_end(ctx, K_TRSM, ev, (double)rows * NB * NB, 2.0 * rows * NB * 8, st);
   }
-  // Trailing update of tile columns [lo, hi) of the matrix starting at s0 (T = 128-tiles)
-  // with panel columns kb .. kb + kd. tr = 64 (latency-critical narrow bands) or 128.
-  // ti0 (band launches only): first tile row, so a band can skip the rows of a diagonal block.
-  void syrk(hipStream_t st, int64_t s0, int64_t kb, int kd, int64_t T, int lo, int hi, int tr,
-            int prio = 0, int ti0 = 0) {
-    syrk_p(st, s0, Panel{A + kb, lda, 0}, kd, T, lo, hi, tr, prio, ti0, 0);
-  }
-  // Same with the panel rows taken from P; skip (triangle launches only): the first `skip`
-  // tile rows of the triangle are left out (updated by an earlier launch).
-  void syrk_p(hipStream_t st, int64_t s0, Panel P, int kd, int64_t T, int lo, int hi, int tr,
-              int prio, int ti0, int skip) {
+  // Trailing update of tile columns [lo, hi) of the matrix starting at s0 (T = 128-tiles, in
+  // 64-row slabs) with panel columns kb .. kb + kd. prio raises the look-ahead bands' waves.
+  void syrk(hipStream_t st, int64_t s0, int64_t kb, int kd, int64_t T, int lo, int hi,
+            int prio = 0) {
     if (T <= 0 || hi <= lo) return;
     hi = (int)std::min<int64_t>(hi, T);
-    const bool band = hi - lo <= 8;
-    if (!band) {
-      hi = (int)T;
-      tr = tile_rows(T - lo);
-      ti0 = 0;
-    }
-    const int sub = ST / tr;
-    int64_t tiles = 0;
+    if (hi - lo > 8) hi = (int)T;  // wider than a band: the triangle of every column >= lo
+    int64_t units = 0;
     double elems = 0;
     for (int tj = lo; tj < hi; ++tj) {
-      const int r0 = std::max(tj, ti0);
-      if (r0 >= T) continue;
-      tiles += (int64_t)sub * (T - r0);
-      elems += r0 > tj ? (double)(T - r0) * ST * ST
-                       : (double)(T - tj - 1) * ST * ST + (double)ST * (ST + 1) / 2;
+      units += 2 * (T - tj);
+      elems += (double)(T - tj - 1) * ST * ST + (double)ST * (ST + 1) / 2;
     }
-    int64_t skip_units = 0;
-    if (band && skip > 0) {
-      // a band enumerates tile rows from max(tj, ti0): skipping tile rows is a raised ti0
-      ti0 = std::max(ti0, skip);
-      return syrk_p(st, s0, P, kd, T, lo, hi, tr, prio, ti0, 0);
-    }
-    if (!band && skip > 0) {
-      skip_units = (int64_t)sub * skip * (skip + 1) / 2;
-      tiles -= skip_units;
-      elems -= (double)skip * (skip - 1) / 2 * ST * ST + (double)skip * ST * (ST + 1) / 2;
-    }
-    if (tiles <= 0) return;
+    if (units <= 0) return;
     hipEvent_t ev;
     prof_begin(ctx, K_SYRK, &ev, st);
-    if (tr == 64)
-      hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3((unsigned)tiles), dim3(256),
-                         (size_t)ctx->syrk_pad_kb * 1024, st, A, lda, s0, P, kd, (int)T, lo, hi,
-                         prio & ctx->prio_mask, ctx->xcd_remap, ti0, skip_units);
-    else
-      hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3((unsigned)tiles), dim3(256), 0, st, A,
-                         lda, s0, P, kd, (int)T, lo, hi, prio & ctx->prio_mask, ctx->xcd_remap,
-                         ti0, skip_units);
+    hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3((unsigned)units), dim3(256), 0, st, A, lda,
+                       s0, Panel{A + kb, lda, 0}, kd, (int)T, lo, hi, prio, 1, 0, (int64_t)0);
     prof_end(ctx, K_SYRK, ev, elems * 2.0 * kd, elems * 16.0, st);
   }
   int64_t tiles_from(int64_t s0) const { return (end(s0) - s0) / ST; }
@@ -1928,54 +1632,15 @@ struct Launcher {
     prof_begin(ctx, K_PANEL, &ev, st);
     hipLaunchKernelGGL(panel_kernel, dim3((unsigned)(2 + rows / 64)), dim3(256), PANEL_LDS, st, A,
                        lda, kb, pkb, pkd, n, ctx->linvT, ctx->parts, (int)k, ctx->status,
-                       ctx->psync, epoch);
+                       ctx->psync, epoch, ctx->spin_limit);
     prof_end(ctx, K_PANEL, ev,
              (double)NB * NB * NB / 3.0 + (double)rows * NB * NB + 2.0 * (rows + NB) * NB * pkd,
              0, st);
   }
-  // Row height of the triangle's work units: 128-row tiles run 2 per CU, 64-row slabs 3 per
-  // CU (fewer VGPRs); pick the one with fewer (cost-weighted) rounds of workgroups over the
-  // chip, so a triangle just past a multiple of 512 tiles does not leave a mostly idle
-  // last round. LFM_SYRK_TR=64|128 forces one.
-  int tile_rows(int64_t Tt) const {
-    if (ctx->syrk_tr > 0) return ctx->syrk_tr;
-    if (ctx->syrk_tr == 0) return 64;  // measured faster at every size (scripts/probe_syrk.py)
-    const int64_t tiles = Tt * (Tt + 1) / 2;
-    const double r128 = (double)((tiles + 2 * ctx->cus - 1) / (2 * ctx->cus));
-    const double r64 = (double)((2 * tiles + 3 * ctx->cus - 1) / (3 * ctx->cus));
-    return r64 * ctx->slab_cost < r128 ? 64 : 128;
-  }
-  // Schedule 2, side stream: factor the diagonal block of super-panel [k, k + w) only (rows
-  // below (k + w) NB untouched): per column potrf into dinv slot c, the solve of the block's
-  // rows below it, and the update of the block's remaining columns.
-  void diag_factor(hipStream_t st, int64_t k, int w, int64_t n) {
-    const int64_t K1 = (k + w) * NB;
-    for (int c = 0; c < w; ++c) {
-      double* dv = ctx->linvT + (size_t)c * NB * IB;  // 8 x 16 x 16 inverses per column
-      potrf(st, k + c, n, dv);
-      if (c + 1 < w) {
-        const int64_t r0 = (k + c + 1) * NB;
-        trsm_rows(st, k + c, r0, K1 - r0, dv);
-        syrk(st, r0, (k + c) * NB, NB, w - 1 - c, 0, w - 1 - c, 64, 1);
-      }
-    }
-  }
-  // Schedule 2, main stream: the tall part of super-panel [k, k + w) — rows below its diagonal
-  // block, solved column by column with the band update of the super-panel's later columns.
-  void tall_solve(hipStream_t st, int64_t k, int w) {
-    const int64_t K1 = (k + w) * NB;
-    for (int c = 0; c < w; ++c) {
-      const double* dv = ctx->linvT + (size_t)c * NB * IB;
-      const int64_t sc = (k + c + 1) * NB;  // rows below block column k + c start here
-      trsm_rows(st, k + c, K1, end(sc) - K1, dv);
-      if (c + 1 < w)
-        syrk(st, sc, (k + c) * NB, NB, (end(sc) - sc) / ST, 0, w - 1 - c, 64, 0, w - 1 - c);
-    }
-  }
   // Factor the super-panel of block columns [k, k + w): per column potrf + trsm, then the
-  // update of the super-panel's remaining columns with it (K = 128).
+  // update of the super-panel's remaining columns with it (K = 128). w = 1: one fused launch.
   void superpanel(hipStream_t st, int64_t k, int w, int64_t n) {
-    if (w == 1 && ctx->fused) {
+    if (w == 1) {
       panel(st, k, 0, 0, n);
       return;
     }
@@ -1984,7 +1649,7 @@ struct Launcher {
       trsm(st, k + i);
       if (i + 1 < w) {
         const int64_t s0 = (k + i + 1) * NB;
-        syrk(st, s0, (k + i) * NB, NB, tiles_from(s0), 0, w - 1 - i, 64, 1);
+        syrk(st, s0, (k + i) * NB, NB, tiles_from(s0), 0, w - 1 - i, 1);
       }
     }
   }
@@ -1996,44 +1661,6 @@ int env_int(const char* name, int def) {
 }
 }  // namespace
 
-// Diagnostic: average duration (us) of the diagonal-block kernel with phase mask `mask`
-// over `reps` launches on a 128 x 128 block of ctx->A (must hold >= 128*128 doubles).
-int probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us) {
-  int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)NB * NB * 8);
-  if (r) return r;
-  r = ensure(ctx, (void**)&ctx->parts, &ctx->parts_cap, 64);
-  if (r) return r;
-  hipStream_t st = ctx->stream;
-  auto launch = [&](int m) {
-    switch (m & 15) {
-#define LFM_PH(v) case v: hipFuncSetAttribute(reinterpret_cast<const void*>(&potrf_diag_kernel<v>), \
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                             (int)(MB_DOUBLES * sizeof(double))); \
-                            hipLaunchKernelGGL(potrf_diag_kernel<v>, dim3(1), dim3(256), MB_DOUBLES * sizeof(double), st, \
-                                              ctx->A, (int64_t)NB, (int64_t)0, (int64_t)NB, ctx->linvT, ctx->parts, 0, ctx->status); break;
-      LFM_PH(0) LFM_PH(1) LFM_PH(2) LFM_PH(3) LFM_PH(4) LFM_PH(5) LFM_PH(6) LFM_PH(7)
-      LFM_PH(8) LFM_PH(9) LFM_PH(10) LFM_PH(11) LFM_PH(12) LFM_PH(13) LFM_PH(14) LFM_PH(15)
-#undef LFM_PH
-    }
-  };
-  launch(mask);
-  hipEvent_t a, b;
-  hipEventCreate(&a);
-  hipEventCreate(&b);
-  hipEventRecord(a, st);
-  for (int i = 0; i < reps; ++i) launch(mask);
-  hipEventRecord(b, st);
-  hipError_t e = hipStreamSynchronize(st);
-  float ms = 0;
-  hipEventElapsedTime(&ms, a, b);
-  hipEventDestroy(a);
-  hipEventDestroy(b);
-  *us = ms * 1e3 / reps;
-  return hip_fail(ctx, e, "probe_potrf");
-}
-
-// Diagnostic: average duration (us) of one full-lower-triangle SYRK launch over a T x T grid
-// of 128-tiles with update depth kd; cio bit 0 = C tile I/O, bit 2 = 64-row slabs (with C I/O).
 // Diagnostic: the pivot reciprocal square root of the diagonal factor (v_rsq_f64 + one
 // Newton step) over host values x[n] -> y[n] (tests bound its relative error).
 __global__ void rsq_probe_kernel(const double* x, double* y, int64_t n) {
@@ -2065,41 +1692,19 @@ __global__ void fill_hash_kernel(double* a, int64_t cnt) {
   }
 }
 
-// Diagnostic load for probe_syrk (cio bit 5): one workgroup per side CU issuing fp64 MFMAs on
-// register operands for `iters` rounds, as an upper bound of the chain's power draw.
-__global__ __launch_bounds__(256) void mfma_burn_kernel(double* out, int iters) {
-  double a = 1.0 + threadIdx.x * 1e-3, b = 1.0 - threadIdx.x * 1e-3;
-  double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int i = 0; i < iters; ++i)
-#pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] = mfma4(a + u, b, acc[u]);
-  double t = 0;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) t += acc[u];
-  if (t == 1.2345e300) out[0] = t;
-}
-
-// probe_syrk cio bit 6: every store write-through and every load device-coherent (the cost
-// of streaming consecutive steps through one launch)
-__global__ __launch_bounds__(256, LFM_SLAB_WGS) void syrk_coh_kernel(double* __restrict__ A,
-                                                                    int64_t lda, int64_t s,
-                                                                    Panel P, int kd, int T) {
-  __shared__ double sP[64 + ST][KB + 1];
-  int64_t lo, hi;
-  xcd_range(gridDim.x, (int)(blockIdx.x % 8), &lo, &hi);
-  syrk_unit<true, 64, true, KB, true>(A, lda, s, P, kd, T, 0, T, lo + blockIdx.x / 8, 0, sP);
-}
-
+// Diagnostic: average duration (us) of one full-lower-triangle trailing-update launch (64-row
+// slabs) over a T x T grid of 128-tiles with update depth kd. cio bit 0: C tile I/O (else the
+// MFMAs alone), bit 3: random operands (else zeros), bit 4: on schedule 3's CU-masked bulk
+// stream instead of every CU.
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const int64_t n = (int64_t)T * ST + 512;
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
   if (r) return r;
-  if (cio & 8)  // random operands instead of zeros
+  if (cio & 8)
     hipLaunchKernelGGL(fill_hash_kernel, dim3(4096), dim3(256), 0, ctx->stream, ctx->A, n * n);
   else
     hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8, ctx->stream);
-  const unsigned tiles = (unsigned)((int64_t)T * (T + 1) / 2);
-  // cio bit 4: on schedule 3's CU-masked main stream (the bulk's CUs) instead of every CU
+  const unsigned units = (unsigned)((int64_t)T * (T + 1));
   hipStream_t st = (cio & 16) && ctx->m3 ? ctx->m3 : ctx->stream;
   if (st != ctx->stream) {
     hipEvent_t f;
@@ -2110,37 +1715,17 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   }
   const Panel pan{ctx->A, n, 0};
   auto go = [&]() {
-    if (cio & 64) {
-      hipLaunchKernelGGL(syrk_coh_kernel, dim3(2 * tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, pan, kd, T);
-      return;
-    }
-    if (cio & 4) {  // 64-row slabs, C I/O
-      hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(2 * tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, pan, kd, T, 0, T, 0, ctx->xcd_remap, 0, (int64_t)0);
-      return;
-    }
     if (cio & 1)
-      hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, pan, kd, T, 0, T, 0, ctx->xcd_remap, 0, (int64_t)0);
+      hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(units), dim3(256), 0, st, ctx->A, n,
+                         (int64_t)512, pan, kd, T, 0, T, 0, 1, 0, (int64_t)0);
     else
-      hipLaunchKernelGGL((syrk_kernel<false, 128>), dim3(tiles), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, pan, kd, T, 0, T, 0, ctx->xcd_remap, 0, (int64_t)0);
+      hipLaunchKernelGGL((syrk_kernel<false, 64>), dim3(units), dim3(256), 0, st, ctx->A, n,
+                         (int64_t)512, pan, kd, T, 0, T, 0, 1, 0, (int64_t)0);
   };
   go();
   hipEvent_t a, b;
   hipEventCreate(&a);
   hipEventCreate(&b);
-  if ((cio & 32) && ctx->s3) {
-    hipEvent_t f;
-    hipEventCreate(&f);
-    hipEventRecord(f, st);
-    hipStreamWaitEvent(ctx->s3, f, 0);
-    hipEventDestroy(f);
-    // ~ (reps + 1) x the probe's duration of MFMA issue on the side CUs
-    hipLaunchKernelGGL(mfma_burn_kernel, dim3((unsigned)ctx->side_cus), dim3(256), 0, ctx->s3,
-                       ctx->A, 400000 * (reps + 1));
-  }
   hipEventRecord(a, st);
   for (int i = 0; i < reps; ++i) go();
   hipEventRecord(b, st);
@@ -2149,38 +1734,8 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   hipEventElapsedTime(&ms, a, b);
   hipEventDestroy(a);
   hipEventDestroy(b);
-  if ((cio & 32) && ctx->s3) hipStreamSynchronize(ctx->s3);
   *us = ms * 1e3 / reps;
   return hip_fail(ctx, e, "probe_syrk");
-}
-
-// Diagnostic: average duration (us) of one panel solve over `rows` rows (multiple of 64)
-// below a unit diagonal block, variant 2 or 3.
-int probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us) {
-  const int64_t n = NB + rows;
-  int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
-  if (r) return r;
-  hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8, ctx->stream);
-  hipMemsetAsync(ctx->linvT, 0, NB * NB * 8, ctx->stream);
-  hipStream_t st = ctx->stream;
-  const int saved = ctx->trsm_variant;
-  ctx->trsm_variant = variant;
-  Launcher L{ctx, ctx->A, n, n, 0};
-  L.trsm(st, 0);
-  hipEvent_t a, b;
-  hipEventCreate(&a);
-  hipEventCreate(&b);
-  hipEventRecord(a, st);
-  for (int i = 0; i < reps; ++i) L.trsm(st, 0);
-  hipEventRecord(b, st);
-  hipError_t e = hipStreamSynchronize(st);
-  ctx->trsm_variant = saved;
-  float ms = 0;
-  hipEventElapsedTime(&ms, a, b);
-  hipEventDestroy(a);
-  hipEventDestroy(b);
-  *us = ms * 1e3 / reps;
-  return hip_fail(ctx, e, "probe_trsm");
 }
 
 int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,
@@ -2192,11 +1747,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     hipFuncSetAttribute(reinterpret_cast<const void*>(&potrf_diag_kernel<15>),
                         hipFuncAttributeMaxDynamicSharedMemorySize,
                         (int)(MB_DOUBLES * sizeof(double)));
-    const void* chains[4] = {reinterpret_cast<const void*>(&chain_kernel<false, 0>),
-                             reinterpret_cast<const void*>(&chain_kernel<true, 0>),
-                             reinterpret_cast<const void*>(&chain_kernel<false, 512>),
-                             reinterpret_cast<const void*>(&chain_kernel<true, 512>)};
-    for (const void* f : chains)
+    for (const void* f : {reinterpret_cast<const void*>(&chain_kernel<false>),
+                          reinterpret_cast<const void*>(&chain_kernel<true>)})
       hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)CHAIN_LDS);
     attr = true;
   }
@@ -2214,26 +1766,22 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   const int64_t nblk = bordered ? Mp / NB : npb;
   int r = ensure(ctx, (void**)&ctx->parts, &ctx->parts_cap, (size_t)nblk * sizeof(double));
   if (r) return r;
-  // step plan: super-panels of w = 4, 2 or 1 block columns while the trailing matrix is
-  // large, so the bulk trailing update runs with depth 128 w (C traffic per flop / w)
-  const bool s3 = ctx->sched == 3 && ctx->lookahead && ctx->side_cus > 0 && mode == CHOL_MLL;
-  // schedule 3: w = 4 down to 6144 rows, then one or two w = 2 steps down to 5120 — the last
-  // deep (w = 4) update would otherwise hold up the first w = 1 chains (their inputs come from
-  // the launch after it): measured 0.13-0.24 ms faster than going from w = 4 to w = 1 directly
+  const bool s3 = ctx->sched == 3 && ctx->side_cus > 0 && mode == CHOL_MLL;
+  // Step plan: super-panels of w = 4 block columns while the trailing matrix has at least
+  // LFM_W4_MIN rows, w = 2 down to LFM_W2_MIN, then w = 1, so the bulk trailing update runs
+  // with depth 128 w (C traffic per flop / w). Schedule 3: w = 4 down to 6144 rows, then one
+  // or two w = 2 steps down to 5120 — the last deep update would otherwise hold up the first
+  // w = 1 chains (measured 0.13-0.24 ms faster than going from w = 4 to w = 1 directly); its
+  // first super-panel is one block wide (its factor precedes any bulk work).
   const int64_t w4min = env_int("LFM_W4_MIN", 6144);
   const int64_t w2min = env_int("LFM_W2_MIN", s3 ? 5120 : 4096);
-  const int64_t w8min = env_int("LFM_W8_MIN", 1 << 30);
   std::vector<std::pair<int64_t, int>> steps;
-  // schedule 3: the first super-panel's factor and solve precede any bulk work, so it is kept
-  // narrow (LFM_FIRST_W, default 1); the next one's chain hides behind step 0's update
-  const int first_w = s3 ? env_int("LFM_FIRST_W", 1) : 0;
   for (int64_t k = 0; k < nblk;) {
     const int64_t m = bordered ? Mp + NB : Mp - k * NB;
     int w = 1;
-    if (m >= w8min && k + 8 <= nblk) w = 8;
-    else if (m >= w4min && k + 4 <= nblk) w = 4;
+    if (m >= w4min && k + 4 <= nblk) w = 4;
     else if (m >= w2min && k + 2 <= nblk) w = 2;
-    if (k == 0 && first_w > 0) w = std::min(w, first_w);
+    if (k == 0 && s3) w = 1;
     steps.emplace_back(k, w);
     k += w;
   }
@@ -2246,31 +1794,20 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   hipLaunchKernelGGL(status_init_kernel, dim3(1), dim3(1), 0, main, ctx->status);
   // the trailing update after the last super-panel matters only for the bordered rows
   auto trailing = [&](int s) { return s + 1 < S || mode != CHOL_MLL; };
-  // Super-panel s is prepared ahead on the side stream while the trailing matrix is large
-  // enough for the main stream's bulk update to hide it; below LFM_SERIAL_BELOW rows the
-  // steps run back to back on the main stream (no cross-stream event hops in the tail).
-  const int64_t serial_below = env_int("LFM_SERIAL_BELOW", 0);
-  auto ahead = [&](int s) {
-    if (!ctx->lookahead) return false;
-    const int64_t m = bordered ? Mp + NB : Mp - steps[s].first * NB;
-    return m >= serial_below;
-  };
   int64_t zsplit = 0;  // finalize: z columns below zsplit come from ctx->zvec
-  // schedule 3 needs CUs of its own for the side stream (LFM_SIDE_CUS): its waiting step
-  // units would otherwise hold every slot the side stream's factor kernels need
   if (s3) {
-    // the CU-partitioned stream pair, ordered after / before ctx->stream's work
+    // Schedule 3 on the CU-partitioned stream pair (LFM_SIDE_CUS CUs for the side stream),
+    // ordered after / before ctx->stream's work. Side stream, per super-panel s (columns
+    // [K0, K1), W = K1 - K0): chain_kernel factors only the W x W diagonal block, copied into a
+    // workspace with an identity border, so it also yields Bd = L11^{-T}. Main stream: one
+    // step_kernel per step applies step s's trailing update from X_s (the next super-panel's
+    // columns first, then the rest) and finishes with X_{s+1} = A21 Bd_{s+1}, the tall panel
+    // solve as a GEMM, once the side stream's factor of block s + 1 has landed. Cross-stream
+    // order within a step is by device flags (ctx->flags), reset per call.
     hipEventRecord(ev[0], ctx->stream);
     main = ctx->m3;
     side = ctx->s3;
     hipStreamWaitEvent(main, ev[0], 0);
-    // Schedule 3. Side stream, per super-panel s (columns [K0, K1), W = K1 - K0): the chain
-    // factors only the W x W diagonal block, copied into a workspace with an identity border
-    // (chain_init_kernel), so it also yields Bd = L11^{-T}. Main stream: one step_kernel per
-    // step applies step s's trailing update from X_s (next diagonal block first, then the next
-    // super-panel's columns, then the rest) and finishes with X_{s+1} = A21 Bd_{s+1}, the tall
-    // panel solve as a GEMM, once the side stream's factor of block s + 1 has landed.
-    // Cross-stream order within a step is by device flags (ctx->flags), reset per call.
     int wmax = 1;
     for (const auto& st : steps) wmax = std::max(wmax, st.second);
     const int64_t Wmax = (int64_t)wmax * NB, Tmax = Mp / ST + 1;
@@ -2300,13 +1837,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       const int ws = steps[s].second;
       return (unsigned)(ws * (ws + 1) + 2 * ws * steps[s - 1].second);
     };
-    // the chain's PX / P0 phases in 32 x 32 tiles (bit 0 / bit 1), for w = 1 and wider chains
-    const int chain_small1 = env_int("LFM_CHAIN_SMALL", 3);
-    const int chain_small4 = env_int("LFM_CHAIN_SMALL4", 7);  // bit 2: in-chain solve / band
-    // w = 1 chains with both small phases: fence-free hand-offs (chain_kernel<true>)
-    const bool chain_light = env_int("LFM_CHAIN_LIGHT", 1) != 0;
-    // the diagonal factor's panel solve pinned column by column (potrf_block PH bit 9)
-    const bool solve_pin = env_int("LFM_SOLVE_PIN", 1) != 0;
     // chain(s): factor block s on the side stream's CUs (one launch, see chain_kernel)
     auto chain = [&](int s, bool dev_wait = true) {
       ChainArgs c{};
@@ -2325,7 +1855,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         c.Bdp = wkbuf(s - 1) + (int64_t)c.kd * c.kd;
         c.xd = ctx->xd;
       }
-      c.small = c.w == 1 ? chain_small1 : chain_small4;
       c.n = n;
       c.dinv = ctx->linvT;
       c.linv = ctx->linv_full;
@@ -2334,36 +1863,50 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       c.zvec = ctx->zvec;
       c.bar = bars + s;
       c.done = chain_done + s;
+      c.spin = ctx->spin_limit;
       c.stamps = ctx->dbg_stamps ? ctx->dbg_stamps + 16 * (size_t)std::min(s, 255) : nullptr;
       hipEvent_t pe;
       prof_begin(ctx, K_POTRF, &pe, side);
-      const bool light = c.w == 1 && (c.small & 3) == 3 && chain_light;
-      auto kern = light ? (solve_pin ? chain_kernel<true, 512> : chain_kernel<true, 0>)
-                        : (solve_pin ? chain_kernel<false, 512> : chain_kernel<false, 0>);
-      hipLaunchKernelGGL(kern, dim3((unsigned)ctx->side_cus), dim3(256), CHAIN_LDS, side, c);
-      const double W = c.w * NB;
-      prof_end(ctx, K_POTRF, pe, W * W * W / 3.0 + W * W * W, 0, side);
+      hipLaunchKernelGGL(c.w == 1 ? chain_kernel<true> : chain_kernel<false>,
+                         dim3((unsigned)ctx->side_cus), dim3(256), CHAIN_LDS, side, c);
+      // algorithmic: the block's factor W^3 / 3, its pending update from X_{s-1} (the
+      // block's lower elements x 2 kd) and its rows of X_{s-1} (W kd^2); issued adds the
+      // block inverse (W^3) and the padded 32 x 32 tiles
+      const double W = c.w * NB, kd = c.kd;
+      prof_end(ctx, K_POTRF, pe, W * W * W / 3.0 + W * (W + 1) * kd + W * kd * kd, 0, side,
+               W * W * W / 3.0 + W * W * W + W * W * kd + 2.0 * W * kd * kd);
     };
     // tall units of step s: rows [K1_s, Mp) x w_s column blocks
     auto tall_units = [&](int s) {
       const int64_t K1 = (steps[s].first + steps[s].second) * NB;
       return (int)((Mp - K1) / 64 * steps[s].second);
     };
-    const char* tp = std::getenv("LFM_TALL_POS");
-    const double tall_pos = tp ? std::atof(tp) : 1.0;  // fraction of the rest ahead of the tall units
     auto launch_step = [&](StepArgs& g) {
       g.n = n;  // padding rows past n are skipped
-      g.nr1 = (int)std::min<double>(g.nr, std::max(0.0, tall_pos * g.nr));
-      g.exp = env_int("LFM_STEP_EXP", 0);
-      const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 +
-                           (int64_t)(g.nr1 + 7) / 8 * 8 + (int64_t)(g.nt + 7) / 8 * 8 +
-                           (int64_t)(g.nr - g.nr1 + 7) / 8 * 8;
+      g.spin = ctx->spin_limit;
+      const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 + (int64_t)(g.nr + 7) / 8 * 8 +
+                           (int64_t)(g.nt + 7) / 8 * 8;
       if (grid == 0) return;
-      double el = (double)g.na * 64 * ST + (double)g.nr * 64 * ST;
+      // issued: every 64 x 128 unit in full (padding rows included), tall units as GEMMs with
+      // the triangular inverse; algorithmic: the update of the unpadded augmented trailing
+      // matrix (rows s0 .. n, residual row n included: it is the forward substitution) less
+      // the next diagonal block (the chain's), and the triangular solve of the rows below
+      // the next super-panel (rows .. n) against its W' x W' factor
+      const double issued = ((double)g.na + g.nr) * 64 * ST * 2.0 * g.kd +
+                            (double)g.nt * 64 * ST * NB * (g.tw + 1);
+      double alg = 0.0;
+      if (g.na + g.nr > 0) {
+        const double m = (double)(n - g.s0), d = std::min<double>(g.wn * NB, m);
+        alg += 2.0 * g.kd * (m * (m + 1) / 2 + m - d * (d + 1) / 2);
+      }
+      if (g.nt > 0) {
+        const double W2 = (double)g.tw * NB;
+        alg += (double)std::max<int64_t>(0, n + 1 - g.tr0) * W2 * W2;
+      }
       hipEvent_t pe;
       prof_begin(ctx, K_SYRK, &pe, main);
       hipLaunchKernelGGL(step_kernel, dim3((unsigned)grid), dim3(256), 0, main, g);
-      prof_end(ctx, K_SYRK, pe, el * 2.0 * g.kd + (double)g.nt * 64 * ST * NB * (g.tw + 1), 0, main);
+      prof_end(ctx, K_SYRK, pe, alg, 0, main, issued);
     };
     auto tall_args = [&](StepArgs& g, int s) {  // tall part of the step launch: step s's rows
       const int64_t K0 = steps[s].first * NB;
@@ -2381,67 +1924,11 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.chain_done = chain_done + s;
       g.status = ctx->status;
     };
-    // side: chain(0) after the gram; every later chain(s) follows chain(s - 1) in stream order
-    // and waits on the device for its inputs (xready[s]) from the main launch in flight
-    hipEventRecord(ev[0], main);
-    hipStreamWaitEvent(side, ev[0], 0);
-    // LFM_S3_EVENTS=1: the same work ordered by stream events only (tall units in launches of
-    // their own after the factor's event, chains after the tall launch's event) — for tools
-    // that serialise dispatches (rocprofv3 --pmc), under which device-side waits between the
-    // two streams could never be met
-    const bool evmode = env_int("LFM_S3_EVENTS", 0) != 0;
-    hipEvent_t* evc = ev + 1;      // [S] chain(s) done (events mode)
-    hipEvent_t* evt = ev + 1 + S;  // [S] X_s complete (events mode)
-    if (evmode) {
-      chain(0);
-      hipEventRecord(evc[0], side);
-      for (int s = 0; s < S; ++s) {
-        if (s > 0) {
-          const int64_t K1 = (steps[s - 1].first + steps[s - 1].second) * NB;
-          const int W = steps[s - 1].second * NB, wn = steps[s].second;
-          const int T = (int)((Mp - K1) / ST);
-          StepArgs g{};  // step s - 1's trailing update only
-          g.A = A;
-          g.lda = lda;
-          g.s0 = K1;
-          g.px = Panel{xbuf(s - 1), W, K1};
-          g.kd = W;
-          g.T = T;
-          g.wn = wn;
-          g.na = 2 * wn * (T - wn);
-          g.nr = (T - wn) * (T - wn + 1);
-          g.status = ctx->status;
-          launch_step(g);
-        }
-        hipStreamWaitEvent(main, evc[s], 0);
-        StepArgs g{};  // X_s
-        tall_args(g, s);
-        g.chain_done = nullptr;
-        g.a_done = nullptr;
-        g.xready = nullptr;
-        launch_step(g);
-        hipEventRecord(evt[s], main);
-        if (s + 1 < S) {
-          hipStreamWaitEvent(side, evt[s], 0);
-          chain(s + 1, false);
-          hipEventRecord(evc[s + 1], side);
-        }
-      }
-    } else {
-    chain(0);
-    {
-      // X_0 once the first block is factored (its units wait for chain_done[0])
-      StepArgs g{};
-      tall_args(g, 0);
-      g.a_done = nullptr;
-      launch_step(g);
-    }
-    for (int s = 0; s + 1 < S; ++s) {
+    // update of step s (trailing matrix from K1_s), excluding the next diagonal block
+    auto update_args = [&](StepArgs& g, int s) {
       const int64_t K1 = (steps[s].first + steps[s].second) * NB;
       const int W = steps[s].second * NB, wn = steps[s + 1].second;
       const int T = (int)((Mp - K1) / ST);
-      chain(s + 1);
-      StepArgs g{};
       g.A = A;
       g.lda = lda;
       g.s0 = K1;
@@ -2451,81 +1938,96 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.wn = wn;
       g.na = 2 * wn * (T - wn);
       g.nr = (T - wn) * (T - wn + 1);  // 2 slabs per tile of the (T - wn)-tile triangle
-      tall_args(g, s + 1);
-      g.a_done = a_done + (size_t)s * Tmax;
-      // the block after next: its tiles (rest) and rows (ahead) feed chain(s + 2)
-      if (s + 2 < S) {
-        g.xready = xready + s + 2;
-        g.lead = steps[s + 2].second;
-      }
-      launch_step(g);
-    }
-    }  // device-ordered mode
-    hipEventRecord(ev[2 * S + 1], side);
-    hipStreamWaitEvent(main, ev[2 * S + 1], 0);
-  } else if (ctx->sched == 2 && ctx->lookahead) {
-    // Schedule 2: the side stream factors only each super-panel's diagonal block (a few
-    // workgroups); the main stream solves the tall panel below it and applies the bulk
-    // update, leaving the next super-panel's diagonal block to the side stream.
+      g.status = ctx->status;
+    };
+    // side: chain(0) after the gram; every later chain(s) follows chain(s - 1) in stream order
+    // and waits on the device for its inputs (xready[s]) from the main launch in flight
     hipEventRecord(ev[0], main);
     hipStreamWaitEvent(side, ev[0], 0);
-    L.diag_factor(side, steps[0].first, steps[0].second, n);
-    hipEventRecord(ev[1], side);
-    for (int s = 0; s < S; ++s) {
-      const int64_t k = steps[s].first;
-      const int w = steps[s].second;
-      const int64_t K0 = k * NB, K1 = (k + w) * NB;
-      hipStreamWaitEvent(main, ev[1 + 2 * s], 0);
-      L.tall_solve(main, k, w);
-      hipEventRecord(ev[2 + 2 * s], main);
-      const bool nxt = s + 1 < S;
-      const int wn = nxt ? steps[s + 1].second : 0;
-      if (trailing(s)) {
-        const int64_t T = L.tiles_from(K1);
-        if (wn) L.syrk(main, K1, K0, NB * w, T, 0, wn, 64, 0, wn);  // below the next block
-        if (wn < T) L.syrk(main, K1, K0, NB * w, T, wn, (int)T, 128);
+    if (ctx->s3_events) {
+      // The same work ordered by stream events only (tall units in launches of their own after
+      // the factor's event, chains after the tall launch's event) — for tools that serialise
+      // dispatches (rocprofv3 --pmc), under which device-side waits between the two streams
+      // could never be met.
+      hipEvent_t* evc = ev + 1;      // [S] chain(s) done
+      hipEvent_t* evt = ev + 1 + S;  // [S] X_s complete
+      chain(0);
+      hipEventRecord(evc[0], side);
+      for (int s = 0; s < S; ++s) {
+        if (s > 0) {
+          StepArgs g{};  // step s - 1's trailing update only
+          update_args(g, s - 1);
+          launch_step(g);
+        }
+        hipStreamWaitEvent(main, evc[s], 0);
+        StepArgs g{};  // X_s
+        tall_args(g, s);
+        g.chain_done = nullptr;
+        launch_step(g);
+        hipEventRecord(evt[s], main);
+        if (s + 1 < S) {
+          hipStreamWaitEvent(side, evt[s], 0);
+          chain(s + 1, false);
+          hipEventRecord(evc[s + 1], side);
+        }
       }
-      if (nxt) {
-        hipStreamWaitEvent(side, ev[2 + 2 * s], 0);
-        L.syrk(side, K1, K0, NB * w, wn, 0, wn, 64, 1);  // the next diagonal block
-        L.diag_factor(side, steps[s + 1].first, wn, n);
-        hipEventRecord(ev[1 + 2 * (s + 1)], side);
+    } else {
+      chain(0);
+      {
+        // X_0 once the first block is factored (its units wait for chain_done[0])
+        StepArgs g{};
+        tall_args(g, 0);
+        launch_step(g);
+      }
+      for (int s = 0; s + 1 < S; ++s) {
+        chain(s + 1);
+        StepArgs g{};
+        update_args(g, s);
+        tall_args(g, s + 1);
+        g.a_done = a_done + (size_t)s * Tmax;
+        // the block after next: its tiles (rest) and rows (ahead) feed chain(s + 2)
+        if (s + 2 < S) {
+          g.xready = xready + s + 2;
+          g.lead = steps[s + 2].second;
+        }
+        launch_step(g);
       }
     }
+    hipEventRecord(ev[2 * S + 1], side);
+    hipStreamWaitEvent(main, ev[2 * S + 1], 0);
   } else {
-  if (ahead(0)) {
+    // Schedule 1 (gradient / posterior modes, or no CU partition): super-panel s + 1 is
+    // factored on the high-priority side stream while the main stream runs the bulk of step
+    // s's trailing update.
     hipEventRecord(ev[0], main);
     hipStreamWaitEvent(side, ev[0], 0);
     L.superpanel(side, steps[0].first, steps[0].second, n);
     hipEventRecord(ev[1], side);
-  }
-  for (int s = 0; s < S; ++s) {
-    const int64_t k = steps[s].first;
-    const int w = steps[s].second;
-    const int64_t s0 = (k + w) * NB;
-    const int64_t T = L.tiles_from(s0);
-    if (ahead(s)) hipStreamWaitEvent(main, ev[1 + 2 * s], 0);
-    else L.superpanel(main, k, w, n);
-    // ahead(s + 1) implies ahead(s): the trailing matrix only shrinks
-    const bool nxt = s + 1 < S && ahead(s + 1);
-    const int wn = nxt ? steps[s + 1].second : 0;
-    // main: the bulk of step s's trailing update (tile columns >= wn), depth 128 w
-    if (trailing(s)) L.syrk(main, s0, k * NB, NB * w, T, wn, (int)T, 128);
-    hipEventRecord(ev[2 + 2 * s], main);
-    if (nxt) {
-      // side: the next super-panel's columns first (after main's previous bulk update,
-      // which wrote the same tiles), then its factorisation
-      if (s > 0) hipStreamWaitEvent(side, ev[2 + 2 * (s - 1)], 0);
-      if (wn == 1 && ctx->fused) {
-        L.panel(side, steps[s + 1].first, k * NB, NB * w, n);
-      } else {
-        L.syrk(side, s0, k * NB, NB * w, T, 0, wn, 64, 1);
-        L.superpanel(side, steps[s + 1].first, steps[s + 1].second, n);
+    for (int s = 0; s < S; ++s) {
+      const int64_t k = steps[s].first;
+      const int w = steps[s].second;
+      const int64_t s0 = (k + w) * NB;
+      const int64_t T = L.tiles_from(s0);
+      hipStreamWaitEvent(main, ev[1 + 2 * s], 0);
+      const bool nxt = s + 1 < S;
+      const int wn = nxt ? steps[s + 1].second : 0;
+      // main: the bulk of step s's trailing update (tile columns >= wn), depth 128 w
+      if (trailing(s)) L.syrk(main, s0, k * NB, NB * w, T, wn, (int)T);
+      hipEventRecord(ev[2 + 2 * s], main);
+      if (nxt) {
+        // side: the next super-panel's columns first (after main's previous bulk update,
+        // which wrote the same tiles), then its factorisation
+        if (s > 0) hipStreamWaitEvent(side, ev[2 + 2 * (s - 1)], 0);
+        if (wn == 1) {
+          L.panel(side, steps[s + 1].first, k * NB, NB * w, n);
+        } else {
+          L.syrk(side, s0, k * NB, NB * w, T, 0, wn, 1);
+          L.superpanel(side, steps[s + 1].first, steps[s + 1].second, n);
+        }
+        hipEventRecord(ev[1 + 2 * (s + 1)], side);
       }
-      hipEventRecord(ev[1 + 2 * (s + 1)], side);
     }
   }
-  }  // schedule 1
   r = hip_fail(ctx, hipGetLastError(), "cholesky launch");
   if (r) return r;
   hipEvent_t pe;

@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/lfm.h"
+#include "../../include/lfm_diag.h"
 
 namespace lfm {
 
@@ -46,7 +47,7 @@ struct GridLayout {
 struct ProfEvent {
   int cls;
   hipEvent_t a, b;
-  double flops, bytes;
+  double flops, bytes, issued;
 };
 
 }  // namespace lfm
@@ -57,11 +58,7 @@ struct lfm_ctx {
   hipStream_t side = nullptr;    // high-priority look-ahead stream: panel factor + solve
   hipStream_t m3 = nullptr;      // schedule 3: bulk stream (CUs outside the chain's)
   hipStream_t s3 = nullptr;      // schedule 3: factor-chain stream (LFM_SIDE_CUS CUs)
-  bool lookahead = true;
-  int trsm_variant = 2;          // panel-solve kernel variant (LFM_TRSM=2|3)
-  int syrk_tr = 0;               // force SYRK triangle work-unit rows (LFM_SYRK_TR=64|128)
   int cus = 256;                 // compute units of the device
-  double slab_cost = 0.75;       // time of a round of 64-row slabs / a round of 128-tiles
   std::vector<hipEvent_t> evs;   // cross-stream dependency events (timing disabled)
   std::string err;
   int nb = 128;  // Cholesky block size
@@ -84,11 +81,9 @@ struct lfm_ctx {
   unsigned* psync = nullptr;                     // fused panel: [0] factor epoch, [1] slab count
   unsigned panel_epoch = 0;                      // fused panel launches so far
   int side_cus = 0;                              // CUs reserved for the side stream (LFM_SIDE_CUS)
-  int sched = 3;                                 // look-ahead schedule 1, 2 or 3 (LFM_SCHED)
-  int fused = 1;                                 // fused panel kernel for w = 1 steps (LFM_FUSED)
-  int syrk_pad_kb = 0;                           // extra LDS per slab workgroup: caps residency (LFM_SYRK_PAD_KB)
-  int xcd_remap = 1;                             // XCD-contiguous SYRK tile order (LFM_XCD_REMAP)
-  int prio_mask = 1;                             // raise look-ahead SYRK band wave priority (LFM_BAND_PRIO)
+  int sched = 3;                                 // look-ahead schedule 1 or 3 (LFM_SCHED)
+  bool s3_events = false;                        // schedule 3 ordered by events (LFM_S3_EVENTS)
+  unsigned spin_limit = 1u << 26;                // device-side wait bound (LFM_DEBUG_SPIN_LIMIT)
   double* result = nullptr;                      // [0..] scalar results
   double* gacc = nullptr; size_t gacc_bytes = 0; // gradient accumulators + output
 
@@ -113,6 +108,13 @@ struct lfm_ctx {
 // ---------------------------------------------------------------- helpers
 namespace lfm {
 
+// Device status word (ctx->status[0], finalize copies it to result[3]): INT_MAX = every pivot
+// positive; >= 0 = first non-positive / NaN pivot; STATUS_TIMEOUT = a bounded device-side
+// wait ran out (it wins the atomicMin over any pivot index).
+constexpr int STATUS_TIMEOUT = -2;
+// LFM_OK, LFM_E_NOT_PD (pivot index in the message) or LFM_E_TIMEOUT for a status word.
+int status_code(lfm_ctx* ctx, double st);
+
 int set_err(lfm_ctx* ctx, int code, const std::string& msg);
 int hip_fail(lfm_ctx* ctx, hipError_t e, const char* what);
 int ensure(lfm_ctx* ctx, void** p, size_t* cap, size_t bytes);
@@ -120,8 +122,9 @@ int ensure_pinned(lfm_ctx* ctx, size_t bytes);
 
 // profiling hooks around a launch on ctx->stream
 void prof_begin(lfm_ctx* ctx, int cls, hipEvent_t* a, hipStream_t st = nullptr);
+// flops / bytes: algorithmic work of the launch; issued (< 0: = flops): what it issues
 void prof_end(lfm_ctx* ctx, int cls, hipEvent_t a, double flops, double bytes,
-              hipStream_t st = nullptr);
+              hipStream_t st = nullptr, double issued = -1.0);
 int ensure_events(lfm_ctx* ctx, size_t count);
 int prof_flush(lfm_ctx* ctx);
 
@@ -207,9 +210,7 @@ int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int ma
 // diagnostics (lfm_probe.hip)
 int probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double* ms);
 int probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d);
-int probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us);
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us);
-int probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us);
 int probe_mfma4_layout(lfm_ctx* ctx, const double* a, const double* b, const double* c,
                        double* d);
 int probe_rates(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflops);

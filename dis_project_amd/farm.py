@@ -74,6 +74,68 @@ class TorchGather:
         return torch.cat(out).numpy()
 
 
+class ResidentEvaluator:
+    """MLL evaluations of many hyperparameter sets on ONE dataset held in HBM (the C3 random
+    restarts; bench.py's C2 step): x / y are uploaded and their layout analysed once
+    (``lfm_data_create``), each evaluation uploads only the 3G + 3 hyperparameters
+    (``lfm_mll_f64_data``). Not PD -> NaN (JAX semantics); a device-side timeout raises."""
+
+    def __init__(self, ctx: _lib.Context, data, negative: bool = False):
+        self.ctx, self.negative = ctx, bool(negative)
+        lib, h = ctx.lib, ctx.handle
+        x = np.ascontiguousarray(data.X, dtype=np.float64).reshape(-1, 3)
+        y = np.ascontiguousarray(data.y, dtype=np.float64).reshape(-1)
+        self.n = x.shape[0]
+        self.dx, self.dy, self.data = _lib.c_void_p(), _lib.c_void_p(), _lib.c_void_p()
+        ctx.check(lib.lfm_dev_alloc(h, x.nbytes, _lib.ctypes.byref(self.dx)))
+        ctx.check(lib.lfm_dev_alloc(h, y.nbytes, _lib.ctypes.byref(self.dy)))
+        ctx.check(lib.lfm_memcpy_h2d(h, self.dx, x.ctypes.data, x.nbytes))
+        ctx.check(lib.lfm_memcpy_h2d(h, self.dy, y.ctypes.data, y.nbytes))
+        ctx.check(lib.lfm_data_create(h, self.dx, self.dy, self.n, _lib.ctypes.byref(self.data)))
+        self._hyps = {}
+        self._out = np.empty(1)
+
+    def __call__(self, models) -> np.ndarray:
+        vals = np.empty(len(models))
+        for i, m in enumerate(models):
+            hp = self._hyps.get(id(m))
+            if hp is None:
+                hp = self._hyps[id(m)] = (m, m.hyp())  # keeps m alive: id() stays unique
+            rc = self.ctx.lib.lfm_mll_f64_data(self.ctx.handle, self.data, hp[1].ref,
+                                               int(self.negative), _lib.dptr(self._out))
+            self.ctx.check(rc, allow_not_pd=True)
+            vals[i] = self._out[0]
+        return vals
+
+    def close(self):
+        if self.data:
+            self.ctx.lib.lfm_data_destroy(self.data)
+            self.ctx.lib.lfm_dev_free(self.ctx.handle, self.dx)
+            self.ctx.lib.lfm_dev_free(self.ctx.handle, self.dy)
+            self.data = None
+
+
+def workload(kind: str, genes: int = 64, timepoints: int = 256, restarts: int = 32):
+    """Problems of a farm workload as (models, datasets):
+
+    ``c3``  BASELINE.json configs[2]: the C2 grid (``genes`` x ``timepoints``) under
+            ``restarts`` random-restart hyperparameter sets (configs.c3_restarts), one dataset;
+    ``c5``  configs[4]: 3 synthetic replicates x 5 leave-one-gene-out ablations at N = 28
+            (configs.c5_ablations, notebook.py:33-75).
+    """
+    from . import configs
+
+    if kind == "c3":
+        base = configs.grid_workload(f"synthetic_{genes}x{timepoints}_fp64", genes, timepoints,
+                                     seed_params=2, seed_y=3)
+        models = configs.c3_restarts(base, restarts)
+        return models, [base.data] * len(models)
+    if kind == "c5":
+        ws = configs.c5_ablations()
+        return [w.model for w in ws], [w.data for w in ws]
+    raise ValueError(f"unknown farm workload {kind!r}")
+
+
 class Farm:
     """Evaluate P independent problems over W ranks and all-gather the results.
 
@@ -100,3 +162,26 @@ class Farm:
             rr = partition(nprob, self.world, r)
             out[rr.start:rr.stop] = recv[r, : len(rr)]
         return out
+
+    def run_problems(self, models, datasets, evaluate) -> np.ndarray:
+        """One round over (models, datasets) — bench.py's step for ``--workload c3 / c5``:
+        this rank evaluates its block through ``evaluate(models, datasets) -> values`` and the
+        slots are all-gathered. Returns every problem's value on every rank."""
+        if len(models) != len(datasets):
+            raise ValueError("models and datasets must pair up")
+        return self.run(len(models), lambda idx: evaluate([models[i] for i in idx],
+                                                          [datasets[i] for i in idx]))
+
+
+def gpu_evaluator(ctx: _lib.Context, datasets, negative: bool = False):
+    """The product evaluator of a farm round on this rank's GPU: problems sharing one large
+    dataset go through a ResidentEvaluator (x / y in HBM once); small ones through one
+    batched launch (``CustomConjMLL.batch``: one workgroup per problem, n <= 128)."""
+    from .objectives import CustomConjMLL
+
+    shared = len({id(d) for d in datasets}) == 1 and datasets[0].n > 128
+    if shared:
+        res = ResidentEvaluator(ctx, datasets[0], negative)
+        return (lambda models, data: res(models)), res.close
+    mll = CustomConjMLL(negative=negative)
+    return (lambda models, data: mll.batch(models, data)), (lambda: None)

@@ -19,6 +19,10 @@
  *   - Return value: LFM_OK (0) or an LFM_E_* code; lfm_last_error() has the text.
  *     LFM_E_NOT_PD mirrors JAX's silent NaN on a failed Cholesky: the scalar
  *     output is set to NaN and the failing pivot index is in lfm_last_error().
+ *     LFM_E_TIMEOUT is NOT a property of the input: a bounded device-side wait of the
+ *     factorisation's cross-stream hand-off ran out (e.g. a tool serialised the two
+ *     streams' dispatches). The result is invalid; callers must raise, never map it to NaN.
+ *   - Diagnostics (rate / layout probes, phase stamps) are declared in lfm_diag.h.
  */
 #ifndef LFM_H
 #define LFM_H
@@ -30,7 +34,7 @@
 extern "C" {
 #endif
 
-#define LFM_ABI_VERSION 1
+#define LFM_ABI_VERSION 2
 
 enum {
   LFM_OK = 0,
@@ -39,7 +43,8 @@ enum {
   LFM_E_NOT_PD = 3, /* Cholesky pivot <= 0 or NaN; scalar result is NaN    */
   LFM_E_OOM = 4,    /* device allocation failed                            */
   LFM_E_RCCL = 5,   /* RCCL not loadable / collective failed               */
-  LFM_E_STATE = 6   /* call out of order (e.g. farm not initialised)       */
+  LFM_E_STATE = 6,  /* call out of order (e.g. farm not initialised)       */
+  LFM_E_TIMEOUT = 7 /* device-side wait ran out: result invalid (not NaN)  */
 };
 
 /* gram / cross-covariance output selection */
@@ -74,13 +79,17 @@ typedef struct {
   lfm_hyp hyp;
 } lfm_problem;
 
-/* Per-kernel-class timing, filled when profiling is on (HIP events on the ctx stream). */
+/* Per-kernel-class timing, filled when profiling is on (HIP events on the stream each
+ * launch runs on). flops / bytes are ALGORITHMIC: the blocked Cholesky's work on the
+ * unpadded (n + 1)-row augmented matrix (N^3 / 3 over a factorisation), not what the
+ * padded tiles issue; issued_flops is the MFMA work the launches actually issue. */
 typedef struct {
   char name[32];
   int64_t launches;
-  double total_ms;   /* sum of per-launch HIP-event durations              */
-  double flops;      /* algorithmic flops over all launches                */
-  double bytes;      /* algorithmic HBM bytes over all launches            */
+  double total_ms;     /* sum of per-launch HIP-event durations              */
+  double flops;        /* algorithmic flops over all launches                */
+  double bytes;        /* algorithmic HBM bytes over all launches            */
+  double issued_flops; /* flops issued (padded tiles, inverse-based solves)  */
 } lfm_kstat;
 
 /* ---------------------------------------------------------------- context */
@@ -153,6 +162,8 @@ int lfm_dev_alloc(lfm_ctx* ctx, size_t bytes, void** out);
 int lfm_dev_free(lfm_ctx* ctx, void* p);
 int lfm_memcpy_h2d(lfm_ctx* ctx, void* dst, const void* src, size_t bytes);
 int lfm_memcpy_d2h(lfm_ctx* ctx, void* dst, const void* src, size_t bytes);
+/* Sets `bytes` bytes of device memory at dst to the byte `value` (e.g. sentinel fills). */
+int lfm_memset_dev(lfm_ctx* ctx, void* dst, int value, size_t bytes);
 /* As lfm_mll_f64 with x / y already on the ctx's device. */
 int lfm_mll_f64_dev(lfm_ctx* ctx, const double* d_x, const double* d_y, int64_t n,
                     const lfm_hyp* hyp, int negative, double* out);
@@ -181,9 +192,6 @@ int lfm_profile_classes(lfm_ctx* ctx, unsigned mask);
 int lfm_profile_reset(lfm_ctx* ctx);
 /* Copies up to max entries; *count = number of kernel classes seen. */
 int lfm_profile_read(lfm_ctx* ctx, lfm_kstat* stats, int max, int* count);
-/* Diagnostics: phase timestamps (s_memrealtime, 100 MHz) of the schedule-3 factor chain,
- * 16 per super-panel step. enable = 1 arms them; enable = 0 copies up to max out. */
-int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max);
 
 /* -------------------------------- multi-GPU farm: RCCL all-gather over xGMI */
 /* Rank 0 creates the 128-byte unique id; the caller ships it to every rank. */
@@ -192,32 +200,6 @@ int lfm_farm_init(lfm_ctx* ctx, const unsigned char id[128], int nranks, int ran
 /* All-gather count fp64 per rank (host in, host out: recv holds nranks*count). */
 int lfm_farm_allgather_f64(lfm_ctx* ctx, const double* send, int64_t count, double* recv);
 int lfm_farm_destroy(lfm_ctx* ctx);
-
-/* ------------------------------------------------------------ diagnostics */
-/* Throughput probe of v_mfma_f64_16x16x4_f64: *tflops over a grid of nblocks x 256. */
-int lfm_probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double* ms);
-/* Shader cycles per v_mfma_f64_16x16x4_f64 per wave (8 chains) and the shader clock (MHz)
- * seen by block 0 of an nblocks x 256 grid. */
-int lfm_probe_mfma_f64_cycles(lfm_ctx* ctx, int nblocks, int iters, double* cyc_per_mfma,
-                              double* mhz);
-/* v_mfma_f64_4x4x4_4b_f64 on one wave: per-lane a, b, c [64] -> d[5][64] for
- * (CBSZ, ABID) = (0,0), (2,0), (2,1), (2,2), (2,3). */
-int lfm_probe_mfma4_layout(lfm_ctx* ctx, const double* a, const double* b, const double* c,
-                           double* d);
-/* fp64 rate probes: which = 0 VALU v_fma_f64, 1 v_mfma_f64_4x4x4_4b_f64 (TFLOP/s). */
-int lfm_probe_rate(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflops);
-/* Trailing-update kernel alone on a T x T grid of 128-tiles, depth kd (128 | 256),
- * cio = 0 skips the C tile read/write: average us/launch. */
-int lfm_probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us);
-/* Panel-solve kernel alone (variant 2 | 3) over `rows` rows: average us/launch. */
-int lfm_probe_trsm(lfm_ctx* ctx, int variant, int rows, int reps, double* us);
-/* Diagonal-block factor kernel with phase mask (bit0 register factor, bit1 panel,
- * bit2 trailing update, bit3 HBM load/store; 15 = product kernel): average us/launch. */
-int lfm_probe_potrf(lfm_ctx* ctx, int mask, int reps, double* us);
-/* The diagonal factor's pivot reciprocal square root (v_rsq_f64 + one Newton step) on x[n]. */
-int lfm_probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y);
-/* Layout probe: D = A(16x4) * B(4x16) on one wave; A,B,D row-major host arrays. */
-int lfm_probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,56 @@
+/*
+ * lfm_diag.h — diagnostics of liblfm.so, kept out of the product ABI (include/lfm.h).
+ *
+ * Hardware probes (MFMA lane maps and issue rates, the trailing-update kernel alone) and
+ * phase timestamps of the schedule-3 factor chain. They back the measurements quoted in
+ * DESIGN.md and the layout / pivot known-answer tests; no product call path uses them.
+ * Same conventions as lfm.h (LFM_OK / LFM_E_* return codes, synchronous at return).
+ */
+#ifndef LFM_DIAG_H
+#define LFM_DIAG_H
+
+#include <stdint.h>
+
+#include "lfm.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Phase timestamps (s_memrealtime, 100 MHz) of the schedule-3 factor chain, 16 per
+ * super-panel step. enable = 1 arms them; enable = 0 copies up to max out and disarms. */
+int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max);
+
+/* The diagonal factor's pivot reciprocal square root (v_rsq_f64 + one Newton step) on x[n]. */
+int lfm_probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y);
+
+/* Layout probe: D = A(16x4) * B(4x16) on one wave through v_mfma_f64_16x16x4_f64;
+ * A, B, D row-major host arrays. */
+int lfm_probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d);
+
+/* v_mfma_f64_4x4x4_4b_f64 on one wave: per-lane a, b, c [64] -> d[5][64] for
+ * (CBSZ, ABID) = (0,0), (2,0), (2,1), (2,2), (2,3). */
+int lfm_probe_mfma4_layout(lfm_ctx* ctx, const double* a, const double* b, const double* c,
+                           double* d);
+
+/* Throughput of v_mfma_f64_16x16x4_f64 over a grid of nblocks x 256 threads. */
+int lfm_probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double* ms);
+
+/* Shader cycles per v_mfma_f64_16x16x4_f64 per wave (8 chains) and the shader clock (MHz)
+ * seen by block 0 of an nblocks x 256 grid. */
+int lfm_probe_mfma_f64_cycles(lfm_ctx* ctx, int nblocks, int iters, double* cyc_per_mfma,
+                              double* mhz);
+
+/* fp64 rate probes (TFLOP/s): which = 0 VALU v_fma_f64, 1 v_mfma_f64_4x4x4_4b_f64,
+ * 2 / 3 the 16x16x4 / 4x4x4_4b MFMA on pseudo-random register operands. */
+int lfm_probe_rate(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflops);
+
+/* The trailing-update kernel alone (64-row slabs) on a T x T grid of 128-tiles, depth kd:
+ * average us per launch. cio bit 0: C tile I/O (else MFMAs only), bit 3: random operands,
+ * bit 4: on schedule 3's CU-masked bulk stream. */
+int lfm_probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LFM_DIAG_H */

@@ -1,0 +1,88 @@
+"""ctypes binding of oracle/liblfm_cpu.so — TEST INFRASTRUCTURE ONLY.
+
+The C++ / OpenMP CPU restatement of the reference's MLL path (oracle/lfm_cpu.cpp): the
+full-size parity check of the GPU path and bench.py's timed ``cpu_baseline``. Only
+``tests/``, ``__graft_entry__`` and ``bench.py``'s ``cpu_baseline`` leg import it; the product
+package never does. Build: ``make -C oracle`` (``__graft_entry__.build()`` runs it).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_double, c_int, c_int64
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblfm_cpu.so")
+_dp = POINTER(c_double)
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FileNotFoundError(f"{LIB_PATH} missing: run `make -C oracle`")
+        lib = ctypes.CDLL(LIB_PATH)
+        lib.lfm_cpu_gram.restype = c_int
+        lib.lfm_cpu_gram.argtypes = [_dp, c_int64, c_int64, _dp, _dp, c_double, c_double, _dp,
+                                     c_int64, c_int]
+        lib.lfm_cpu_potrf.restype = c_int64
+        lib.lfm_cpu_potrf.argtypes = [_dp, c_int64, c_int64, c_int]
+        lib.lfm_cpu_mll.restype = c_double
+        lib.lfm_cpu_mll.argtypes = [_dp, _dp, c_int64, c_int64, _dp, _dp, _dp, c_double, c_double,
+                                    c_double, c_int, c_int, _dp, _dp]
+        _lib = lib
+    return _lib
+
+
+def _f64(a):
+    return np.ascontiguousarray(np.asarray(a, np.float64))
+
+
+def _p(a):
+    return a.ctypes.data_as(_dp)
+
+
+def mll(x, y, D, S, B, l, obs_stddev, jitter, negative=False, threads=0, work=None):
+    """CustomConjMLL(negative).step on the CPU. Returns (value, info) with info = dict(mll,
+    logdet, quad, t_gram, t_chol, t_solve, fail, threads). `work`: optional n x n float64
+    scratch (reused across calls)."""
+    lib = load()
+    x, y, D, S, B = (_f64(v) for v in (x, y, D, S, B))
+    x = x.reshape(-1, 3)
+    n = x.shape[0]
+    info = np.zeros(8)
+    wp = None
+    if work is not None:
+        assert work.dtype == np.float64 and work.size >= n * n and work.flags.c_contiguous
+        wp = _p(work)
+    v = lib.lfm_cpu_mll(_p(x), _p(y.reshape(-1)), n, D.size, _p(D), _p(S), _p(B), float(l),
+                        float(obs_stddev), float(jitter), int(bool(negative)), int(threads), wp,
+                        _p(info))
+    keys = ["mll", "logdet", "quad", "t_gram", "t_chol", "t_solve", "fail", "threads"]
+    return float(v), dict(zip(keys, info.tolist()))
+
+
+def gram_lower(x, D, S, l, diag_add=0.0, threads=0):
+    """Lower triangle of K(x, x) + diag_add I (upper part zero)."""
+    lib = load()
+    x, D, S = (_f64(v) for v in (x, D, S))
+    x = x.reshape(-1, 3)
+    n = x.shape[0]
+    K = np.zeros((n, n))
+    rc = lib.lfm_cpu_gram(_p(x), n, D.size, _p(D), _p(S), float(l), float(diag_add), _p(K), n,
+                          int(threads))
+    if rc:
+        raise ValueError("lfm_cpu_gram: bad arguments")
+    return K
+
+
+def potrf(A, threads=0):
+    """In-place lower Cholesky of a C-contiguous float64 square array; returns the failing
+    pivot or -1."""
+    lib = load()
+    assert A.dtype == np.float64 and A.flags.c_contiguous and A.shape[0] == A.shape[1]
+    return int(lib.lfm_cpu_potrf(_p(A), A.shape[0], A.shape[0], int(threads)))

@@ -1,7 +1,7 @@
 """Interleaved A/B timing of per-call settings (env variables read by chol_factor_solve on
 every call) in one context at N = 16384: rounds of [variant 0, variant 1, ...], so thermal /
 power drift over the run hits every variant alike. Usage:
-    python scripts/ab.py "LFM_W4_MIN=6144" "LFM_W4_MIN=5120 LFM_W8_MIN=8192" ...
+    python scripts/ab.py "LFM_W4_MIN=6144" "LFM_W4_MIN=5120 LFM_W2_MIN=4096" ...
 Prints one line per variant: median / min ms per evaluation over the rounds, MLL."""
 import os
 import sys

@@ -211,3 +211,27 @@ def test_full_size_golden_rows_regenerate():
         n = x.shape[0]
         mll = -0.5 * (n * math.log(2 * math.pi) + float(g[tag + "_logdet"]) + float(g[tag + "_quad"]))
         assert mll == pytest.approx(float(g[tag + "_mll"]), rel=1e-15)
+
+
+def test_unselected_branch_overflow_diverges_deliberately():
+    """The reference evaluates all four kernel branches and multiplies three by 0
+    (model.py:188-193): where an unselected branch overflows, 0 * inf poisons the entry with
+    NaN. A latent/latent pair (flags 0, gene index -1 -> the last gene, utils.py:285) whose
+    wrapped gene has D l / 2 = 40 (exp(gamma^2) = inf in kernel_xx) is NaN in the reference
+    (O.kernel_pairs) but finite in the device semantics, which evaluate only the selected
+    branch (lfm_math.h kernel_ref; O.kernel_scalar restates that): kff = exp(-dt^2 / (2 l)).
+    This is the documented deviation; every finite reference entry agrees."""
+    D = np.array([0.4, 40.0])
+    S = np.array([1.0, 1.0])
+    a = np.array([1.0, -1.0, 0.0])
+    b = np.array([4.0, -1.0, 0.0])
+    with np.errstate(all="ignore"):
+        ref = O.kernel_pairs(a[None, :], b[None, :], D, S, 2.0)[0]
+    assert np.isnan(ref)
+    dev = O.kernel_scalar(a, b, D, S, 2.0)
+    assert dev == math.exp(-(3.0**2) / (2 * 2.0))
+    # a pair whose branches are all finite agrees exactly between the two semantics
+    a2 = np.array([1.0, 0.0, 0.0])
+    b2 = np.array([4.0, 0.0, 1.0])
+    assert abs(O.kernel_pairs(a2[None, :], b2[None, :], D, S, 2.0)[0] -
+               O.kernel_scalar(a2, b2, D, S, 2.0)) < 1e-14
