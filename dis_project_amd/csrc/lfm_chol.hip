@@ -943,7 +943,16 @@ struct StepArgs {
   unsigned* xready;  // NULL: no chain waits on this launch
   int lead;
   unsigned spin;     // poll bound of every device-side wait (PANEL_TIMEOUT past it)
+  unsigned long long* stamps;  // diagnostics (NULL: off): [4] launch stamps, lfm_diag.h
 };
+
+// Diagnostics: atomic max of the 100 MHz clock (or of its bitwise NOT: the earliest start)
+__device__ __forceinline__ void stamp_max(unsigned long long* p, bool negate = false) {
+  if (p && threadIdx.x == 0) {
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    __hip_atomic_fetch_max(p, negate ? ~t : t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 __device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
   __builtin_amdgcn_s_waitcnt(0);  // this thread's write-through stores have completed
@@ -969,6 +978,8 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
   const int64_t u = lo + (b - base) / 8;
   if (u >= hi) return;
   const int role = seg + 1;
+  unsigned long long* const st = g.stamps;
+  if (st) stamp_max(st, true);
   if (role == 1) {
     // device-coherent stores + a counter bump once they have completed: the tall units read
     // these rows with device-coherent loads (no L2 writeback / invalidate on either side)
@@ -980,12 +991,21 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
       __hip_atomic_fetch_add(&g.a_done[trow], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0 && g.xready && trow < g.wn + g.lead)
       __hip_atomic_fetch_add(g.xready, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (st) {
+      stamp_max(st + 1);
+      stamp_max(st + 3);
+    }
     return;
   }
   if (role == 2) {
     const bool lead = syrk_unit<true, 64>(g.A, g.lda, g.s0, g.px, g.kd, g.T, g.wn, g.T, u, 0, sP,
                                           g.xready ? g.wn + g.lead : 0, g.n);
     if (lead) bump_after_stores(g.xready);
+    if (st) {
+      __syncthreads();
+      stamp_max(st + 1);
+      stamp_max(st + 3);
+    }
     return;
   }
   // tall unit (row slab rb, column block cb) of step s + 1
@@ -1009,6 +1029,7 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
       if (threadIdx.x == 0) atomicMin(g.status, PANEL_TIMEOUT);
       return;
     }
+    if (st) stamp_max(st + 2);
   }
   const int W = g.tw * NB;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1029,6 +1050,10 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
       Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
       if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + cb * NB + wc + jr * 16 + li] = acc[ir][jr];
     }
+  if (st) {
+    __syncthreads();
+    stamp_max(st + 3);
+  }
 }
 
 // ---------------------------------------------------------- fused panel
@@ -1984,6 +2009,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         StepArgs g{};
         update_args(g, s);
         tall_args(g, s + 1);
+        if (ctx->dbg_stamps) g.stamps = ctx->dbg_stamps + 256 * 16 + 4 * (size_t)std::min(s, 255);
         g.a_done = a_done + (size_t)s * Tmax;
         // the block after next: its tiles (rest) and rows (ahead) feed chain(s + 2)
         if (s + 2 < S) {

@@ -87,7 +87,8 @@ struct lfm_ctx {
   double* result = nullptr;                      // [0..] scalar results
   double* gacc = nullptr; size_t gacc_bytes = 0; // gradient accumulators + output
 
-  unsigned long long* dbg_stamps = nullptr;     // chain phase stamps (lfm_debug_stamps), 256 x 16
+  unsigned long long* dbg_stamps = nullptr;     // lfm_debug_stamps: chain phases 256 x 16, then
+                                                // step launches 256 x 4
 
   // pinned host staging
   double* hpin = nullptr; size_t hpin_bytes = 0;

@@ -17,8 +17,12 @@
 extern "C" {
 #endif
 
-/* Phase timestamps (s_memrealtime, 100 MHz) of the schedule-3 factor chain, 16 per
- * super-panel step. enable = 1 arms them; enable = 0 copies up to max out and disarms. */
+/* Timestamps (s_memrealtime, 100 MHz) of the schedule-3 factorisation: 256 rows of 16
+ * chain-phase stamps per super-panel step, then 256 rows of 4 per main-stream step launch s
+ * (s's update + the tall solve of s + 1): [0] bitwise NOT of the first unit's start,
+ * [1] the last update unit's end, [2] the last tall unit's wait end (the chain's factor
+ * landed), [3] the last unit's end. enable = 1 arms them; enable = 0 copies up to max
+ * (<= 256 * 20) values out and disarms. */
 int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max);
 
 /* The diagonal factor's pivot reciprocal square root (v_rsq_f64 + one Newton step) on x[n]. */

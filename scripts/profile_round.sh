@@ -1,18 +1,20 @@
 #!/bin/bash
 # Round profile set (run on the GPU box from the repo root):
-#   1. rocprofv3 --kernel-trace --stats of a short bench            -> gpurun_out/prof_trace/
-#   2. two PMC passes (FETCH_SIZE, WRITE_SIZE), counters only       -> gpurun_out/prof_fetch|prof_write/
+#   1. rocprofv3 --kernel-trace --stats of bench.py (5 timed + 2 warm C2 evaluations); the
+#      traced run's own JSON line is kept beside the stats (gpurun_out/prof_trace_bench.json)
+#   2. two PMC passes (FETCH_SIZE, WRITE_SIZE), counters only, schedule 3 event-ordered
 #   3. summarize_profile.py: profiles/syrk_traffic.json (read by bench.py's roofline.traffic)
-#   4. bench.py (default workload, with the CPU baseline)            -> gpurun_out/bench_<R>.json
+#   4. the untraced bench.py (default workload, with the CPU baseline) -> gpurun_out/bench_<R>.json
 # Each GPU step has its own time limit; the script stops at the first failure. Afterwards run
 # `python scripts/summarize_profile.py <R> gpurun_out/bench_<R>.json` in the container to
 # regenerate the same profiles/ files from the merged gpurun_out/.
 set -u
 export TMPDIR=/tmp
-R=${1:-r01}
+R=${1:-r02}
 STEPS=${STEPS:-10}
 scripts/gpu_step.sh prof_trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace \
-  -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit $?
+  -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline || exit $?
+grep '^{' gpurun_out/prof_trace.log | tail -1 > gpurun_out/prof_trace_bench.json || exit $?
 LFM_S3_EVENTS=1 scripts/gpu_step.sh prof_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch \
   -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile || exit $?
 LFM_S3_EVENTS=1 scripts/gpu_step.sh prof_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write \

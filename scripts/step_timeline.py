@@ -1,0 +1,107 @@
+"""Per-step timeline of the schedule-3 factorisation at N = 16384 from device stamps
+(lfm_debug_stamps, 100 MHz s_memrealtime; include/lfm_diag.h): for each main-stream step
+launch s (step s's trailing update + the tall solve of super-panel s + 1) the launch span,
+the update units' span and rate, how long the tall units' last wait ran past the update
+(the chain-bound exposure), and the chain (s + 1)'s own span.
+
+    python scripts/step_timeline.py [--json out.json]
+"""
+import ctypes
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
+from dis_project_amd import _lib, configs  # noqa: E402
+
+NB = 128
+
+
+def plan(n):
+    """Schedule 3's step plan (lfm_chol.hip chol_factor_solve, default LFM_W4_MIN/W2_MIN)."""
+    Mp = (n + 1 + NB - 1) // NB * NB
+    nblk = (n + NB - 1) // NB
+    w4 = int(os.environ.get("LFM_W4_MIN", 6144))
+    w2 = int(os.environ.get("LFM_W2_MIN", 5120))
+    steps, k = [], 0
+    while k < nblk:
+        m = Mp - k * NB
+        w = 4 if (m >= w4 and k + 4 <= nblk) else 2 if (m >= w2 and k + 2 <= nblk) else 1
+        if k == 0:
+            w = 1
+        steps.append((k, w))
+        k += w
+    return steps
+
+
+def main():
+    work = configs.c2()
+    n = work.n
+    x = np.ascontiguousarray(work.data.X)
+    y = np.ascontiguousarray(work.data.y.reshape(-1))
+    ctx = _lib.Context(0)
+    lib, h = ctx.lib, ctx.handle
+    dx, dy = _lib.c_void_p(), _lib.c_void_p()
+    ctx.check(lib.lfm_dev_alloc(h, x.nbytes, ctypes.byref(dx)))
+    ctx.check(lib.lfm_dev_alloc(h, y.nbytes, ctypes.byref(dy)))
+    ctx.check(lib.lfm_memcpy_h2d(h, dx, x.ctypes.data, x.nbytes))
+    ctx.check(lib.lfm_memcpy_h2d(h, dy, y.ctypes.data, y.nbytes))
+    out = np.empty(1)
+    hp = work.model.hyp()
+    import time
+    for _ in range(3):
+        ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, n, hp.ref, 0, _lib.dptr(out)))
+    t0 = time.perf_counter()
+    for _ in range(5):
+        ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, n, hp.ref, 0, _lib.dptr(out)))
+    plain_ms = (time.perf_counter() - t0) / 5 * 1e3
+    ctx.check(lib.lfm_debug_stamps(h, 1, None, 0))
+    t0 = time.perf_counter()
+    ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, n, hp.ref, 0, _lib.dptr(out)))
+    stamped_ms = (time.perf_counter() - t0) * 1e3
+    buf = (ctypes.c_ulonglong * (256 * 20))()
+    ctx.check(lib.lfm_debug_stamps(h, 0, buf, 256 * 20))
+    allst = np.frombuffer(buf, dtype=np.uint64)
+    ch = allst[: 256 * 16].reshape(256, 16).astype(np.int64)
+    sp = allst[256 * 16:].reshape(256, 4).copy()
+    steps = plan(n)
+    S = len(steps)
+    first = ~sp[:, 0]  # earliest unit start (stored as the max of the bitwise NOT)
+    t_ref = int(min(int(ch[0][0]), int(first[0])))
+    us = lambda t: (int(t) - t_ref) * 0.01  # noqa: E731
+    rows = []
+    tot_exposed = 0.0
+    print(f"N={n}: {S} steps, plain {plain_ms:.2f} ms/eval, stamped {stamped_ms:.2f} ms")
+    print(" s  w  m_tr   launch[us]  update[us] TF/s  exposed[us] chain(s+1)[us]")
+    for s in range(S - 1):
+        k, w = steps[s]
+        K1 = (k + w) * NB
+        m = n - K1
+        wn = steps[s + 1][1]
+        d = min(wn * NB, m)
+        alg = 2.0 * w * NB * (m * (m + 1) / 2 + m - d * (d + 1) / 2)
+        st0, upd_end, wait_end, end = int(first[s]), int(sp[s][1]), int(sp[s][2]), int(sp[s][3])
+        launch = (end - st0) * 0.01
+        upd = (upd_end - st0) * 0.01 if upd_end else 0.0
+        exposed = max(0.0, (wait_end - upd_end) * 0.01) if wait_end and upd_end else 0.0
+        tot_exposed += exposed
+        c = ch[s + 1]
+        chain = (c[15] - c[0]) * 0.01 if c[0] and c[15] else float("nan")
+        tf = alg / (upd * 1e-6) / 1e12 if upd > 0 else 0.0
+        rows.append(dict(s=s, w=w, m=m, start_us=us(st0), launch_us=launch, update_us=upd,
+                         update_tflops=tf, exposed_us=exposed, chain_next_us=chain,
+                         chain_next_start_us=us(c[0]) if c[0] else None,
+                         chain_next_done_us=us(c[15]) if c[15] else None))
+        print(f"{s:2d} {w:2d} {m:6d} {launch:10.1f} {upd:10.1f} {tf:5.1f} {exposed:10.1f} {chain:10.1f}")
+    end_all = max(int(v) for v in sp[: S - 1, 3])
+    print(f"span first unit -> last unit: {(end_all - int(first[0])) * 0.01:.1f} us; "
+          f"chain-bound exposure (tall units waiting past the update) {tot_exposed:.1f} us")
+    if len(sys.argv) > 2 and sys.argv[1] == "--json":
+        json.dump({"n": n, "plain_ms": plain_ms, "stamped_ms": stamped_ms,
+                   "exposed_us": tot_exposed, "steps": rows}, open(sys.argv[2], "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -36,8 +36,13 @@ def main():
     stats = os.path.join(OUT, "prof_trace", "run_kernel_stats.csv")
     shutil.copy(stats, os.path.join(PROF, f"{rnd}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
-    lines = [f"# {rnd}: rocprofv3 --kernel-trace --stats, `bench.py --steps 3 --warmup 1` "
-             "(4 evaluations at N = 16384)", "",
+    traced = None
+    tb = os.path.join(OUT, "prof_trace_bench.json")
+    if os.path.exists(tb) and open(tb).read().strip():
+        traced = json.loads(open(tb).read().strip().splitlines()[-1])
+    evals_traced = (traced["steps"] + traced["warmup"]) if traced else None
+    lines = [f"# {rnd}: rocprofv3 --kernel-trace --stats, `bench.py --steps 5 --warmup 2 "
+             "--no-cpu-baseline` (7 evaluations at N = 16384)", "",
              "| kernel | calls | avg us | total ms | share % |", "|---|---|---|---|---|"]
     for r in rows:
         lines.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
@@ -81,6 +86,31 @@ def main():
                    "hbm_bytes_per_eval": total / evals, "evals": evals,
                    "hbm_bytes_per_launch": total / max(1, launches), "launches": launches},
                   open(os.path.join(PROF, "syrk_traffic.json"), "w"), indent=1)
+    # the roofline recomputed from the trace: the step kernel's rocprof average duration and the
+    # traced bench line's algorithmic flops per launch (lfm_kstat.flops, the same launches)
+    step = next((r for r in rows if short(r["Name"]).startswith("step_kernel")), None)
+    if step and traced and traced.get("roofline"):
+        rf = traced["roofline"]
+        avg_s = float(step["AverageNs"]) * 1e-9
+        ach = rf["flops_per_launch"] / avg_s / 1e12
+        calls_per_eval = int(step["Calls"]) / evals_traced
+        kern_ms = float(step["TotalDurationNs"]) / 1e6 / evals_traced
+        lines += ["", "Roofline of step_kernel from this trace (bench.py prices it the same way):", "",
+                  f"- algorithmic flops per launch (traced bench line): {rf['flops_per_launch']:.4e} "
+                  f"(issued: {rf['issued_flops_per_launch']:.4e})",
+                  f"- rocprof average duration: {avg_s * 1e6:.1f} us over {step['Calls']} launches "
+                  f"({calls_per_eval:.0f} per evaluation)",
+                  f"- achieved {ach:.2f} TFLOP/s = **{ach / 78.6:.3f}** of 78.6 (traced bench line's own "
+                  f"HIP-event frac: {rf['frac']:.3f})",
+                  f"- step_kernel time per evaluation {kern_ms:.2f} ms; the traced run's wall "
+                  f"{traced['ms_per_step']:.2f} ms per evaluation (consecutive step launches overlap "
+                  "at their boundaries, so the kernel sum can exceed the wall)"]
+        json.dump({"round": rnd, "step_kernel_avg_us": avg_s * 1e6, "calls_per_eval": calls_per_eval,
+                   "flops_per_launch": rf["flops_per_launch"], "achieved_tflops": ach,
+                   "frac": ach / 78.6, "bench_traced_frac": rf["frac"],
+                   "step_kernel_ms_per_eval": kern_ms, "traced_wall_ms_per_eval": traced["ms_per_step"]},
+                  open(os.path.join(PROF, f"{rnd}_roofline.json"), "w"), indent=1)
+        shutil.copy(tb, os.path.join(PROF, f"{rnd}_bench_traced.json"))
     lines += ["", "HBM per launch (PMC, separate passes; read side x2 per MI355X_MICROARCH.md §HBM):",
               "", "| kernel | launches | read B/launch (x2) | write B/launch |", "|---|---|---|---|"]
     for k, v in sorted(out.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"]):

@@ -53,6 +53,28 @@ def test_mfma_f64_layout(lfm):
     np.testing.assert_array_equal(d, a @ b)
 
 
+def test_mfma4_layout(lfm):
+    """v_mfma_f64_4x4x4_4b_f64 lane maps the trailing update relies on (lfm_chol.hip
+    gemm_accumulate): block g = (lane >> 2) & 3 holds A_g[i][k] at lane 16k + 4g + i,
+    B_g[k][j] at lane 16k + 4g + j, C/D_g[i][j] at lane 16i + 4g + j. (The CBSZ / ABID
+    A-broadcast fields do not broadcast on the f64 form: one-hot probes of every mode give
+    this same map, scripts/probe_mfma4_layout.py — so A is replicated in registers.)"""
+    from dis_project_amd._lib import dptr, get_context
+
+    rng = np.random.default_rng(4)
+    a, b, c = (rng.integers(-4, 5, 64).astype(np.float64) for _ in range(3))
+    d = np.empty(5 * 64)
+    ctx = get_context()
+    ctx.check(ctx.lib.lfm_probe_mfma4_layout(ctx.handle, dptr(a), dptr(b), dptr(c), dptr(d)))
+    d = d.reshape(5, 64)
+    for g in range(4):
+        A = np.array([[a[16 * k + 4 * g + i] for k in range(4)] for i in range(4)])
+        B = np.array([[b[16 * k + 4 * g + j] for j in range(4)] for k in range(4)])
+        C = np.array([[c[16 * i + 4 * g + j] for j in range(4)] for i in range(4)])
+        got = np.array([[d[0, 16 * i + 4 * g + j] for j in range(4)] for i in range(4)])
+        np.testing.assert_array_equal(got, A @ B + C, err_msg=f"block {g}")
+
+
 # --------------------------------------------------------------- kernel
 def test_h_vs_oracle_and_mpmath(lfm):
     rng = np.random.default_rng(1)
