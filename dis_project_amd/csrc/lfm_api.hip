@@ -1053,7 +1053,7 @@ int lfm_probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y) {
 int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max) {
   if (!ctx) return LFM_E_ARG;
   DeviceGuard g(ctx->device);
-  const size_t cnt = 256 * 20;  // 256 chain rows of 16, then 256 step-launch rows of 4
+  const size_t cnt = 256 * 24;  // 256 chain rows of 16, then 256 step-launch rows of 8
   if (enable) {
     if (!ctx->dbg_stamps) {
       hipError_t e = hipMalloc((void**)&ctx->dbg_stamps, cnt * 8);

@@ -144,6 +144,9 @@ __device__ __forceinline__ void pin16(double (&p)[16]) {
 #ifndef LFM_COH_NT
 #define LFM_COH_NT 1
 #endif
+#ifndef LFM_KK_UNROLL
+#define LFM_KK_UNROLL 1
+#endif
 typedef double double2v __attribute__((ext_vector_type(2)));
 template <bool COH>
 __device__ __forceinline__ double2 ld2(const double* p) {
@@ -764,7 +767,7 @@ __device__ __forceinline__ void gemm_accumulate(const double* __restrict__ pi, i
     __syncthreads();
     if (k0 + KS < kd) gload(k0 + KS);
     {
-#pragma unroll 1
+#pragma unroll LFM_KK_UNROLL
       for (int kk = 0; kk < KS; kk += 4) {
         double bb[4];
 #pragma unroll
@@ -796,6 +799,11 @@ struct Panel {
 #ifndef LFM_SLAB_WGS
 #define LFM_SLAB_WGS 3
 #endif
+// Bulk trailing update (step_kernel's update units): K depth of one LDS stage and the unroll
+// of the 4-deep MFMA steps within it
+#ifndef LFM_STEP_KS
+#define LFM_STEP_KS 16
+#endif
 // One TR x 128 work unit of a band / triangle launch: C -= P_i P_j^T over panel depth kd,
 // C the lower part of the trailing matrix of A starting at row / column s. b = the unit's
 // index in the enumeration below.
@@ -806,7 +814,8 @@ template <bool CIO, int TR, bool COH = false, int KS = KB, bool LDCOH = false>
 __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, int64_t s, Panel P,
                                           int kd, int T, int tj_lo, int tj_hi, int64_t b, int ti0,
                                           double (*__restrict__ sP)[KS + 1], int coh_lim = 0,
-                                          int64_t pad_after = INT64_MAX) {
+                                          int64_t pad_after = INT64_MAX,
+                                          int64_t pad_end = INT64_MAX) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
@@ -836,8 +845,9 @@ __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, i
   const int64_t i0 = s + (int64_t)ti * TR, j0 = s + (int64_t)tj * ST;
   const bool diag = i0 < j0 + ST;  // the tile reaches the diagonal: keep col <= row only
   const bool in_lead = (i0 - s) / ST < coh_lim && (j0 - s) / ST < coh_lim;
-  // rows past pad_after are identity padding of the augmented matrix: nothing reads their update
-  if (i0 > pad_after && !in_lead) return false;
+  // rows in (pad_after, pad_end) are identity padding of the augmented matrix (their panel
+  // entries are zero): nothing reads their update
+  if (i0 > pad_after && i0 < pad_end && !in_lead) return false;
   const bool coh = COH || in_lead;
   double* Cb = A + (i0 + wr + lk) * lda + j0 + wc + li;  // C[wr + lk][wc + li]
   const int ld4 = (int)(4 * lda);  // row-group stride (elements); 60 * ld4 < 2^31 for lda < 2^23
@@ -943,7 +953,9 @@ struct StepArgs {
   unsigned* xready;  // NULL: no chain waits on this launch
   int lead;
   unsigned spin;     // poll bound of every device-side wait (PANEL_TIMEOUT past it)
-  unsigned long long* stamps;  // diagnostics (NULL: off): [4] launch stamps, lfm_diag.h
+  unsigned long long* stamps;  // diagnostics (NULL: off): [8] launch stamps, lfm_diag.h
+  int64_t pad_end;   // rows in (n, pad_end) are skipped identity padding (INT64_MAX: every
+                     // row past n; n + 1: none)
 };
 
 // Diagnostics: atomic max of the 100 MHz clock (or of its bitwise NOT: the earliest start)
@@ -963,7 +975,9 @@ __device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
 
 
 __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
-  __shared__ double sP[64 + ST][KB + 1];
+  __shared__ double sPbuf[(64 + ST) * (LFM_STEP_KS + 1)];
+  double (*sP)[KB + 1] = reinterpret_cast<double (*)[KB + 1]>(sPbuf);
+  double (*sPu)[LFM_STEP_KS + 1] = reinterpret_cast<double (*)[LFM_STEP_KS + 1]>(sPbuf);
   const int64_t b = blockIdx.x;
   // roles in blockIdx order: ahead (1), rest (2), tall (3), each padded to a multiple of 8
   const int cnt[3] = {g.na, g.nr, g.nt};
@@ -983,7 +997,8 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
   if (role == 1) {
     // device-coherent stores + a counter bump once they have completed: the tall units read
     // these rows with device-coherent loads (no L2 writeback / invalidate on either side)
-    syrk_unit<true, 64, true>(g.A, g.lda, g.s0, g.px, g.kd, g.T, 0, g.wn, u, g.wn, sP, 0, g.n);
+    syrk_unit<true, 64, true, LFM_STEP_KS>(g.A, g.lda, g.s0, g.px, g.kd, g.T, 0, g.wn, u, g.wn, sPu,
+                                           0, g.n, g.pad_end);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     const int trow = g.wn + (int)(u % (2 * (g.T - g.wn))) / 2;  // 128-tile row of the unit
@@ -998,13 +1013,26 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
     return;
   }
   if (role == 2) {
-    const bool lead = syrk_unit<true, 64>(g.A, g.lda, g.s0, g.px, g.kd, g.T, g.wn, g.T, u, 0, sP,
-                                          g.xready ? g.wn + g.lead : 0, g.n);
+    unsigned long long c0 = 0, r0 = 0;
+    if (st) {
+      c0 = __builtin_amdgcn_s_memtime();
+      r0 = __builtin_amdgcn_s_memrealtime();
+    }
+    const bool lead = syrk_unit<true, 64, false, LFM_STEP_KS>(g.A, g.lda, g.s0, g.px, g.kd, g.T,
+                                                              g.wn, g.T, u, 0, sPu,
+                                                              g.xready ? g.wn + g.lead : 0, g.n,
+                                                              g.pad_end);
     if (lead) bump_after_stores(g.xready);
     if (st) {
       __syncthreads();
       stamp_max(st + 1);
       stamp_max(st + 3);
+      if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(st + 4, __builtin_amdgcn_s_memtime() - c0, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(st + 5, __builtin_amdgcn_s_memrealtime() - r0, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     return;
   }
@@ -1013,14 +1041,16 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
   const int64_t nrb = g.nt / g.tw;
   const int cb = g.tw - 1 - (int)(u / nrb);
   const int64_t i0 = g.tr0 + (u % nrb) * 64;
-  if (i0 > g.n) return;  // identity padding rows: their X is never read
+  if (i0 > g.n && i0 < g.pad_end) return;  // identity padding rows: their X is never read
   {
     __shared__ int ok;
     // relaxed polling and device-coherent operand loads below instead of an acquire fence:
     // an agent-scope acquire invalidates this XCD's L2 under the running bulk units
     if (threadIdx.x == 0) {
       bool good = !g.chain_done || spin_until<false>(g.chain_done, 1u, g.spin);
-      if (good && g.a_done)
+      // rows past step s's update (bordered: the border rows that entered the window with
+      // super-panel s + 1, zero in every earlier panel column) have no ahead unit to wait for
+      if (good && g.a_done && (i0 - g.s0) / ST < g.T)
         good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], 2u * g.wn, g.spin);
       ok = good;
     }
@@ -1791,7 +1821,9 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   const int64_t nblk = bordered ? Mp / NB : npb;
   int r = ensure(ctx, (void**)&ctx->parts, &ctx->parts_cap, (size_t)nblk * sizeof(double));
   if (r) return r;
-  const bool s3 = ctx->sched == 3 && ctx->side_cus > 0 && mode == CHOL_MLL;
+  // schedule 3 for the MLL and for the bordered inverse (gradient); the Schur-complement
+  // posterior keeps schedule 1
+  const bool s3 = ctx->sched == 3 && ctx->side_cus > 0 && mode != CHOL_SCHUR;
   // Step plan: super-panels of w = 4 block columns while the trailing matrix has at least
   // LFM_W4_MIN rows, w = 2 down to LFM_W2_MIN, then w = 1, so the bulk trailing update runs
   // with depth 128 w (C traffic per flop / w). Schedule 3: w = 4 down to 6144 rows, then one
@@ -1833,6 +1865,14 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     main = ctx->m3;
     side = ctx->s3;
     hipStreamWaitEvent(main, ev[0], 0);
+    // the trailing matrix of a step whose super-panel ends at column K1: rows / columns
+    // [K1, Mp) (MLL), or the Mp-row window [K1, K1 + Mp) the identity border has reached
+    // (bordered: rows Mp + j are zero in panel columns < j; the window size is constant)
+    auto rows_end = [&](int64_t K1) { return bordered ? K1 + Mp : Mp; };
+    // MLL: rows past n are identity padding whose updates nothing reads; bordered: none is
+    // skipped (the border rows have real entries in the padding columns, which are
+    // eliminated too, so the padding rows' X must exist)
+    const int64_t pad_end = bordered ? n + 1 : INT64_MAX;
     int wmax = 1;
     for (const auto& st : steps) wmax = std::max(wmax, st.second);
     const int64_t Wmax = (int64_t)wmax * NB, Tmax = Mp / ST + 1;
@@ -1904,10 +1944,11 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     // tall units of step s: rows [K1_s, Mp) x w_s column blocks
     auto tall_units = [&](int s) {
       const int64_t K1 = (steps[s].first + steps[s].second) * NB;
-      return (int)((Mp - K1) / 64 * steps[s].second);
+      return (int)((rows_end(K1) - K1) / 64 * steps[s].second);
     };
     auto launch_step = [&](StepArgs& g) {
       g.n = n;  // padding rows past n are skipped
+      g.pad_end = pad_end;
       g.spin = ctx->spin_limit;
       const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 + (int64_t)(g.nr + 7) / 8 * 8 +
                            (int64_t)(g.nt + 7) / 8 * 8;
@@ -1921,12 +1962,15 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
                             (double)g.nt * 64 * ST * NB * (g.tw + 1);
       double alg = 0.0;
       if (g.na + g.nr > 0) {
-        const double m = (double)(n - g.s0), d = std::min<double>(g.wn * NB, m);
-        alg += 2.0 * g.kd * (m * (m + 1) / 2 + m - d * (d + 1) / 2);
+        // bordered: the whole Mp-row window is algorithmic (Cholesky + inverse = Mp^3)
+        const double m = bordered ? (double)Mp : (double)(n - g.s0);
+        const double d = std::min<double>(g.wn * NB, m);
+        alg += 2.0 * g.kd * (m * (m + 1) / 2 + (bordered ? 0.0 : m) - d * (d + 1) / 2);
       }
       if (g.nt > 0) {
         const double W2 = (double)g.tw * NB;
-        alg += (double)std::max<int64_t>(0, n + 1 - g.tr0) * W2 * W2;
+        const int64_t rows = bordered ? rows_end(g.tk0) - g.tr0 : n + 1 - g.tr0;
+        alg += (double)std::max<int64_t>(0, rows) * W2 * W2;
       }
       hipEvent_t pe;
       prof_begin(ctx, K_SYRK, &pe, main);
@@ -1949,11 +1993,12 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.chain_done = chain_done + s;
       g.status = ctx->status;
     };
-    // update of step s (trailing matrix from K1_s), excluding the next diagonal block
+    // update of step s (trailing matrix from K1_s), excluding the next diagonal block (none
+    // after the last super-panel: the bordered mode's final update of its border block)
     auto update_args = [&](StepArgs& g, int s) {
       const int64_t K1 = (steps[s].first + steps[s].second) * NB;
-      const int W = steps[s].second * NB, wn = steps[s + 1].second;
-      const int T = (int)((Mp - K1) / ST);
+      const int W = steps[s].second * NB, wn = s + 1 < S ? steps[s + 1].second : 0;
+      const int T = (int)((rows_end(K1) - K1) / ST);
       g.A = A;
       g.lda = lda;
       g.s0 = K1;
@@ -1996,6 +2041,11 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
           hipEventRecord(evc[s + 1], side);
         }
       }
+      if (bordered) {
+        StepArgs g{};  // the last super-panel's update of the border block
+        update_args(g, S - 1);
+        launch_step(g);
+      }
     } else {
       chain(0);
       {
@@ -2009,13 +2059,18 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         StepArgs g{};
         update_args(g, s);
         tall_args(g, s + 1);
-        if (ctx->dbg_stamps) g.stamps = ctx->dbg_stamps + 256 * 16 + 4 * (size_t)std::min(s, 255);
+        if (ctx->dbg_stamps) g.stamps = ctx->dbg_stamps + 256 * 16 + 8 * (size_t)std::min(s, 255);
         g.a_done = a_done + (size_t)s * Tmax;
         // the block after next: its tiles (rest) and rows (ahead) feed chain(s + 2)
         if (s + 2 < S) {
           g.xready = xready + s + 2;
           g.lead = steps[s + 2].second;
         }
+        launch_step(g);
+      }
+      if (bordered) {
+        StepArgs g{};  // the last super-panel's update of the border block (-S_aug^{-1})
+        update_args(g, S - 1);
         launch_step(g);
       }
     }

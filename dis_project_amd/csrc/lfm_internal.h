@@ -88,7 +88,7 @@ struct lfm_ctx {
   double* gacc = nullptr; size_t gacc_bytes = 0; // gradient accumulators + output
 
   unsigned long long* dbg_stamps = nullptr;     // lfm_debug_stamps: chain phases 256 x 16, then
-                                                // step launches 256 x 4
+                                                // step launches 256 x 8
 
   // pinned host staging
   double* hpin = nullptr; size_t hpin_bytes = 0;

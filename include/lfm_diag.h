@@ -18,11 +18,13 @@ extern "C" {
 #endif
 
 /* Timestamps (s_memrealtime, 100 MHz) of the schedule-3 factorisation: 256 rows of 16
- * chain-phase stamps per super-panel step, then 256 rows of 4 per main-stream step launch s
+ * chain-phase stamps per super-panel step, then 256 rows of 8 per main-stream step launch s
  * (s's update + the tall solve of s + 1): [0] bitwise NOT of the first unit's start,
  * [1] the last update unit's end, [2] the last tall unit's wait end (the chain's factor
- * landed), [3] the last unit's end. enable = 1 arms them; enable = 0 copies up to max
- * (<= 256 * 20) values out and disarms. */
+ * landed), [3] the last unit's end, [4] / [5] the sums over the update ('rest') units of
+ * their shader-clock (s_memtime) / 100 MHz (s_memrealtime) durations: the in-kernel clock
+ * is [4] / [5] x 100 MHz. enable = 1 arms them; enable = 0 copies up to max (<= 256 * 24)
+ * values out and disarms. */
 int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max);
 
 /* The diagonal factor's pivot reciprocal square root (v_rsq_f64 + one Newton step) on x[n]. */

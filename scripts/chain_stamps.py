@@ -26,9 +26,9 @@ for _ in range(3):
     ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, x.shape[0], hp.ref, 0, _lib.dptr(out)))
 ctx.check(lib.lfm_debug_stamps(h, 1, None, 0))
 ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, x.shape[0], hp.ref, 0, _lib.dptr(out)))
-buf = (ctypes.c_ulonglong * (256 * 16))()
-ctx.check(lib.lfm_debug_stamps(h, 0, buf, 256 * 16))
-st = np.frombuffer(buf, dtype=np.uint64).reshape(256, 16).astype(np.int64)
+buf = (ctypes.c_ulonglong * (256 * 24))()
+ctx.check(lib.lfm_debug_stamps(h, 0, buf, 256 * 24))
+st = np.frombuffer(buf, dtype=np.uint64)[:256 * 16].reshape(256, 16).astype(np.int64)
 for s in range(256):
     row = st[s]
     if row[0] == 0:

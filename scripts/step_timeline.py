@@ -61,11 +61,11 @@ def main():
     t0 = time.perf_counter()
     ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, n, hp.ref, 0, _lib.dptr(out)))
     stamped_ms = (time.perf_counter() - t0) * 1e3
-    buf = (ctypes.c_ulonglong * (256 * 20))()
-    ctx.check(lib.lfm_debug_stamps(h, 0, buf, 256 * 20))
+    buf = (ctypes.c_ulonglong * (256 * 24))()
+    ctx.check(lib.lfm_debug_stamps(h, 0, buf, 256 * 24))
     allst = np.frombuffer(buf, dtype=np.uint64)
     ch = allst[: 256 * 16].reshape(256, 16).astype(np.int64)
-    sp = allst[256 * 16:].reshape(256, 4).copy()
+    sp = allst[256 * 16:].reshape(256, 8).copy()
     steps = plan(n)
     S = len(steps)
     first = ~sp[:, 0]  # earliest unit start (stored as the max of the bitwise NOT)
@@ -74,7 +74,7 @@ def main():
     rows = []
     tot_exposed = 0.0
     print(f"N={n}: {S} steps, plain {plain_ms:.2f} ms/eval, stamped {stamped_ms:.2f} ms")
-    print(" s  w  m_tr   launch[us]  update[us] TF/s  exposed[us] chain(s+1)[us]")
+    print(" s  w  m_tr   launch[us]  update[us] TF/s  exposed[us] chain(s+1)[us] clock[MHz]")
     for s in range(S - 1):
         k, w = steps[s]
         K1 = (k + w) * NB
@@ -90,11 +90,13 @@ def main():
         c = ch[s + 1]
         chain = (c[15] - c[0]) * 0.01 if c[0] and c[15] else float("nan")
         tf = alg / (upd * 1e-6) / 1e12 if upd > 0 else 0.0
+        mhz = float(sp[s][4]) / float(sp[s][5]) * 100.0 if sp[s][5] else 0.0
         rows.append(dict(s=s, w=w, m=m, start_us=us(st0), launch_us=launch, update_us=upd,
                          update_tflops=tf, exposed_us=exposed, chain_next_us=chain,
                          chain_next_start_us=us(c[0]) if c[0] else None,
-                         chain_next_done_us=us(c[15]) if c[15] else None))
-        print(f"{s:2d} {w:2d} {m:6d} {launch:10.1f} {upd:10.1f} {tf:5.1f} {exposed:10.1f} {chain:10.1f}")
+                         chain_next_done_us=us(c[15]) if c[15] else None, update_clock_mhz=mhz))
+        print(f"{s:2d} {w:2d} {m:6d} {launch:10.1f} {upd:10.1f} {tf:5.1f} {exposed:10.1f} {chain:10.1f} "
+              f"{mhz:7.0f}")
     end_all = max(int(v) for v in sp[: S - 1, 3])
     print(f"span first unit -> last unit: {(end_all - int(first[0])) * 0.01:.1f} us; "
           f"chain-bound exposure (tall units waiting past the update) {tot_exposed:.1f} us")

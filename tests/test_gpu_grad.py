@@ -112,3 +112,64 @@ def test_grad_n1024_vs_oracle(lfm):
     m = model_of(lfm, D, S, B, 2.5, 1.0, 1e-4)
     val, gr = lfm.CustomConjMLL(negative=True).value_and_grad(m, lfm.Dataset(x, y))
     check(val, gr, ref["value"], ref, {k: ref["scale_" + k] for k, _ in KEYS})
+
+
+@pytest.mark.parametrize("env", [{"LFM_SCHED": "1"}, {"LFM_SCHED": "3"},
+                                 {"LFM_SCHED": "3", "LFM_W4_MIN": "1024"},
+                                 {"LFM_SCHED": "3", "LFM_W4_MIN": "1024", "LFM_S3_EVENTS": "1"}])
+def test_grad_schedules_vs_oracle(lfm, env, monkeypatch):
+    """N = 1024 (4 genes x 256): the bordered inverse through schedule 1 and through schedule
+    3's sliding Mp-row window (w = 1 steps; w = 4 super-panels with LFM_W4_MIN=1024; its
+    event-ordered profiling mode), each against the oracle's complex-step gradient."""
+    from dis_project_amd import _lib
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(4256)
+    G, T = 4, 256
+    D = rng.uniform(0.2, 1.0, G); S = rng.uniform(0.5, 1.5, G); B = rng.uniform(0.01, 0.1, G)
+    t = np.linspace(0, 12, T)
+    x = np.stack((np.tile(t, G), np.repeat(np.arange(G), T), np.ones(G * T)), -1)
+    y = np.repeat(B / D, T) + 0.5 * rng.standard_normal(G * T)
+    ref = O.mll_grad(x, y, D, S, B, 2.3, 0.8, 1e-4, negative=True)
+    m = model_of(lfm, D, S, B, 2.3, 0.8, 1e-4)
+    ctx = _lib.Context(0)  # schedule knobs are read when a context is created
+    try:
+        val = np.empty(1)
+        gv = np.empty(3 * G + 2)
+        hp = m.hyp()
+        ctx.check(ctx.lib.lfm_mll_grad_f64(ctx.handle, _lib.dptr(np.ascontiguousarray(x)),
+                                           _lib.dptr(y), x.shape[0], hp.ref, 1, _lib.dptr(val),
+                                           _lib.dptr(gv)))
+    finally:
+        ctx.close()
+    gr = {"true_d": gv[:G], "true_s": gv[G:2 * G], "true_b": gv[2 * G:3 * G], "l": gv[3 * G],
+          "obs_stddev": gv[3 * G + 1]}
+    check(float(val[0]), gr, ref["value"], ref, {k: ref["scale_" + k] for k, _ in KEYS})
+
+
+def test_grad_n16384_schedule3_matches_schedule1(lfm, monkeypatch):
+    """C2 at full size (N = 16384): the schedule-3 bordered inverse (the default) and the
+    schedule-1 one give the same value (1e-11) and gradient (1e-9 of the largest component)."""
+    from dis_project_amd import _lib, configs
+
+    work = configs.c2()
+    x = np.ascontiguousarray(work.data.X)
+    y = np.ascontiguousarray(work.data.y.reshape(-1))
+    G = work.model.num_genes
+    out = {}
+    for sched in ("3", "1"):
+        monkeypatch.setenv("LFM_SCHED", sched)
+        ctx = _lib.Context(0)
+        try:
+            val, gv = np.empty(1), np.empty(3 * G + 2)
+            ctx.check(ctx.lib.lfm_mll_grad_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
+                                               work.model.hyp().ref, 1, _lib.dptr(val),
+                                               _lib.dptr(gv)))
+            out[sched] = (float(val[0]), gv.copy())
+        finally:
+            ctx.close()
+    (v3, g3), (v1, g1) = out["3"], out["1"]
+    assert v3 == pytest.approx(v1, rel=1e-11)
+    assert np.all(np.isfinite(g3))
+    assert np.max(np.abs(g3 - g1)) <= 1e-9 * np.max(np.abs(g1)), np.max(np.abs(g3 - g1))
