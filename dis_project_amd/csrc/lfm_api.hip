@@ -438,9 +438,11 @@ int env_int_api(const char* name, int def) {
 //   LFM_SIDE_CUS         CUs reserved for the schedule-3 factor chain (0: schedule 1 only)
 //   LFM_S3_EVENTS        1: schedule 3 ordered by stream events (for rocprofv3 --pmc)
 //   LFM_DEBUG_SPIN_LIMIT poll bound of every device-side wait (tests force timeouts with 0)
+//   LFM_GRAD_DIRECT      1: the gradient's per-pair path even on a grid layout (cross-check)
 hipError_t create_streams(lfm_ctx* ctx) {
   ctx->sched = env_int_api("LFM_SCHED", 3) == 1 ? 1 : 3;
   ctx->s3_events = env_int_api("LFM_S3_EVENTS", 0) != 0;
+  ctx->grad_direct = env_int_api("LFM_GRAD_DIRECT", 0) != 0;
   if (const char* sl = std::getenv("LFM_DEBUG_SPIN_LIMIT"))
     ctx->spin_limit = (unsigned)std::strtoul(sl, nullptr, 10);
   int least = 0, greatest = 0;
@@ -535,7 +537,8 @@ void lfm_ctx_destroy(lfm_ctx* ctx) {
                   (void*)ctx->xin, (void*)ctx->linvT, (void*)ctx->parts, (void*)ctx->status,
                   (void*)ctx->result, (void*)ctx->farm_buf, (void*)ctx->gacc,
                   (void*)ctx->psync, (void*)ctx->wk, (void*)ctx->xbuf, (void*)ctx->zvec,
-                  (void*)ctx->flags, (void*)ctx->linv_full, (void*)ctx->dbg_stamps, (void*)ctx->xd})
+                  (void*)ctx->flags, (void*)ctx->linv_full, (void*)ctx->dbg_stamps, (void*)ctx->xd,
+                  (void*)ctx->gtab})
     if (p) hipFree(p);
   if (ctx->hpin) hipHostFree(ctx->hpin);
   for (auto& p : ctx->pending) {
@@ -738,7 +741,8 @@ int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
   r = chol_factor_solve(ctx, ctx->A, M2, n, Mp, negative, ctx->result, CHOL_INVERSE);
   if (r) return r;
   double* d_out = ctx->gacc + 2 * G + 1;
-  r = launch_grad(ctx, st.h, d_x, n, ctx->A, M2, Mp, hyp->obs_stddev, negative, ctx->gacc, d_out);
+  r = launch_grad(ctx, st.h, d_x, n, ctx->A, M2, Mp, hyp->obs_stddev, negative, ctx->gacc, d_out,
+                  &st.lay, st.d_times, st.d_bg);
   if (r) return r;
   const size_t ng = (size_t)(3 * G + 2);
   r = ensure_pinned(ctx, (ng + 16) * sizeof(double));

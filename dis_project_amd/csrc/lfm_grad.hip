@@ -26,6 +26,11 @@
 
 namespace lfm {
 
+// e^{A} erfc(z) without overflow: erfcx(z) e^{A - z^2} once erfc(z) underflows towards 0.
+__device__ __forceinline__ double exp_erfc_g(double A, double z) {
+  return z > 0.0 ? erfcx(z) * exp(A - z * z) : exp(A) * erfc(z);
+}
+
 // ---------------------------------------------------------------- duals
 // Value and derivatives with respect to (D_row_gene, D_col_gene, l).
 struct Dual3 {
@@ -260,6 +265,186 @@ __global__ __launch_bounds__(1024) void grad_finish_kernel(
   }
 }
 
+// ------------------------------------------------------- grid (table) path
+// On the dataset_3d grid every transcendental of kernel_xx and of its derivatives in
+// (D_j, D_k, l) separates per (gene, tau) or per (gene, d = tau' - tau), as in the gram's
+// tables (lfm_gram.hip): with g = D l / 2, delta = d dt, A = g^2 - D delta, z = g - delta/l,
+// y = t/l + g, u = g - t/l (and A - z^2 = -delta^2/l^2, g^2 - u^2 = D t - t^2/l^2):
+//   Wt = e^A erfc(z)  dW/dD = Wt (g l - delta) - c e^{-delta^2/l^2} l/2
+//                     dW/dl = Wt g D - c e^{-delta^2/l^2} (D/2 + delta/l^2)
+//   Xt = e^A          dX/dD = Xt (g l - delta),  dX/dl = Xt g D
+//   Pt = erfc(y)      dP/dD = -c e^{-y^2} l/2,   dP/dl = -c e^{-y^2} (D/2 - t/l^2)
+//   Et = e^{-D t}     dE/dD = -t Et
+//   Qt = e^{g^2}(erfc(u) - erfc(g))
+//                     dQ/dD = g l Qt - c (l/2) (e^{D t - t^2/l^2} - 1)
+//                     dQ/dl = g D Qt - c ((D/2 + t/l^2) e^{D t - t^2/l^2} - D/2)
+// with c = 2/sqrt(pi). Layout (doubles), W = 2T - 1: the six Toeplitz rows
+// Wt Xt WtD XtD Wtl Xtl (G x W each), then the eight time rows Pt PtD Ptl Et EtD Qt QtD Qtl
+// (G x T each).
+size_t grad_tables_doubles(int G, int T) {
+  return 6 * (size_t)G * (2 * (size_t)T - 1) + 8 * (size_t)G * T;
+}
+
+__global__ void grad_tables_kernel(HypDev p, int T, double dt, const double* __restrict__ times,
+                                   double* __restrict__ tab) {
+  const int G = p.G;
+  const int64_t W = 2 * (int64_t)T - 1, nW = (int64_t)G * W, nT = (int64_t)G * T;
+  const int64_t total = 6 * nW + 8 * nT;
+  const double l = p.l, c2 = 1.1283791670955125739;  // 2 / sqrt(pi)
+  for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+       idx += (int64_t)gridDim.x * blockDim.x) {
+    double v;
+    if (idx < 6 * nW) {
+      const int which = (int)(idx / nW);
+      const int64_t q = idx - which * nW;
+      const int g = (int)(q / W);
+      const int d = (int)(q - (int64_t)g * W) - (T - 1);
+      const double D = p.D[g], gam = D * l / 2.0, delta = (double)d * dt;
+      const double A = gam * gam - D * delta;
+      const double X = exp(A);
+      const double Wv = exp_erfc_g(A, gam - delta / l);
+      const double ez = c2 * exp(-(delta / l) * (delta / l));
+      switch (which) {
+        case 0: v = Wv; break;
+        case 1: v = X; break;
+        case 2: v = Wv * (gam * l - delta) - ez * (l / 2.0); break;
+        case 3: v = X * (gam * l - delta); break;
+        case 4: v = Wv * gam * D - ez * (D / 2.0 + delta / (l * l)); break;
+        default: v = X * gam * D; break;
+      }
+    } else {
+      const int64_t q0 = idx - 6 * nW;
+      const int which = (int)(q0 / nT);
+      const int64_t q = q0 - which * nT;
+      const int g = (int)(q / T);
+      const double t = times[q - (int64_t)g * T];
+      const double D = p.D[g], gam = D * l / 2.0;
+      if (which < 3) {
+        const double y = t / l + gam, ey = c2 * exp(-y * y);
+        v = which == 0 ? erfc(y) : which == 1 ? -ey * (l / 2.0) : -ey * (D / 2.0 - t / (l * l));
+      } else if (which < 5) {
+        const double E = exp(-D * t);
+        v = which == 3 ? E : -t * E;
+      } else {
+        const double Q = exp_erfc_g(gam * gam, gam - t / l) - erfcx(gam);
+        const double eq = exp(D * t - t * t / (l * l));
+        v = which == 5 ? Q
+            : which == 6 ? gam * l * Q - c2 * (l / 2.0) * (eq - 1.0)
+                         : gam * D * Q - c2 * ((D / 2.0 + t / (l * l)) * eq - D / 2.0);
+      }
+    }
+    tab[idx] = v;
+  }
+}
+
+// One workgroup per 64-row x 256-column lower tile (T % 256 == 0: the tile lies in one
+// (gene j, gene k) block), the tile's Toeplitz windows and row tables staged in LDS, one
+// thread per column. Per element the kernel value and its three derivatives (D_j, D_k, l)
+// cost 12 conflict-free LDS reads, ~35 FMAs and one coalesced read of W; the gene-pair
+// constant Cm = S_j S_k l sqrt(pi)/2 / (D_j + D_k) is applied once per tile to the
+// W-weighted sums, which go out as five atomics per workgroup.
+// acc layout as grad_pairs_kernel: [0,G) dD  [G,2G) dS  [2G] dl.
+__global__ __launch_bounds__(256) void grad_grid_kernel(HypDev p, const double* __restrict__ tab,
+                                                        int Tn, const int* __restrict__ bg,
+                                                        int64_t n, const double* __restrict__ Bt,
+                                                        int64_t ldb, const double* __restrict__ al,
+                                                        double* __restrict__ acc) {
+  constexpr int R = 64, C = 256, WIN = C + R - 1;
+  __shared__ double sT[12][WIN];   // k-side tables at d, j-side tables at -d
+  __shared__ double sR[8][R];      // row (tau) tables
+  __shared__ double red[4][4];
+  // 1-D grid over the lower tiles (as gram_grid_aligned_kernel)
+  const int64_t b = blockIdx.x;
+  int64_t q = (int64_t)((sqrt(2.0 * (double)b + 1.0) - 1.0) * 0.5);
+  while (2 * (q + 1) * (q + 2) <= b) ++q;
+  while (2 * q * (q + 1) > b) --q;
+  const int64_t off = b - 2 * q * (q + 1);
+  const int64_t r0 = (4 * q + off / (q + 1)) * R, c0 = (off % (q + 1)) * C;
+  const int tid = threadIdx.x, G = p.G;
+  const int64_t W = 2 * (int64_t)Tn - 1, nW = (int64_t)G * W, nT = (int64_t)G * Tn;
+  const double* Tt = tab;           // Toeplitz tables, table w at Tt + w nW
+  const double* Pt = tab + 6 * nW;  // time tables, table w at Pt + w nT
+  const int j = bg[r0 / Tn], k = bg[c0 / Tn];
+  const int tau0 = (int)(r0 % Tn), tp0 = (int)(c0 % Tn);
+  const int dmin = tp0 - tau0 - (R - 1);
+  for (int e = tid; e < WIN; e += 256) {
+    const int64_t d = dmin + e;
+#pragma unroll
+    for (int w = 0; w < 6; ++w) {
+      sT[w][e] = Tt[w * nW + (int64_t)k * W + (Tn - 1) + d];
+      sT[6 + w][e] = Tt[w * nW + (int64_t)j * W + (Tn - 1) - d];
+    }
+  }
+  if (tid < R) {
+    const int64_t kr = (int64_t)k * Tn + tau0 + tid, jr = (int64_t)j * Tn + tau0 + tid;
+    sR[0][tid] = Pt[0 * nT + kr];  // Pk(tau), dPk/dD, dPk/dl
+    sR[1][tid] = Pt[1 * nT + kr];
+    sR[2][tid] = Pt[2 * nT + kr];
+    sR[3][tid] = Pt[3 * nT + jr];  // Ej(tau), dEj/dD
+    sR[4][tid] = Pt[4 * nT + jr];
+    sR[5][tid] = Pt[5 * nT + jr];  // Qj(tau), dQj/dD, dQj/dl
+    sR[6][tid] = Pt[6 * nT + jr];
+    sR[7][tid] = Pt[7 * nT + jr];
+  }
+  const int tp = tp0 + tid;
+  const int64_t kc = (int64_t)k * Tn + tp, jc = (int64_t)j * Tn + tp;
+  const double Pj = Pt[0 * nT + jc], PjD = Pt[1 * nT + jc], Pjl = Pt[2 * nT + jc];
+  const double Ek = Pt[3 * nT + kc], EkD = Pt[4 * nT + kc];
+  const double Qk = Pt[5 * nT + kc], QkD = Pt[6 * nT + kc], Qkl = Pt[7 * nT + kc];
+  const int64_t c = c0 + tid;
+  const double ac = al[c];
+  __syncthreads();
+  double sV = 0.0, sVj = 0.0, sVk = 0.0, sVl = 0.0;
+  const double* bp = Bt + r0 * ldb + c;
+#pragma unroll 4
+  for (int i = 0; i < R; ++i) {
+    const int64_t row = r0 + i;
+    if (c > row || row >= n) continue;
+    const int e = tid + (R - 1) - i;
+    const double Wk = sT[0][e], Xk = sT[1][e], WkD = sT[2][e], XkD = sT[3][e];
+    const double Wkl = sT[4][e], Xkl = sT[5][e];
+    const double Wj = sT[6][e], Xj = sT[7][e], WjD = sT[8][e], XjD = sT[9][e];
+    const double Wjl = sT[10][e], Xjl = sT[11][e];
+    const double Pk = sR[0][i], PkD = sR[1][i], Pkl = sR[2][i];
+    const double Ej = sR[3][i], EjD = sR[4][i], Qj = sR[5][i], QjD = sR[6][i], Qjl = sR[7][i];
+    const double EE = Ek * Ej, QQ = Qk + Qj;
+    const double V = Wk + Wj - Xk * Pk - Xj * Pj - EE * QQ;
+    const double Vk = WkD - XkD * Pk - Xk * PkD - EkD * Ej * QQ - EE * QkD;
+    const double Vj = WjD - XjD * Pj - Xj * PjD - Ek * EjD * QQ - EE * QjD;
+    const double Vl = Wkl - Xkl * Pk - Xk * Pkl + Wjl - Xjl * Pj - Xj * Pjl - EE * (Qkl + Qjl);
+    double w = bp[(int64_t)i * ldb] + 2.0 * al[row] * ac;
+    if (row == c) w *= 0.5;
+    sV += w * V;
+    sVj += w * Vj;
+    sVk += w * Vk;
+    sVl += w * Vl;
+  }
+  sV = wave_sum(sV);
+  sVj = wave_sum(sVj);
+  sVk = wave_sum(sVk);
+  sVl = wave_sum(sVl);
+  if ((tid & 63) == 0) {
+    red[tid >> 6][0] = sV;
+    red[tid >> 6][1] = sVj;
+    red[tid >> 6][2] = sVk;
+    red[tid >> 6][3] = sVl;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const double V = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    const double Vj = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+    const double Vk = red[0][2] + red[1][2] + red[2][2] + red[3][2];
+    const double Vl = red[0][3] + red[1][3] + red[2][3] + red[3][3];
+    const double l = p.l, iDD = 1.0 / (p.D[j] + p.D[k]);
+    const double Cm = p.S[j] * p.S[k] * l * kSqrtPi * 0.5 * iDD;
+    unsafeAtomicAdd(acc + j, Cm * (Vj - V * iDD));
+    unsafeAtomicAdd(acc + k, Cm * (Vk - V * iDD));
+    unsafeAtomicAdd(acc + G + j, Cm * V / p.S[j]);
+    unsafeAtomicAdd(acc + G + k, Cm * V / p.S[k]);
+    unsafeAtomicAdd(acc + 2 * G, Cm * (V / l + Vl));
+  }
+}
+
 int launch_border_init(lfm_ctx* ctx, double* A, int64_t lda, int64_t Mp) {
   hipEvent_t ev;
   prof_begin(ctx, K_AUGMENT, &ev);
@@ -271,17 +456,32 @@ int launch_border_init(lfm_ctx* ctx, double* A, int64_t lda, int64_t Mp) {
 
 int launch_grad(lfm_ctx* ctx, const HypDev& h, const double* d_x, int64_t n, const double* A,
                 int64_t lda, int64_t Mp, double obs_stddev, int negative, double* acc,
-                double* d_out) {
+                double* d_out, const GridLayout* lay, const double* d_times, const int* d_bg) {
   const double* Bt = A + Mp * lda + Mp;
   const double* al = Bt + n * lda;
   hipMemsetAsync(acc, 0, (size_t)(2 * h.G + 1) * sizeof(double), ctx->stream);
+  // the table path on the aligned grid layout (T % 256 == 0, the C2-C4 shape), else the
+  // general per-pair dual-number path (LFM_GRAD_DIRECT=1 forces it: a test's cross-check)
+  const bool grid = lay && lay->ok && lay->T % 256 == 0 && n % 256 == 0 && !ctx->grad_direct;
   hipEvent_t ev;
   prof_begin(ctx, K_GRAD, &ev);
-  dim3 grid((unsigned)((n + 255) / 256), (unsigned)((n + GR - 1) / GR));
-  hipLaunchKernelGGL(grad_pairs_kernel, grid, dim3(256), 0, ctx->stream, h, d_x, n, Bt, lda, al,
-                     acc);
+  if (grid) {
+    int r = ensure(ctx, (void**)&ctx->gtab, &ctx->gtab_bytes,
+                   grad_tables_doubles(h.G, lay->T) * sizeof(double));
+    if (r) return r;
+    const size_t nt = grad_tables_doubles(h.G, lay->T);
+    hipLaunchKernelGGL(grad_tables_kernel, dim3((unsigned)std::min<size_t>((nt + 255) / 256, 4096)),
+                       dim3(256), 0, ctx->stream, h, lay->T, lay->dt, d_times, ctx->gtab);
+    const int64_t Q = n / 256;
+    hipLaunchKernelGGL(grad_grid_kernel, dim3((unsigned)(2 * Q * (Q + 1))), dim3(256), 0,
+                       ctx->stream, h, ctx->gtab, lay->T, d_bg, n, Bt, lda, al, acc);
+  } else {
+    dim3 grid2((unsigned)((n + 255) / 256), (unsigned)((n + GR - 1) / GR));
+    hipLaunchKernelGGL(grad_pairs_kernel, grid2, dim3(256), 0, ctx->stream, h, d_x, n, Bt, lda,
+                       al, acc);
+  }
   prof_end(ctx, K_GRAD, ev, 0, (double)n * (n + 1) / 2 * 8);
-  int r = hip_fail(ctx, hipGetLastError(), "grad_pairs_kernel");
+  int r = hip_fail(ctx, hipGetLastError(), "grad kernel");
   if (r) return r;
   hipLaunchKernelGGL(grad_finish_kernel, dim3(1), dim3(1024), 0, ctx->stream, h, d_x, n, Bt, lda,
                      al, acc, obs_stddev, ctx->result, negative, d_out);

@@ -84,6 +84,8 @@ struct lfm_ctx {
   int sched = 3;                                 // look-ahead schedule 1 or 3 (LFM_SCHED)
   bool s3_events = false;                        // schedule 3 ordered by events (LFM_S3_EVENTS)
   unsigned spin_limit = 1u << 26;                // device-side wait bound (LFM_DEBUG_SPIN_LIMIT)
+  bool grad_direct = false;                      // gradient: per-pair path only (LFM_GRAD_DIRECT)
+  double* gtab = nullptr; size_t gtab_bytes = 0; // gradient tables (grid layout)
   double* result = nullptr;                      // [0..] scalar results
   double* gacc = nullptr; size_t gacc_bytes = 0; // gradient accumulators + output
 
@@ -204,7 +206,8 @@ int posterior_blocked(lfm_ctx* ctx, const HypDev& h, const double* d_x, const do
                       double* d_mean, double* d_cov);
 int launch_grad(lfm_ctx* ctx, const HypDev& h, const double* d_x, int64_t n, const double* A,
                 int64_t lda, int64_t Mp, double obs_stddev, int negative, double* acc,
-                double* d_out);
+                double* d_out, const GridLayout* lay = nullptr, const double* d_times = nullptr,
+                const int* d_bg = nullptr);
 int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn,
                        int negative, double* d_out, int* d_status);
 

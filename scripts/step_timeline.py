@@ -4,7 +4,10 @@ launch s (step s's trailing update + the tall solve of super-panel s + 1) the la
 the update units' span and rate, how long the tall units' last wait ran past the update
 (the chain-bound exposure), and the chain (s + 1)'s own span.
 
-    python scripts/step_timeline.py [--json out.json]
+    python scripts/step_timeline.py [--json out.json] [--grad]
+
+--grad times value_and_grad's bordered factorisation (2Mp x 2Mp, every step updating the
+sliding Mp-row window) instead of the MLL's.
 """
 import ctypes
 import json
@@ -19,15 +22,15 @@ from dis_project_amd import _lib, configs  # noqa: E402
 NB = 128
 
 
-def plan(n):
+def plan(n, bordered=False):
     """Schedule 3's step plan (lfm_chol.hip chol_factor_solve, default LFM_W4_MIN/W2_MIN)."""
     Mp = (n + 1 + NB - 1) // NB * NB
-    nblk = (n + NB - 1) // NB
+    nblk = Mp // NB if bordered else (n + NB - 1) // NB
     w4 = int(os.environ.get("LFM_W4_MIN", 6144))
     w2 = int(os.environ.get("LFM_W2_MIN", 5120))
     steps, k = [], 0
     while k < nblk:
-        m = Mp - k * NB
+        m = Mp + NB if bordered else Mp - k * NB
         w = 4 if (m >= w4 and k + 4 <= nblk) else 2 if (m >= w2 and k + 2 <= nblk) else 1
         if k == 0:
             w = 1
@@ -37,6 +40,7 @@ def plan(n):
 
 
 def main():
+    grad = "--grad" in sys.argv
     work = configs.c2()
     n = work.n
     x = np.ascontiguousarray(work.data.X)
@@ -49,25 +53,35 @@ def main():
     ctx.check(lib.lfm_memcpy_h2d(h, dx, x.ctypes.data, x.nbytes))
     ctx.check(lib.lfm_memcpy_h2d(h, dy, y.ctypes.data, y.nbytes))
     out = np.empty(1)
+    gv = np.empty(3 * work.model.num_genes + 2)
     hp = work.model.hyp()
     import time
+
+    def run():
+        if grad:
+            ctx.check(lib.lfm_mll_grad_f64(h, _lib.dptr(x), _lib.dptr(y), n, hp.ref, 1,
+                                           _lib.dptr(out), _lib.dptr(gv)))
+        else:
+            ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, n, hp.ref, 0, _lib.dptr(out)))
+
     for _ in range(3):
-        ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, n, hp.ref, 0, _lib.dptr(out)))
+        run()
     t0 = time.perf_counter()
     for _ in range(5):
-        ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, n, hp.ref, 0, _lib.dptr(out)))
+        run()
     plain_ms = (time.perf_counter() - t0) / 5 * 1e3
     ctx.check(lib.lfm_debug_stamps(h, 1, None, 0))
     t0 = time.perf_counter()
-    ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, n, hp.ref, 0, _lib.dptr(out)))
+    run()
     stamped_ms = (time.perf_counter() - t0) * 1e3
     buf = (ctypes.c_ulonglong * (256 * 24))()
     ctx.check(lib.lfm_debug_stamps(h, 0, buf, 256 * 24))
     allst = np.frombuffer(buf, dtype=np.uint64)
     ch = allst[: 256 * 16].reshape(256, 16).astype(np.int64)
     sp = allst[256 * 16:].reshape(256, 8).copy()
-    steps = plan(n)
+    steps = plan(n, grad)
     S = len(steps)
+    Mp = (n + 1 + NB - 1) // NB * NB
     first = ~sp[:, 0]  # earliest unit start (stored as the max of the bitwise NOT)
     t_ref = int(min(int(ch[0][0]), int(first[0])))
     us = lambda t: (int(t) - t_ref) * 0.01  # noqa: E731
@@ -78,10 +92,10 @@ def main():
     for s in range(S - 1):
         k, w = steps[s]
         K1 = (k + w) * NB
-        m = n - K1
+        m = Mp if grad else n - K1
         wn = steps[s + 1][1]
         d = min(wn * NB, m)
-        alg = 2.0 * w * NB * (m * (m + 1) / 2 + m - d * (d + 1) / 2)
+        alg = 2.0 * w * NB * (m * (m + 1) / 2 + (0 if grad else m) - d * (d + 1) / 2)
         st0, upd_end, wait_end, end = int(first[s]), int(sp[s][1]), int(sp[s][2]), int(sp[s][3])
         launch = (end - st0) * 0.01
         upd = (upd_end - st0) * 0.01 if upd_end else 0.0
@@ -100,9 +114,9 @@ def main():
     end_all = max(int(v) for v in sp[: S - 1, 3])
     print(f"span first unit -> last unit: {(end_all - int(first[0])) * 0.01:.1f} us; "
           f"chain-bound exposure (tall units waiting past the update) {tot_exposed:.1f} us")
-    if len(sys.argv) > 2 and sys.argv[1] == "--json":
-        json.dump({"n": n, "plain_ms": plain_ms, "stamped_ms": stamped_ms,
-                   "exposed_us": tot_exposed, "steps": rows}, open(sys.argv[2], "w"), indent=1)
+    if "--json" in sys.argv:
+        json.dump({"n": n, "grad": grad, "plain_ms": plain_ms, "stamped_ms": stamped_ms,
+                   "exposed_us": tot_exposed, "steps": rows}, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
 
 
 if __name__ == "__main__":

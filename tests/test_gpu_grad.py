@@ -116,11 +116,14 @@ def test_grad_n1024_vs_oracle(lfm):
 
 @pytest.mark.parametrize("env", [{"LFM_SCHED": "1"}, {"LFM_SCHED": "3"},
                                  {"LFM_SCHED": "3", "LFM_W4_MIN": "1024"},
-                                 {"LFM_SCHED": "3", "LFM_W4_MIN": "1024", "LFM_S3_EVENTS": "1"}])
+                                 {"LFM_SCHED": "3", "LFM_W4_MIN": "1024", "LFM_S3_EVENTS": "1"},
+                                 {"LFM_SCHED": "3", "LFM_GRAD_DIRECT": "1"}])
 def test_grad_schedules_vs_oracle(lfm, env, monkeypatch):
     """N = 1024 (4 genes x 256): the bordered inverse through schedule 1 and through schedule
     3's sliding Mp-row window (w = 1 steps; w = 4 super-panels with LFM_W4_MIN=1024; its
-    event-ordered profiling mode), each against the oracle's complex-step gradient."""
+    event-ordered profiling mode), each against the oracle's complex-step gradient; the
+    gradient reduction through the grid-table kernel (the default on this layout) and through
+    the per-pair dual-number kernel (LFM_GRAD_DIRECT=1)."""
     from dis_project_amd import _lib
 
     for k, v in env.items():
@@ -150,7 +153,8 @@ def test_grad_schedules_vs_oracle(lfm, env, monkeypatch):
 
 def test_grad_n16384_schedule3_matches_schedule1(lfm, monkeypatch):
     """C2 at full size (N = 16384): the schedule-3 bordered inverse (the default) and the
-    schedule-1 one give the same value (1e-11) and gradient (1e-9 of the largest component)."""
+    schedule-1 one, and the grid-table gradient kernel (the default) and the per-pair
+    dual-number one, give the same value (1e-11) and gradient (1e-9 of the largest component)."""
     from dis_project_amd import _lib, configs
 
     work = configs.c2()
@@ -158,18 +162,22 @@ def test_grad_n16384_schedule3_matches_schedule1(lfm, monkeypatch):
     y = np.ascontiguousarray(work.data.y.reshape(-1))
     G = work.model.num_genes
     out = {}
-    for sched in ("3", "1"):
+    for sched, direct in (("3", "0"), ("1", "0"), ("3", "1")):
         monkeypatch.setenv("LFM_SCHED", sched)
+        monkeypatch.setenv("LFM_GRAD_DIRECT", direct)
         ctx = _lib.Context(0)
         try:
             val, gv = np.empty(1), np.empty(3 * G + 2)
             ctx.check(ctx.lib.lfm_mll_grad_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
                                                work.model.hyp().ref, 1, _lib.dptr(val),
                                                _lib.dptr(gv)))
-            out[sched] = (float(val[0]), gv.copy())
+            out[sched + direct] = (float(val[0]), gv.copy())
         finally:
             ctx.close()
-    (v3, g3), (v1, g1) = out["3"], out["1"]
+    (v3, g3), (v1, g1), (vd, gd) = out["30"], out["10"], out["31"]
     assert v3 == pytest.approx(v1, rel=1e-11)
+    assert vd == pytest.approx(v3, rel=1e-11)
     assert np.all(np.isfinite(g3))
-    assert np.max(np.abs(g3 - g1)) <= 1e-9 * np.max(np.abs(g1)), np.max(np.abs(g3 - g1))
+    scale = np.max(np.abs(gd))
+    assert np.max(np.abs(g3 - g1)) <= 1e-9 * scale, np.max(np.abs(g3 - g1))
+    assert np.max(np.abs(g3 - gd)) <= 1e-9 * scale, np.max(np.abs(g3 - gd))
