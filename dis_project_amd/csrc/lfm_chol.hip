@@ -801,6 +801,16 @@ struct Panel {
 #endif
 // Bulk trailing update (step_kernel's update units): K depth of one LDS stage and the unroll
 // of the 4-deep MFMA steps within it
+// rest-triangle enumeration: tile rows in groups of Q, Q x Q supertiles within a group (1: row
+// by row)
+#ifndef LFM_SUPERTILE
+#define LFM_SUPERTILE 6
+#endif
+// rectangular bands (the step kernel's next-super-panel columns) enumerated row by row (0:
+// column by column)
+#ifndef LFM_BAND_ROWS
+#define LFM_BAND_ROWS 1
+#endif
 #ifndef LFM_STEP_KS
 #define LFM_STEP_KS 16
 #endif
@@ -823,7 +833,15 @@ __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, i
 
   constexpr int SUB = ST / TR;  // row tiles per 128 rows
   int ti, tj;  // ti in TR-row units
-  if (tj_hi - tj_lo <= 8) {
+  if (LFM_BAND_ROWS && tj_hi - tj_lo <= 8 && ti0 >= tj_hi) {
+    // rectangular band (every row below the band's columns): row by row, so consecutive units
+    // share a row panel and the band's few column panels stay in L2
+    const int nb = tj_hi - tj_lo;
+    const int64_t r = b / (nb * SUB);
+    const int rem = (int)(b - r * nb * SUB);
+    tj = tj_lo + rem / SUB;
+    ti = SUB * (ti0 + (int)r) + rem % SUB;
+  } else if (tj_hi - tj_lo <= 8) {
     // band: tile columns [tj_lo, tj_hi), tile rows max(tj, ti0) .. T - 1
     tj = tj_lo;
     while (b >= (int64_t)SUB * max(0, T - max(tj, ti0))) {
@@ -833,14 +851,37 @@ __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, i
     ti = SUB * max(tj, ti0) + (int)b;
   } else {
     // triangle of 128-tiles over tile columns [tj_lo, T), SUB row slabs of TR rows per tile;
-    // tile rows are enumerated in order, so a launch can skip the first ones (b offset)
+    // groups of LFM_SUPERTILE tile rows are enumerated in order (so a launch can skip the first
+    // ones: b offset), within a group Q x Q supertiles in turn, tiles row by row within those:
+    // consecutive units (one XCD's co-resident workgroups) then share row and column panels
     const int sub = (int)(b % SUB);
     b /= SUB;
     int a = (int)((sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
     while ((int64_t)(a + 1) * (a + 2) / 2 <= b) ++a;
     while ((int64_t)a * (a + 1) / 2 > b) --a;
-    tj = (int)(b - (int64_t)a * (a + 1) / 2) + tj_lo;
-    ti = SUB * (a + tj_lo) + sub;
+    constexpr int Q = LFM_SUPERTILE;
+    if constexpr (Q > 1) {
+      const int R = a / Q, r0 = R * Q, qr = min(Q, T - tj_lo - r0);
+      const int64_t off = b - (int64_t)r0 * (r0 + 1) / 2;
+      const int64_t full = (int64_t)R * qr * Q;
+      int lr, lc;
+      if (off < full) {
+        const int C = (int)(off / (qr * Q)), t = (int)(off % (qr * Q));
+        lr = t / Q;
+        lc = C * Q + t % Q;
+      } else {
+        const int d = (int)(off - full);
+        lr = (int)((sqrt(8.0 * (double)d + 1.0) - 1.0) * 0.5);
+        while ((lr + 1) * (lr + 2) / 2 <= d) ++lr;
+        while (lr * (lr + 1) / 2 > d) --lr;
+        lc = r0 + d - lr * (lr + 1) / 2;
+      }
+      tj = lc + tj_lo;
+      ti = SUB * (r0 + lr + tj_lo) + sub;
+    } else {
+      tj = (int)(b - (int64_t)a * (a + 1) / 2) + tj_lo;
+      ti = SUB * (a + tj_lo) + sub;
+    }
   }
   const int64_t i0 = s + (int64_t)ti * TR, j0 = s + (int64_t)tj * ST;
   const bool diag = i0 < j0 + ST;  // the tile reaches the diagonal: keep col <= row only
@@ -1001,7 +1042,8 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
                                            0, g.n, g.pad_end);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
-    const int trow = g.wn + (int)(u % (2 * (g.T - g.wn))) / 2;  // 128-tile row of the unit
+    // 128-tile row of the unit (the band's enumeration order, syrk_unit)
+    const int trow = LFM_BAND_ROWS ? g.wn + (int)(u / (2 * g.wn)) : g.wn + (int)(u % (2 * (g.T - g.wn))) / 2;
     if (threadIdx.x == 0 && g.a_done)
       __hip_atomic_fetch_add(&g.a_done[trow], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0 && g.xready && trow < g.wn + g.lead)
