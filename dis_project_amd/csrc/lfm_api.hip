@@ -736,8 +736,6 @@ int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
   if (r) return r;
   r = launch_augment(ctx, st.h, d_x, d_y, nullptr, n, ctx->A, M2, Mp);
   if (r) return r;
-  r = launch_border_init(ctx, ctx->A, M2, Mp);
-  if (r) return r;
   r = chol_factor_solve(ctx, ctx->A, M2, n, Mp, negative, ctx->result, CHOL_INVERSE);
   if (r) return r;
   double* d_out = ctx->gacc + 2 * G + 1;

@@ -814,6 +814,47 @@ struct Panel {
 #ifndef LFM_STEP_KS
 #define LFM_STEP_KS 16
 #endif
+// The tile body of syrk_unit: C (TR x 128 at row i0, column j0) -= panel rows i0.. x rows j0..
+// over depth kd; CLOAD = false: C starts from zero (not read).
+template <bool CIO, int TR, int KS, bool LDCOH, bool CLOAD>
+__device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, Panel P, int kd,
+                                          int64_t i0, int64_t j0, bool diag, bool coh,
+                                          double (*__restrict__ sP)[KS + 1]) {
+  constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
+  const int li = lane & 15, lk = lane >> 4;
+  double* Cb = A + (i0 + wr + lk) * lda + j0 + wc + li;  // C[wr + lk][wc + li]
+  const int ld4 = (int)(4 * lda);  // row-group stride (elements); 60 * ld4 < 2^31 for lda < 2^23
+
+  double acc[IRN][4];
+#pragma unroll
+  for (int ir = 0; ir < IRN; ++ir)
+#pragma unroll
+    for (int jr = 0; jr < 4; ++jr)
+      acc[ir][jr] = (CIO && CLOAD) ? -ld1<LDCOH>(&Cb[ir * ld4 + jr * 16]) : 0.0;
+  gemm_accumulate<TR, false, LDCOH, KS>(P.p + (i0 - P.r0) * P.ld, P.ld, P.p + (j0 - P.r0) * P.ld,
+                                        P.ld, kd, acc, sP);
+
+  int ld4s = ld4;
+  asm volatile("" : "+v"(ld4s));  // recompute store addresses instead of keeping 64 pointers live
+#pragma unroll
+  for (int ir = 0; ir < IRN; ++ir)
+#pragma unroll
+    for (int jr = 0; jr < 4; ++jr) {
+      const int64_t row = i0 + wr + ir * 4 + lk, col = j0 + wc + jr * 16 + li;
+      if (CIO && (!diag || col <= row)) {
+        // coh: device-coherent (write-through) stores, read by another XCD in flight
+        if (coh)
+          __hip_atomic_store(&Cb[ir * ld4s + jr * 16], -acc[ir][jr], __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+        else
+          Cb[ir * ld4s + jr * 16] = -acc[ir][jr];
+      }
+      if (!CIO && acc[ir][jr] == 1.2345e300) Cb[0] = 0.0;  // keep the MFMAs live
+    }
+}
+
 // One TR x 128 work unit of a band / triangle launch: C -= P_i P_j^T over panel depth kd,
 // C the lower part of the trailing matrix of A starting at row / column s. b = the unit's
 // index in the enumeration below.
@@ -825,12 +866,8 @@ __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, i
                                           int kd, int T, int tj_lo, int tj_hi, int64_t b, int ti0,
                                           double (*__restrict__ sP)[KS + 1], int coh_lim = 0,
                                           int64_t pad_after = INT64_MAX,
-                                          int64_t pad_end = INT64_MAX) {
-  constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
-  const int li = lane & 15, lk = lane >> 4;
-
+                                          int64_t pad_end = INT64_MAX,
+                                          int64_t zero_from = INT64_MAX) {
   constexpr int SUB = ST / TR;  // row tiles per 128 rows
   int ti, tj;  // ti in TR-row units
   if (LFM_BAND_ROWS && tj_hi - tj_lo <= 8 && ti0 >= tj_hi) {
@@ -890,34 +927,14 @@ __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, i
   // entries are zero): nothing reads their update
   if (i0 > pad_after && i0 < pad_end && !in_lead) return false;
   const bool coh = COH || in_lead;
-  double* Cb = A + (i0 + wr + lk) * lda + j0 + wc + li;  // C[wr + lk][wc + li]
-  const int ld4 = (int)(4 * lda);  // row-group stride (elements); 60 * ld4 < 2^31 for lda < 2^23
-
-  double acc[IRN][4];
-#pragma unroll
-  for (int ir = 0; ir < IRN; ++ir)
-#pragma unroll
-    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = CIO ? -ld1<LDCOH>(&Cb[ir * ld4 + jr * 16]) : 0.0;
-  gemm_accumulate<TR, false, LDCOH, KS>(P.p + (i0 - P.r0) * P.ld, P.ld, P.p + (j0 - P.r0) * P.ld,
-                                        P.ld, kd, acc, sP);
-
-  int ld4s = ld4;
-  asm volatile("" : "+v"(ld4s));  // recompute store addresses instead of keeping 64 pointers live
-#pragma unroll
-  for (int ir = 0; ir < IRN; ++ir)
-#pragma unroll
-    for (int jr = 0; jr < 4; ++jr) {
-      const int64_t row = i0 + wr + ir * 4 + lk, col = j0 + wc + jr * 16 + li;
-      if (CIO && (!diag || col <= row)) {
-        // coh: device-coherent (write-through) stores, read by another XCD in flight
-        if (coh)
-          __hip_atomic_store(&Cb[ir * ld4s + jr * 16], -acc[ir][jr], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-        else
-          Cb[ir * ld4s + jr * 16] = -acc[ir][jr];
-      }
-      if (!CIO && acc[ir][jr] == 1.2345e300) Cb[0] = 0.0;  // keep the MFMAs live
-    }
+  // rows >= zero_from are zeros no update has written yet (the bordered matrix's border rows
+  // entering the window; never initialised in memory): a tile body that does not load C. (A
+  // per-element load-or-zero choice makes hipcc branch around every load and wait on each, +7 %
+  // per evaluation; a selected base pointer costs 2 VGPRs, occupancy 4 -> 3 waves / SIMD.)
+  if (i0 >= zero_from)
+    syrk_tile<CIO, TR, KS, LDCOH, false>(A, lda, P, kd, i0, j0, diag, coh, sP);
+  else
+    syrk_tile<CIO, TR, KS, LDCOH, true>(A, lda, P, kd, i0, j0, diag, coh, sP);
   return in_lead;
 }
 
@@ -997,6 +1014,12 @@ struct StepArgs {
   unsigned long long* stamps;  // diagnostics (NULL: off): [8] launch stamps, lfm_diag.h
   int64_t pad_end;   // rows in (n, pad_end) are skipped identity padding (INT64_MAX: every
                      // row past n; n + 1: none)
+  // bordered matrix (the gradient's inverse): border row Mp + i is e_i in the first Mp columns
+  // and zero after until the window reaches it, so it is never initialised in memory —
+  // update units of rows >= zero_from start from C = 0, and the tall units of rows >=
+  // copy_from (= Mp + K0: A21 is the identity there) copy Bd's row (row - copy_from)
+  int64_t zero_from;
+  int64_t copy_from;
 };
 
 // Diagnostics: atomic max of the 100 MHz clock (or of its bitwise NOT: the earliest start)
@@ -1015,7 +1038,8 @@ __device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
 }
 
 
-__global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
+// (256, 4): 128 VGPRs, 4 waves / SIMD (the zero-C tile body would otherwise take 134)
+__global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) {
   __shared__ double sPbuf[(64 + ST) * (LFM_STEP_KS + 1)];
   double (*sP)[KB + 1] = reinterpret_cast<double (*)[KB + 1]>(sPbuf);
   double (*sPu)[LFM_STEP_KS + 1] = reinterpret_cast<double (*)[LFM_STEP_KS + 1]>(sPbuf);
@@ -1039,7 +1063,7 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
     // device-coherent stores + a counter bump once they have completed: the tall units read
     // these rows with device-coherent loads (no L2 writeback / invalidate on either side)
     syrk_unit<true, 64, true, LFM_STEP_KS>(g.A, g.lda, g.s0, g.px, g.kd, g.T, 0, g.wn, u, g.wn, sPu,
-                                           0, g.n, g.pad_end);
+                                           0, g.n, g.pad_end, g.zero_from);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     // 128-tile row of the unit (the band's enumeration order, syrk_unit)
@@ -1063,7 +1087,7 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
     const bool lead = syrk_unit<true, 64, false, LFM_STEP_KS>(g.A, g.lda, g.s0, g.px, g.kd, g.T,
                                                               g.wn, g.T, u, 0, sPu,
                                                               g.xready ? g.wn + g.lead : 0, g.n,
-                                                              g.pad_end);
+                                                              g.pad_end, g.zero_from);
     if (lead) bump_after_stores(g.xready);
     if (st) {
       __syncthreads();
@@ -1105,6 +1129,21 @@ __global__ __launch_bounds__(256, LFM_SLAB_WGS) void step_kernel(StepArgs g) {
   }
   const int W = g.tw * NB;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (i0 >= g.copy_from) {
+    // border rows: X = e_{row - copy_from} Bd, the row of Bd (written through by the chain)
+    const double* src = g.Bd + (i0 - g.copy_from) * W + cb * NB;
+    double* dst = g.X + (i0 - g.tr0) * W + cb * NB;
+#pragma unroll 4
+    for (int u = 0; u < 64 * NB / 2 / 256; ++u) {
+      const int idx = tid + 256 * u, r = idx / (NB / 2), c2 = 2 * (idx % (NB / 2));
+      *reinterpret_cast<double2*>(&dst[r * W + c2]) = ld2<true>(&src[(int64_t)r * W + c2]);
+    }
+    if (st) {
+      __syncthreads();
+      stamp_max(st + 3);
+    }
+    return;
+  }
   const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64;
   const int li = lane & 15, lk = lane >> 4;
   double acc[8][4];
@@ -1866,6 +1905,12 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   // schedule 3 for the MLL and for the bordered inverse (gradient); the Schur-complement
   // posterior keeps schedule 1
   const bool s3 = ctx->sched == 3 && ctx->side_cus > 0 && mode != CHOL_SCHUR;
+  // the bordered matrix's bottom rows [I, 0]: in memory for schedule 1; schedule 3 never reads
+  // them before its window reaches them (StepArgs zero_from / copy_from)
+  if (bordered && !s3) {
+    r = launch_border_init(ctx, A, lda, Mp);
+    if (r) return r;
+  }
   // Step plan: super-panels of w = 4 block columns while the trailing matrix has at least
   // LFM_W4_MIN rows, w = 2 down to LFM_W2_MIN, then w = 1, so the bulk trailing update runs
   // with depth 128 w (C traffic per flop / w). Schedule 3: w = 4 down to 6144 rows, then one
@@ -1991,6 +2036,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     auto launch_step = [&](StepArgs& g) {
       g.n = n;  // padding rows past n are skipped
       g.pad_end = pad_end;
+      if (!g.zero_from) g.zero_from = INT64_MAX;
+      if (!g.copy_from) g.copy_from = INT64_MAX;
       g.spin = ctx->spin_limit;
       const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 + (int64_t)(g.nr + 7) / 8 * 8 +
                            (int64_t)(g.nt + 7) / 8 * 8;
@@ -2030,6 +2077,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.tw = w;
       g.Bd = wkbuf(s) + (int64_t)w * NB * w * NB;
       g.X = xbuf(s);
+      if (bordered) g.copy_from = Mp + K0;
       g.n = n;
       g.zvec = ctx->zvec;
       g.chain_done = chain_done + s;
@@ -2048,6 +2096,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.kd = W;
       g.T = T;
       g.wn = wn;
+      if (bordered) g.zero_from = Mp + steps[s].first * NB;
       g.na = 2 * wn * (T - wn);
       g.nr = (T - wn) * (T - wn + 1);  // 2 slabs per tile of the (T - wn)-tile triangle
       g.status = ctx->status;
