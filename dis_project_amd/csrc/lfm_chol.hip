@@ -1831,7 +1831,7 @@ __global__ void fill_hash_kernel(double* a, int64_t cnt) {
 // Diagnostic: average duration (us) of one full-lower-triangle trailing-update launch (64-row
 // slabs) over a T x T grid of 128-tiles with update depth kd. cio bit 0: C tile I/O (else the
 // MFMAs alone), bit 3: random operands (else zeros), bit 4: on schedule 3's CU-masked bulk
-// stream instead of every CU.
+// stream instead of every CU, bit 6: the step kernel's rest role (bit 5: without C loads).
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const int64_t n = (int64_t)T * ST + 512;
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
@@ -1851,7 +1851,24 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   }
   const Panel pan{ctx->A, n, 0};
   auto go = [&]() {
-    if (cio & 1)
+    if (cio & 64) {
+      // the schedule-3 step kernel's rest role alone (the production unit: 16-deep stages,
+      // 4 workgroups / CU, supertile order); bit 5: no C loads (C = 0, stores kept)
+      StepArgs g{};
+      g.A = ctx->A;
+      g.lda = n;
+      g.s0 = 512;
+      g.px = pan;
+      g.kd = kd;
+      g.T = T;
+      g.nr = (int)units;
+      g.n = n;
+      g.pad_end = INT64_MAX;
+      g.spin = ctx->spin_limit;
+      g.zero_from = (cio & 32) ? 0 : INT64_MAX;
+      g.copy_from = INT64_MAX;
+      hipLaunchKernelGGL(step_kernel, dim3((units + 7) / 8 * 8), dim3(256), 0, st, g);
+    } else if (cio & 1)
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(units), dim3(256), 0, st, ctx->A, n,
                          (int64_t)512, pan, kd, T, 0, T, 0, 1, 0, (int64_t)0);
     else

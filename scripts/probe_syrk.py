@@ -7,7 +7,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dis_project_amd import _lib  # noqa: E402
 
 ctx = _lib.get_context(0)
-# cio: bit 0 = C tile I/O, bit 3 = random operands, bit 4 = the CU-masked bulk stream
+# cio: bit 0 = C tile I/O, bit 3 = random operands, bit 4 = the CU-masked bulk stream,
+# bit 6 = the schedule-3 step kernel's rest role (the production unit), bit 5 = its C loads off
 TS = [int(v) for v in os.environ.get("PROBE_T", "126,64,32").split(",")]
 KDS = [int(v) for v in os.environ.get("PROBE_KD", "128,256,512").split(",")]
 CIOS = [int(v) for v in os.environ.get("PROBE_CIO", "1,0,9").split(",")]
