@@ -814,6 +814,18 @@ struct Panel {
 #ifndef LFM_STEP_KS
 #define LFM_STEP_KS 16
 #endif
+// C tile loads of the trailing update: device-coherent, or plain / nontemporal (LFM_C_NT bit 0;
+// bit 1: nontemporal C stores)
+#ifndef LFM_C_NT
+#define LFM_C_NT 3
+#endif
+template <bool COH>
+__device__ __forceinline__ double ldc(const double* p) {
+  if (COH) return ld1<true>(p);
+  if (LFM_C_NT & 1) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
 // The tile body of syrk_unit: C (TR x 128 at row i0, column j0) -= panel rows i0.. x rows j0..
 // over depth kd; CLOAD = false: C starts from zero (not read).
 template <bool CIO, int TR, int KS, bool LDCOH, bool CLOAD>
@@ -832,7 +844,7 @@ __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, P
   for (int ir = 0; ir < IRN; ++ir)
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr)
-      acc[ir][jr] = (CIO && CLOAD) ? -ld1<LDCOH>(&Cb[ir * ld4 + jr * 16]) : 0.0;
+      acc[ir][jr] = (CIO && CLOAD) ? -ldc<LDCOH>(&Cb[ir * ld4 + jr * 16]) : 0.0;
   gemm_accumulate<TR, false, LDCOH, KS>(P.p + (i0 - P.r0) * P.ld, P.ld, P.p + (j0 - P.r0) * P.ld,
                                         P.ld, kd, acc, sP);
 
@@ -848,6 +860,8 @@ __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, P
         if (coh)
           __hip_atomic_store(&Cb[ir * ld4s + jr * 16], -acc[ir][jr], __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
+        else if (LFM_C_NT & 2)
+          __builtin_nontemporal_store(-acc[ir][jr], &Cb[ir * ld4s + jr * 16]);
         else
           Cb[ir * ld4s + jr * 16] = -acc[ir][jr];
       }
