@@ -17,6 +17,10 @@
 
 using namespace lfm;
 
+#ifndef LFM_GRAM_FUSE_DEFAULT
+#define LFM_GRAM_FUSE_DEFAULT 1
+#endif
+
 namespace lfm {
 
 const char* const kClassName[K_NCLASS] = {"tables",   "gram_grid", "gram_direct",
@@ -249,14 +253,19 @@ int mll_blocked(lfm_ctx* ctx, const Staged& st, const double* d_x, const double*
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)Mp * Mp * sizeof(double));
   if (r) return r;
   const double noise = hyp->obs_stddev * hyp->obs_stddev;  // objectives.py:66
+  GramGen gen;
+  const bool fuse = chol_fuses_gram(ctx, CHOL_MLL, st.lay, n);
   if (st.lay.ok) {
     r = ensure(ctx, (void**)&ctx->tab, &ctx->tab_bytes,
                tables_doubles(st.h.G, st.lay.T) * sizeof(double));
     if (r) return r;
     r = launch_tables(ctx, st.h, st.lay, st.d_times, ctx->tab);
     if (r) return r;
-    r = launch_gram_grid<double>(ctx, st.h, st.lay, ctx->tab, st.d_bg, n, hyp->jitter, noise,
-                                 LFM_UPLO_LOWER, ctx->A, Mp);
+    // fused: the factorisation writes / generates Sigma itself (GramGen, lfm_chol.hip)
+    if (fuse) gen = GramGen{ctx->tab, st.d_bg, st.h.G, st.lay.T, hyp->jitter, noise, n};
+    else
+      r = launch_gram_grid<double>(ctx, st.h, st.lay, ctx->tab, st.d_bg, n, hyp->jitter, noise,
+                                   LFM_UPLO_LOWER, ctx->A, Mp);
   } else {
     r = launch_gram_direct<double>(ctx, st.h, d_x, n, d_x, n, hyp->jitter, noise, LFM_UPLO_LOWER,
                                    ctx->A, Mp);
@@ -264,7 +273,8 @@ int mll_blocked(lfm_ctx* ctx, const Staged& st, const double* d_x, const double*
   if (r) return r;
   r = launch_augment(ctx, st.h, d_x, d_y, d_loc, n, ctx->A, Mp, Mp);
   if (r) return r;
-  r = chol_factor_solve(ctx, ctx->A, Mp, n, Mp, negative, ctx->result);
+  r = chol_factor_solve(ctx, ctx->A, Mp, n, Mp, negative, ctx->result, CHOL_MLL,
+                        fuse ? &gen : nullptr);
   if (r) return r;
   double* hres = ctx->hpin + (ctx->hpin_bytes / 8 - 8);
   hipMemcpyAsync(hres, ctx->result, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
@@ -439,10 +449,13 @@ int env_int_api(const char* name, int def) {
 //   LFM_S3_EVENTS        1: schedule 3 ordered by stream events (for rocprofv3 --pmc)
 //   LFM_DEBUG_SPIN_LIMIT poll bound of every device-side wait (tests force timeouts with 0)
 //   LFM_GRAD_DIRECT      1: the gradient's per-pair path even on a grid layout (cross-check)
+//   LFM_GRAM_FUSE        0: the full gram in its own kernel even where the first update could
+//                        generate it (cross-check: the MLL is bit-identical either way)
 hipError_t create_streams(lfm_ctx* ctx) {
   ctx->sched = env_int_api("LFM_SCHED", 3) == 1 ? 1 : 3;
   ctx->s3_events = env_int_api("LFM_S3_EVENTS", 0) != 0;
   ctx->grad_direct = env_int_api("LFM_GRAD_DIRECT", 0) != 0;
+  ctx->gram_fuse = env_int_api("LFM_GRAM_FUSE", LFM_GRAM_FUSE_DEFAULT) != 0;
   if (const char* sl = std::getenv("LFM_DEBUG_SPIN_LIMIT"))
     ctx->spin_limit = (unsigned)std::strtoul(sl, nullptr, 10);
   int least = 0, greatest = 0;
@@ -721,14 +734,18 @@ int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
   r = ensure(ctx, (void**)&ctx->gacc, &ctx->gacc_bytes, (size_t)(5 * G + 3) * sizeof(double));
   if (r) return r;
   const double noise = hyp->obs_stddev * hyp->obs_stddev;  // objectives.py:66
+  GramGen gen;
+  const bool fuse = chol_fuses_gram(ctx, CHOL_INVERSE, st.lay, n);
   if (st.lay.ok) {
     r = ensure(ctx, (void**)&ctx->tab, &ctx->tab_bytes,
                tables_doubles(st.h.G, st.lay.T) * sizeof(double));
     if (r) return r;
     r = launch_tables(ctx, st.h, st.lay, st.d_times, ctx->tab);
     if (r) return r;
-    r = launch_gram_grid<double>(ctx, st.h, st.lay, ctx->tab, st.d_bg, n, hyp->jitter, noise,
-                                 LFM_UPLO_LOWER, ctx->A, M2);
+    if (fuse) gen = GramGen{ctx->tab, st.d_bg, st.h.G, st.lay.T, hyp->jitter, noise, n};
+    else
+      r = launch_gram_grid<double>(ctx, st.h, st.lay, ctx->tab, st.d_bg, n, hyp->jitter, noise,
+                                   LFM_UPLO_LOWER, ctx->A, M2);
   } else {
     r = launch_gram_direct<double>(ctx, st.h, d_x, n, d_x, n, hyp->jitter, noise,
                                    LFM_UPLO_LOWER, ctx->A, M2);
@@ -736,7 +753,8 @@ int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
   if (r) return r;
   r = launch_augment(ctx, st.h, d_x, d_y, nullptr, n, ctx->A, M2, Mp);
   if (r) return r;
-  r = chol_factor_solve(ctx, ctx->A, M2, n, Mp, negative, ctx->result, CHOL_INVERSE);
+  r = chol_factor_solve(ctx, ctx->A, M2, n, Mp, negative, ctx->result, CHOL_INVERSE,
+                        fuse ? &gen : nullptr);
   if (r) return r;
   double* d_out = ctx->gacc + 2 * G + 1;
   r = launch_grad(ctx, st.h, d_x, n, ctx->A, M2, Mp, hyp->obs_stddev, negative, ctx->gacc, d_out,

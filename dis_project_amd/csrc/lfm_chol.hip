@@ -828,10 +828,14 @@ __device__ __forceinline__ double ldc(const double* p) {
 
 // The tile body of syrk_unit: C (TR x 128 at row i0, column j0) -= panel rows i0.. x rows j0..
 // over depth kd; CLOAD = false: C starts from zero (not read).
-template <bool CIO, int TR, int KS, bool LDCOH, bool CLOAD>
+// GEN: C is not read but generated from the gram tables (GramGen, a tile inside one gene pair
+// of an aligned grid layout): the tile's Toeplitz windows and row / column tables staged in
+// sP first, then gram_grid_aligned_kernel's arithmetic per element (bit-identical Sigma).
+template <bool CIO, int TR, int KS, bool LDCOH, bool CLOAD, bool GEN = false>
 __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, Panel P, int kd,
                                           int64_t i0, int64_t j0, bool diag, bool coh,
-                                          double (*__restrict__ sP)[KS + 1]) {
+                                          double (*__restrict__ sP)[KS + 1],
+                                          const GramGen* gen = nullptr) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
@@ -840,11 +844,71 @@ __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, P
   const int ld4 = (int)(4 * lda);  // row-group stride (elements); 60 * ld4 < 2^31 for lda < 2^23
 
   double acc[IRN][4];
+  if constexpr (GEN) {
+    constexpr int WIN = ST + TR - 1;
+    static_assert(4 * WIN + 3 * TR + 3 * ST <= (TR + ST) * (KS + 1), "gram windows in sP");
+    double* sWk = &sP[0][0];
+    double* sXk = sWk + WIN;
+    double* sWj = sXk + WIN;
+    double* sXj = sWj + WIN;
+    double* sPk = sXj + WIN;  // rows: Pt[k][tau], Et[j][tau], Qt[j][tau]
+    double* sEj = sPk + TR;
+    double* sQj = sEj + TR;
+    double* sPj = sQj + TR;   // columns: Pt[j][tau'], Et[k][tau'], Qt[k][tau']
+    double* sEk = sPj + ST;
+    double* sQk = sEk + ST;
+    const int Tn = gen->Tn, G = gen->G;
+    const int64_t Wd = 2 * (int64_t)Tn - 1;
+    const double* Wt = gen->tab;
+    const double* Xt = Wt + (int64_t)G * Wd;
+    const double* Pt = Xt + (int64_t)G * Wd;
+    const double* Et = Pt + (int64_t)G * Tn;
+    const double* Qt = Et + (int64_t)G * Tn;
+    const double* Cm = Qt + (int64_t)G * Tn;
+    const int j = gen->bg[i0 / Tn], k = gen->bg[j0 / Tn];
+    const int tau0 = (int)(i0 % Tn), tp0 = (int)(j0 % Tn);
+    const int dmin = tp0 - tau0 - (TR - 1);
+    for (int e = tid; e < WIN; e += 256) {
+      const int64_t d = dmin + e;
+      sWk[e] = Wt[(int64_t)k * Wd + (Tn - 1) + d];
+      sXk[e] = Xt[(int64_t)k * Wd + (Tn - 1) + d];
+      sWj[e] = Wt[(int64_t)j * Wd + (Tn - 1) - d];
+      sXj[e] = Xt[(int64_t)j * Wd + (Tn - 1) - d];
+    }
+    if (tid < TR) {
+      sPk[tid] = Pt[(int64_t)k * Tn + tau0 + tid];
+      sEj[tid] = Et[(int64_t)j * Tn + tau0 + tid];
+      sQj[tid] = Qt[(int64_t)j * Tn + tau0 + tid];
+    }
+    if (tid < ST) {
+      sPj[tid] = Pt[(int64_t)j * Tn + tp0 + tid];
+      sEk[tid] = Et[(int64_t)k * Tn + tp0 + tid];
+      sQk[tid] = Qt[(int64_t)k * Tn + tp0 + tid];
+    }
+    const double Cjk = Cm[(int64_t)j * G + k];
+    __syncthreads();
 #pragma unroll
-  for (int ir = 0; ir < IRN; ++ir)
+    for (int ir = 0; ir < IRN; ++ir)
 #pragma unroll
-    for (int jr = 0; jr < 4; ++jr)
-      acc[ir][jr] = (CIO && CLOAD) ? -ldc<LDCOH>(&Cb[ir * ld4 + jr * 16]) : 0.0;
+      for (int jr = 0; jr < 4; ++jr) {
+        const int rl = wr + ir * 4 + lk, cl = wc + jr * 16 + li, e = cl - rl + (TR - 1);
+        double v = sWk[e] + sWj[e];
+        v = fma(-sXk[e], sPk[rl], v);
+        v = fma(-sXj[e], sPj[cl], v);
+        v = fma(-(sEk[cl] * sEj[rl]), sQk[cl] + sQj[rl], v);
+        v = Cjk * v;
+        if (i0 + rl == j0 + cl) v = (v + gen->da1) + gen->da2;
+        acc[ir][jr] = -v;
+        if (jr == 3) __builtin_amdgcn_sched_barrier(0);  // one row group's reads at a time
+      }
+    __syncthreads();  // the windows are read: sP is the K stages' again
+  } else {
+#pragma unroll
+    for (int ir = 0; ir < IRN; ++ir)
+#pragma unroll
+      for (int jr = 0; jr < 4; ++jr)
+        acc[ir][jr] = (CIO && CLOAD) ? -ldc<LDCOH>(&Cb[ir * ld4 + jr * 16]) : 0.0;
+  }
   gemm_accumulate<TR, false, LDCOH, KS>(P.p + (i0 - P.r0) * P.ld, P.ld, P.p + (j0 - P.r0) * P.ld,
                                         P.ld, kd, acc, sP);
 
@@ -881,7 +945,8 @@ __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, i
                                           double (*__restrict__ sP)[KS + 1], int coh_lim = 0,
                                           int64_t pad_after = INT64_MAX,
                                           int64_t pad_end = INT64_MAX,
-                                          int64_t zero_from = INT64_MAX) {
+                                          int64_t zero_from = INT64_MAX,
+                                          const GramGen* gen = nullptr) {
   constexpr int SUB = ST / TR;  // row tiles per 128 rows
   int ti, tj;  // ti in TR-row units
   if (LFM_BAND_ROWS && tj_hi - tj_lo <= 8 && ti0 >= tj_hi) {
@@ -947,6 +1012,8 @@ __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, i
   // per evaluation; a selected base pointer costs 2 VGPRs, occupancy 4 -> 3 waves / SIMD.)
   if (i0 >= zero_from)
     syrk_tile<CIO, TR, KS, LDCOH, false>(A, lda, P, kd, i0, j0, diag, coh, sP);
+  else if (gen && i0 + TR <= gen->n)
+    syrk_tile<CIO, TR, KS, LDCOH, false, true>(A, lda, P, kd, i0, j0, diag, coh, sP, gen);
   else
     syrk_tile<CIO, TR, KS, LDCOH, true>(A, lda, P, kd, i0, j0, diag, coh, sP);
   return in_lead;
@@ -1034,6 +1101,7 @@ struct StepArgs {
   // copy_from (= Mp + K0: A21 is the identity there) copy Bd's row (row - copy_from)
   int64_t zero_from;
   int64_t copy_from;
+  GramGen gen;       // gen.tab != NULL: the first step's update units generate Sigma (fused gram)
 };
 
 // Diagnostics: atomic max of the 100 MHz clock (or of its bitwise NOT: the earliest start)
@@ -1077,7 +1145,8 @@ __global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) {
     // device-coherent stores + a counter bump once they have completed: the tall units read
     // these rows with device-coherent loads (no L2 writeback / invalidate on either side)
     syrk_unit<true, 64, true, LFM_STEP_KS>(g.A, g.lda, g.s0, g.px, g.kd, g.T, 0, g.wn, u, g.wn, sPu,
-                                           0, g.n, g.pad_end, g.zero_from);
+                                           0, g.n, g.pad_end, g.zero_from,
+                                           g.gen.tab ? &g.gen : nullptr);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     // 128-tile row of the unit (the band's enumeration order, syrk_unit)
@@ -1101,7 +1170,8 @@ __global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) {
     const bool lead = syrk_unit<true, 64, false, LFM_STEP_KS>(g.A, g.lda, g.s0, g.px, g.kd, g.T,
                                                               g.wn, g.T, u, 0, sPu,
                                                               g.xready ? g.wn + g.lead : 0, g.n,
-                                                              g.pad_end, g.zero_from);
+                                                              g.pad_end, g.zero_from,
+                                                              g.gen.tab ? &g.gen : nullptr);
     if (lead) bump_after_stores(g.xready);
     if (st) {
       __syncthreads();
@@ -1905,8 +1975,13 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   return hip_fail(ctx, e, "probe_syrk");
 }
 
+bool chol_fuses_gram(const lfm_ctx* ctx, int mode, const GridLayout& lay, int64_t n) {
+  return ctx->gram_fuse && lay.ok && lay.T % 256 == 0 && n % 256 == 0 && n >= 1024 &&
+         ctx->sched == 3 && ctx->side_cus > 0 && mode != CHOL_SCHUR;
+}
+
 int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,
-                      double* d_out, int mode) {
+                      double* d_out, int mode, const GramGen* gen) {
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&panel_kernel),
@@ -1963,6 +2038,16 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   const int S = (int)steps.size();
   r = ensure_events(ctx, 2 * (size_t)S + 3);
   if (r) return r;
+  // fused gram (GramGen): in memory only the first block column (chain(0), X_0) and the next
+  // super-panel's diagonal block (chain(1)); launch 0's update units generate the rest
+  const bool fused = gen && s3 && S >= 2;
+  if (gen) {
+    const int64_t K10 = (int64_t)steps[0].second * NB;
+    const int64_t K11 = fused ? (int64_t)(steps[1].first + steps[1].second) * NB : n;
+    r = launch_gram_region(ctx, *gen, 0, n, 0, fused ? K10 : n, A, lda);
+    if (!r && fused) r = launch_gram_region(ctx, *gen, K10, std::min(K11, n), K10, K11, A, lda);
+    if (r) return r;
+  }
   hipStream_t main = ctx->stream, side = ctx->side;
   hipEvent_t* ev = ctx->evs.data();  // [0]: inputs ready; E1_s = ev[1 + 2s]; E2_s = ev[2 + 2s]
   Launcher L{ctx, A, lda, bordered ? 2 * Mp : Mp, bordered ? Mp : 0};
@@ -2128,6 +2213,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.T = T;
       g.wn = wn;
       if (bordered) g.zero_from = Mp + steps[s].first * NB;
+      if (fused && s == 0) g.gen = *gen;
       g.na = 2 * wn * (T - wn);
       g.nr = (T - wn) * (T - wn + 1);  // 2 slabs per tile of the (T - wn)-tile triangle
       g.status = ctx->status;

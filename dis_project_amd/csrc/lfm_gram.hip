@@ -269,6 +269,48 @@ int launch_gram_grid(lfm_ctx* ctx, const HypDev& h, const GridLayout& lay, const
   return hip_fail(ctx, hipGetLastError(), "gram_grid_kernel");
 }
 
+// Lower elements (c <= r) of rows [r0, r1) x columns [c0, c1) of the aligned-grid gram, one
+// thread per element from the tables in global memory, with gram_grid_aligned_kernel's
+// arithmetic (bit-identical). The fused factorisation writes only these blocks.
+__global__ __launch_bounds__(256) void gram_region_kernel(GramGen g, int64_t r0, int64_t c0,
+                                                          int64_t nr, int64_t nc, double* out,
+                                                          int64_t ldo) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= nr * nc) return;
+  const int64_t r = r0 + idx / nc, c = c0 + idx % nc;
+  if (c > r) return;
+  const int Tn = g.Tn, G = g.G;
+  const int64_t W = 2 * (int64_t)Tn - 1;
+  const double* Wt = g.tab;
+  const double* Xt = Wt + (int64_t)G * W;
+  const double* Pt = Xt + (int64_t)G * W;
+  const double* Et = Pt + (int64_t)G * Tn;
+  const double* Qt = Et + (int64_t)G * Tn;
+  const double* Cm = Qt + (int64_t)G * Tn;
+  const int j = g.bg[r / Tn], k = g.bg[c / Tn];
+  const int tau = (int)(r % Tn), tp = (int)(c % Tn), d = tp - tau;
+  double v = Wt[k * W + (Tn - 1) + d] + Wt[j * W + (Tn - 1) - d];
+  v = fma(-Xt[k * W + (Tn - 1) + d], Pt[(int64_t)k * Tn + tau], v);
+  v = fma(-Xt[j * W + (Tn - 1) - d], Pt[(int64_t)j * Tn + tp], v);
+  v = fma(-(Et[(int64_t)k * Tn + tp] * Et[(int64_t)j * Tn + tau]),
+          Qt[(int64_t)k * Tn + tp] + Qt[(int64_t)j * Tn + tau], v);
+  v = Cm[(int64_t)j * G + k] * v;
+  if (r == c) v = (v + g.da1) + g.da2;
+  out[r * ldo + c] = v;
+}
+
+int launch_gram_region(lfm_ctx* ctx, const GramGen& g, int64_t r0, int64_t r1, int64_t c0,
+                       int64_t c1, double* out, int64_t ldo) {
+  const int64_t nr = r1 - r0, nc = c1 - c0;
+  if (nr <= 0 || nc <= 0) return LFM_OK;
+  hipEvent_t ev;
+  prof_begin(ctx, K_GRAM_GRID, &ev);
+  hipLaunchKernelGGL(gram_region_kernel, dim3((unsigned)((nr * nc + 255) / 256)), dim3(256), 0,
+                     ctx->stream, g, r0, c0, nr, nc, out, ldo);
+  prof_end(ctx, K_GRAM_GRID, ev, 0, (double)nr * nc * 8);
+  return hip_fail(ctx, hipGetLastError(), "gram_region_kernel");
+}
+
 template int launch_gram_grid<double>(lfm_ctx*, const HypDev&, const GridLayout&, const double*,
                                       const int*, int64_t, double, double, int, double*, int64_t);
 template int launch_gram_grid<float>(lfm_ctx*, const HypDev&, const GridLayout&, const double*,

@@ -85,6 +85,7 @@ struct lfm_ctx {
   bool s3_events = false;                        // schedule 3 ordered by events (LFM_S3_EVENTS)
   unsigned spin_limit = 1u << 26;                // device-side wait bound (LFM_DEBUG_SPIN_LIMIT)
   bool grad_direct = false;                      // gradient: per-pair path only (LFM_GRAD_DIRECT)
+  bool gram_fuse = true;                         // gram in the first update (LFM_GRAM_FUSE)
   double* gtab = nullptr; size_t gtab_bytes = 0; // gradient tables (grid layout)
   double* result = nullptr;                      // [0..] scalar results
   double* gacc = nullptr; size_t gacc_bytes = 0; // gradient accumulators + output
@@ -193,10 +194,27 @@ int launch_h(lfm_ctx* ctx, const HypDev& h, const int64_t* j, const int64_t* k, 
 int launch_augment(lfm_ctx* ctx, const HypDev& h, const double* x, const double* y,
                    const double* loc, int64_t n, double* A, int64_t lda, int64_t Mp);
 
+// The gram of an aligned grid layout (T % 256 == 0) fused into the factorisation's first
+// trailing update (schedule 3): chol_factor_solve writes only the block columns the chains
+// and the first panel solve read (launch_gram_region), and the first step's update units
+// generate their Sigma tiles from the tables (gram_grid_aligned_kernel's arithmetic, bit-
+// identical) instead of loading them. tab: tables_doubles layout; bg: block genes.
+struct GramGen {
+  const double* tab = nullptr;
+  const int* bg = nullptr;
+  int G = 0, Tn = 0;
+  double da1 = 0.0, da2 = 0.0;
+  int64_t n = 0;  // rows >= n (residual, padding) come from memory (augment_kernel)
+};
+int launch_gram_region(lfm_ctx* ctx, const GramGen& g, int64_t r0, int64_t r1, int64_t c0,
+                       int64_t c1, double* out, int64_t ldo);
+
 // cholesky kernels (lfm_chol.hip)
 enum CholMode { CHOL_MLL = 0, CHOL_INVERSE = 1, CHOL_SCHUR = 2 };
+// gen: the gram to fuse (lfm_api decides with chol_fuses_gram; the full gram is then NOT in A)
 int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,
-                      double* d_out, int mode = CHOL_MLL);
+                      double* d_out, int mode = CHOL_MLL, const GramGen* gen = nullptr);
+bool chol_fuses_gram(const lfm_ctx* ctx, int mode, const GridLayout& lay, int64_t n);
 size_t tables_doubles(int G, int T);
 
 // gradient kernels (lfm_grad.hip)
