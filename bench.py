@@ -260,8 +260,15 @@ def main(argv=None):
                 line["roofline"]["chain_flops_per_eval"] = chain["flops"] / prof_steps
         if gram.get("launches"):
             gbs = gram["bytes"] / (gram["total_ms"] * 1e-3) / 1e9
+            # fused (the schedule-3 default on this layout): the gram kernel writes only the
+            # first block column and the next super-panel's diagonal block; the first trailing
+            # update generates every other Sigma tile from the tables
+            fused = gram["bytes"] < 0.5 * 8.0 * n * (n + 1) / 2 * prof_steps
             line["gram_roofline"] = {
-                "kernel": "gram_grid_aligned_kernel (lower-triangle fp64 fill)", "bound": "hbm",
+                "kernel": ("gram_region_kernel (first block column + next diagonal block; the "
+                           "rest of Sigma is generated inside the first trailing update)" if fused
+                           else "gram_grid_aligned_kernel (lower-triangle fp64 fill)"),
+                "fused": bool(fused), "bound": "hbm",
                 "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": gbs / HBM_PEAK_GBS,
                 "bytes_per_launch": gram["bytes"] / gram["launches"],

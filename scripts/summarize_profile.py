@@ -77,10 +77,11 @@ def main():
     if syrk:
         launches = sum(v["launches"] for _, v in syrk)
         total = sum(v["hbm_bytes_per_launch"] * v["launches"] for _, v in syrk)
-        # evaluations in the PMC run = gram launches (one per MLL evaluation); the PMC passes run
+        # evaluations in the PMC run = finalize launches (one per MLL evaluation; the gram kernel
+        # no longer runs once per evaluation where it is fused); the PMC passes run
         # schedule 3 event-ordered (LFM_S3_EVENTS=1), which splits the launches differently from
         # the bench, so bench.py converts the per-evaluation bytes to its own launch count
-        evals = max(1, out.get("gram_grid_aligned_kernel<double>", {}).get("launches", 1))
+        evals = max(1, out.get("finalize_kernel", {}).get("launches", 1))
         json.dump({"round": rnd, "source": f"profiles/{rnd}_hbm.json (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                    "kernels": [k for k, _ in syrk],
                    "hbm_bytes_per_eval": total / evals, "evals": evals,
