@@ -286,17 +286,66 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
     for (int q = 0; q < IB; ++q) d[q] = (lane < IB && q <= lane) ? MS(c0 + li, c0 + q) : 0.0;
     // PH bit 7: 64-bit DPP moves (v_mov_b64_dpp, one instruction per broadcast) instead of
     // two 32-bit ones
+    if constexpr ((PH & 128) != 0) {
+      // pipelined: column c's update of column c + 1 first, then the pivot chain of c + 1
+      // (broadcast, rsqrt, Newton) is issued ahead of c's remaining updates, whose latency it
+      // hides; the same operations per element in the same order (bit-identical)
+      double dc = row_bcast64(d[0], 0);
+      if (kb + c0 >= npiv) dc = 1.0;
+      double y = rsqrt_1nr(dc);
 #pragma unroll
-    for (int c = 0; c < IB; ++c) {
-      double dc = (PH & 128) ? row_bcast64(d[c], c) : row_bcast(d[c], c);
-      if (kb + c0 + c >= npiv) dc = 1.0;
-      const double y = rsqrt_1nr(dc);
-      pv[c] = dc;
-      yv[c] = y;
-      d[c] = (lane == c) ? dc * y : d[c] * y;
+      for (int c = 0; c < IB; ++c) {
+        pv[c] = dc;
+        yv[c] = y;
+        d[c] = (lane == c) ? dc * y : d[c] * y;
+        if (c + 1 < IB) {
+          d[c + 1] = fma(-d[c], row_bcast64(d[c], c + 1), d[c + 1]);
+          double dn = row_bcast64(d[c + 1], c + 1);
+          if (kb + c0 + c + 1 >= npiv) dn = 1.0;
+          // rsqrt_1nr(dn) = r * fma(-0.5 dn * r, r, 1.5), its dependent steps spread over the
+          // remaining updates in four chunks (scheduling fences keep the interleave: the wave
+          // issues in order, so a dependent step stalls it unless independent work sits between)
+          const double r = __builtin_amdgcn_rsq(dn);
+          const double hh = -0.5 * dn;
+          const int REM = IB - c - 2, K = (REM + 3) / 4;
+          double t1 = 0.0, t2 = 0.0, yn = 0.0;
 #pragma unroll
-      for (int q = c + 1; q < IB; ++q)
-        d[q] = fma(-d[c], (PH & 128) ? row_bcast64(d[c], q) : row_bcast(d[c], q), d[q]);
+          for (int part = 0; part < 4; ++part) {
+            // a chunk's broadcasts first, then its FMAs (each FMA would otherwise wait on the
+            // broadcast issued just before it)
+            double bq[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {  // K <= 4 (REM <= 14)
+              const int q = c + 2 + part * K + i;
+              if (i < K && q < IB) bq[i] = row_bcast64(d[c], q);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int q = c + 2 + part * K + i;
+              if (i < K && q < IB) d[q] = fma(-d[c], bq[i], d[q]);
+            }
+            if (part == 0) t1 = hh * r;
+            if (part == 1) t2 = fma(t1, r, 1.5);
+            if (part == 2) yn = r * t2;
+            __builtin_amdgcn_sched_barrier(0);
+          }
+          dc = dn;
+          y = yn;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < IB; ++c) {
+        double dc = row_bcast(d[c], c);
+        if (kb + c0 + c >= npiv) dc = 1.0;
+        const double y = rsqrt_1nr(dc);
+        pv[c] = dc;
+        yv[c] = y;
+        d[c] = (lane == c) ? dc * y : d[c] * y;
+#pragma unroll
+        for (int q = c + 1; q < IB; ++q) d[q] = fma(-d[c], row_bcast(d[c], q), d[q]);
+      }
     }
     if (lane < IB) {
 #pragma unroll
