@@ -180,6 +180,21 @@ def main(argv=None):
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # the exchange step alone (collective latency reported separately): the same
+    # RCCL all-gather of this workload's NaN-padded slots, outside the timed region
+    collective = None
+    if world > 1:
+        slots = max(farm.slots_per_rank(per_step, world), 1)
+        lat = []
+        for _ in range(25):
+            barrier()
+            t1 = time.perf_counter()
+            gather(np.full(slots, np.nan))
+            lat.append((time.perf_counter() - t1) * 1e6)
+        lt = torch.tensor([float(np.median(lat[5:]))], dtype=torch.float64)
+        dist.all_reduce(lt, op=dist.ReduceOp.MAX)
+        collective = {"op": "ncclAllGather (RCCL)", "bytes_per_rank": 8 * slots,
+                      "latency_us_median": float(lt.item())}
     # the timed region's results: all finite, every step the same values (same inputs)
     res = np.array(timed)
     if not np.all(np.isfinite(res)):
@@ -223,6 +238,8 @@ def main(argv=None):
                                if world > 1 else "none"},
         "mll_first": float(res[0][0]),
     }
+    if collective:
+        line["collective"] = collective
     if a.workload == "c2":
         line["cholesky_gflops_per_gpu"] = chol_flops / (ms_per_step * 1e-3) / 1e9
     if prof and rank == 0:
