@@ -850,6 +850,10 @@ struct Panel {
 #endif
 // Bulk trailing update (step_kernel's update units): K depth of one LDS stage and the unroll
 // of the 4-deep MFMA steps within it
+// schedule-3 MLL bulk super-panel width in block columns
+#ifndef LFM_WBULK
+#define LFM_WBULK 5
+#endif
 // rest-triangle enumeration: tile rows in groups of Q, Q x Q supertiles within a group (1: row
 // by row)
 #ifndef LFM_SUPERTILE
@@ -2066,19 +2070,27 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     r = launch_border_init(ctx, A, lda, Mp);
     if (r) return r;
   }
-  // Step plan: super-panels of w = 4 block columns while the trailing matrix has at least
-  // LFM_W4_MIN rows, w = 2 down to LFM_W2_MIN, then w = 1, so the bulk trailing update runs
-  // with depth 128 w (C traffic per flop / w). Schedule 3: w = 4 down to 6144 rows, then one
-  // or two w = 2 steps down to 5120 — the last deep update would otherwise hold up the first
-  // w = 1 chains (measured 0.13-0.24 ms faster than going from w = 4 to w = 1 directly); its
-  // first super-panel is one block wide (its factor precedes any bulk work).
+  // Step plan: super-panels of w = wbulk (5, schedule-3 MLL; else 4) block columns while the
+  // trailing matrix has at least LFM_W4_MIN rows, w = 2 down to LFM_W2_MIN, then w = 1, so the
+  // bulk trailing update runs with depth 128 w (C traffic per flop / w). Schedule 3: the bulk
+  // width down to 6144 rows, then one or two w = 2 steps down to 5120 — the last deep update
+  // would otherwise hold up the first w = 1 chains (measured 0.13-0.24 ms faster than going
+  // straight to w = 1); its first super-panel is one block wide (its factor precedes any bulk
+  // work).
   const int64_t w4min = env_int("LFM_W4_MIN", 6144);
+  // bulk width: 5 block columns (W = 640) for the MLL — its C traffic per flop is 4/5 of W = 512
+  // and its chain still hides behind the update (A/B: -0.23..-0.26 ms per evaluation; W = 768
+  // and 896 were slower, 1024 much slower); the bordered gradient keeps 4 (5 measured equal)
+  const int wbulk = s3 && !bordered ? LFM_WBULK : 4;
   const int64_t w2min = env_int("LFM_W2_MIN", s3 ? 5120 : 4096);
   std::vector<std::pair<int64_t, int>> steps;
   for (int64_t k = 0; k < nblk;) {
     const int64_t m = bordered ? Mp + NB : Mp - k * NB;
     int w = 1;
-    if (m >= w4min && k + 4 <= nblk) w = 4;
+    // the first bulk super-panel stays 4 wide: its chain runs beside the shallow first update
+    const int wk = steps.size() == 1 ? 4 : wbulk;
+    if (m >= w4min && k + wk <= nblk) w = wk;
+    else if (m >= w4min && k + 4 <= nblk) w = 4;
     else if (m >= w2min && k + 2 <= nblk) w = 2;
     if (k == 0 && s3) w = 1;
     steps.emplace_back(k, w);

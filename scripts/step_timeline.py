@@ -31,7 +31,10 @@ def plan(n, bordered=False):
     steps, k = [], 0
     while k < nblk:
         m = Mp + NB if bordered else Mp - k * NB
-        w = 4 if (m >= w4 and k + 4 <= nblk) else 2 if (m >= w2 and k + 2 <= nblk) else 1
+        # the bulk width (lfm_chol.hip chol_factor_solve): 5, its first super-panel 4 (MLL)
+        wb = 4 if bordered or len(steps) == 1 else 5
+        w = wb if (m >= w4 and k + wb <= nblk) else 4 if (m >= w4 and k + 4 <= nblk) else \
+            2 if (m >= w2 and k + 2 <= nblk) else 1
         if k == 0:
             w = 1
         steps.append((k, w))
