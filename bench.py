@@ -13,7 +13,8 @@ One process per GPU. Workloads:
                 per rank). Weak scaling: value = evaluations by all ranks / wall.
   c3            configs[2]: a step = the 32 random restarts of C2, statically partitioned over
                 the ranks (farm.partition, ceil(32/W) slots per rank), one RCCL all-gather of
-                the NaN-padded slots. Strong scaling: value = 32 x steps / wall.
+                the NaN-padded slots. Strong scaling: value = 32 x steps / wall. Each rank keeps
+                --workers (3) evaluations in flight (farm.ConcurrentEvaluator).
   c5            configs[4]: a step = the 15 replicate x leave-one-gene-out problems (N = 28),
                 each rank's share in one batched launch, then the all-gather. Strong scaling.
 torch.distributed (gloo, CPU) is only the control plane: barrier, max-over-ranks timing and
@@ -59,10 +60,16 @@ def parse(argv=None):
     p.add_argument("--genes", type=int, default=64)
     p.add_argument("--timepoints", type=int, default=256)
     p.add_argument("--restarts", type=int, default=32)
+    p.add_argument("--workers", type=int, default=3,
+                   help="c3: evaluations in flight per GPU (farm.ConcurrentEvaluator, schedule-1 "
+                        "worker contexts); 1 = one schedule-3 context, one evaluation at a time")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-profile", action="store_true",
                    help="do not record per-kernel HIP events in the timed region")
+    p.add_argument("--gather", choices=["rccl", "gloo"], default="rccl",
+                   help="rehearsal only: gloo all-gather and ranks sharing the visible GPUs "
+                        "(W ranks on fewer cards); the measured configuration is rccl")
     return p.parse_args(argv)
 
 
@@ -113,12 +120,16 @@ def main(argv=None):
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    ctx = _lib.get_context(local)
+    # one GPU per rank; the gloo rehearsal may put several ranks on one card
+    dev = local % max(1, _lib.device_count()) if a.gather == "gloo" else local
+    ctx = _lib.get_context(dev)
     lib, h = ctx.lib, ctx.handle
 
     # RCCL farm communicator (replicas-only exchange of per-rank results)
     gather = None
-    if world > 1:
+    if world > 1 and a.gather == "gloo":
+        gather = farm.TorchGather(world)
+    elif world > 1:
         obj = [farm.RcclGather.unique_id(ctx) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         gather = farm.RcclGather(ctx, world, rank, obj[0])
@@ -140,7 +151,8 @@ def main(argv=None):
     else:
         models, datasets = farm.workload(a.workload, a.genes, a.timepoints, a.restarts)
         n = datasets[0].n
-        evaluate, close = farm.gpu_evaluator(ctx, datasets, negative=False)
+        evaluate, close = farm.gpu_evaluator(ctx, datasets, negative=False,
+                                           workers=a.workers)
         per_step = len(models)
 
         def step():
@@ -193,7 +205,8 @@ def main(argv=None):
             lat.append((time.perf_counter() - t1) * 1e6)
         lt = torch.tensor([float(np.median(lat[5:]))], dtype=torch.float64)
         dist.all_reduce(lt, op=dist.ReduceOp.MAX)
-        collective = {"op": "ncclAllGather (RCCL)", "bytes_per_rank": 8 * slots,
+        collective = {"op": "ncclAllGather (RCCL)" if a.gather == "rccl" else "gloo all_gather",
+                      "bytes_per_rank": 8 * slots,
                       "latency_us_median": float(lt.item())}
     # the timed region's results: all finite, every step the same values (same inputs)
     res = np.array(timed)
@@ -212,7 +225,9 @@ def main(argv=None):
               f"N={n}, fp64")
     elif a.workload == "c3":
         wl = (f"configs[2]: {len(res[0])} random restarts of the {a.genes}x{a.timepoints} grid "
-              f"(N={n}, fp64) per step, farmed over {world} GPU(s)")
+              f"(N={n}, fp64) per step, farmed over {world} GPU(s), "
+              + (f"{a.workers} concurrent schedule-1 evaluations per GPU" if a.workers > 1
+                 else "one schedule-3 evaluation at a time per GPU"))
     else:
         wl = (f"configs[4]: 3 replicates x 5 leave-one-gene-out ablations (N={n}) per step, "
               f"farmed over {world} GPU(s), one batched launch per rank")

@@ -93,6 +93,8 @@ PRODUCT_SIGNATURES = [
     ("lfm_last_error", c_char_p, [_c_ctx]),
     ("lfm_ctx_synchronize", c_int, [_c_ctx]),
     ("lfm_ctx_set_block", c_int, [_c_ctx, c_int]),
+    ("lfm_ctx_set_schedule", c_int, [_c_ctx, c_int]),
+    ("lfm_ctx_get_schedule", c_int, [_c_ctx, POINTER(c_int)]),
     ("lfm_mean_function_f64", c_int, [_c_ctx, _dptr, c_int64, POINTER(LfmHyp), _dptr]),
     ("lfm_cross_covariance_f64", c_int,
      [_c_ctx, _dptr, c_int64, _dptr, c_int64, POINTER(LfmHyp), _dptr, c_int64]),
@@ -246,6 +248,17 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    # -- factorisation schedule (include/lfm.h: lfm_ctx_set_schedule)
+    @property
+    def schedule(self) -> int:
+        out = c_int(0)
+        self.check(self.lib.lfm_ctx_get_schedule(self.handle, ctypes.byref(out)))
+        return out.value
+
+    @schedule.setter
+    def schedule(self, value: int):
+        self.check(self.lib.lfm_ctx_set_schedule(self.handle, int(value)))
 
     # -- profiling
     def profile(self, on: bool = True, classes=None):

@@ -451,27 +451,14 @@ int env_int_api(const char* name, int def) {
 //   LFM_GRAD_DIRECT      1: the gradient's per-pair path even on a grid layout (cross-check)
 //   LFM_GRAM_FUSE        0: the full gram in its own kernel even where the first update could
 //                        generate it (cross-check: the MLL is bit-identical either way)
-hipError_t create_streams(lfm_ctx* ctx) {
-  ctx->sched = env_int_api("LFM_SCHED", 3) == 1 ? 1 : 3;
-  ctx->s3_events = env_int_api("LFM_S3_EVENTS", 0) != 0;
-  ctx->grad_direct = env_int_api("LFM_GRAD_DIRECT", 0) != 0;
-  ctx->gram_fuse = env_int_api("LFM_GRAM_FUSE", LFM_GRAM_FUSE_DEFAULT) != 0;
-  if (const char* sl = std::getenv("LFM_DEBUG_SPIN_LIMIT"))
-    ctx->spin_limit = (unsigned)std::strtoul(sl, nullptr, 10);
-  int least = 0, greatest = 0;
-  hipDeviceGetStreamPriorityRange(&least, &greatest);
-  const int side_cus = env_int_api("LFM_SIDE_CUS", 32);
-  hipDeviceProp_t prop;
-  hipGetDeviceProperties(&prop, ctx->device);
-  const int ncu = prop.multiProcessorCount;
-  if (ncu > 0) ctx->cus = ncu;
-  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest);
-  if (e != hipSuccess || side_cus <= 0 || side_cus >= ncu) return e;
-  // Schedule 3 stream pair: CU mask bits [0, cus) for the factor chain (consecutive bits,
-  // which the hardware spreads over the XCDs: bit c lives on XCD c % 8), every other CU for the
-  // main (bulk) stream. The chain kernel needs all of its workgroups (one per CU) resident at
-  // once: checked here, halving the reservation until it holds.
+// Schedule 3's stream pair: CU mask bits [0, cus) for the factor chain (consecutive bits,
+// which the hardware spreads over the XCDs: bit c lives on XCD c % 8), every other CU for the
+// main (bulk) stream. The chain kernel needs all of its workgroups (one per CU) resident at
+// once: checked here, halving the reservation until it holds. Each CU-masked stream holds a
+// hardware queue of its own for the context's lifetime, idle or not.
+hipError_t create_partition(lfm_ctx* ctx, int side_cus) {
+  const int ncu = ctx->cus;
+  if (ctx->m3 || side_cus <= 0 || side_cus >= ncu) return hipSuccess;
   for (int cus = side_cus; cus >= 4; cus /= 2) {
     // every XCD keeps the same number of main CUs, or the partition is refused (measured:
     // an XCD left without main CUs never ran the main launch's workgroups dealt to it)
@@ -482,7 +469,7 @@ hipError_t create_streams(lfm_ctx* ctx) {
       continue;
     std::vector<uint32_t> mside((ncu + 31) / 32, 0u), mmain((ncu + 31) / 32, 0u);
     for (int c = 0; c < ncu; ++c) (c < cus ? mside : mmain)[c / 32] |= 1u << (c % 32);
-    e = hipExtStreamCreateWithCUMask(&ctx->m3, (uint32_t)mmain.size(), mmain.data());
+    hipError_t e = hipExtStreamCreateWithCUMask(&ctx->m3, (uint32_t)mmain.size(), mmain.data());
     if (e == hipSuccess)
       e = hipExtStreamCreateWithCUMask(&ctx->s3, (uint32_t)mside.size(), mside.data());
     if (e != hipSuccess) return e;
@@ -498,6 +485,50 @@ hipError_t create_streams(lfm_ctx* ctx) {
   }
   ctx->side_cus = 0;  // no usable partition: schedule 1
   return hipSuccess;
+}
+
+// Give the pair's hardware queues back (schedule 1 never uses them). Measured on C3: idle
+// CU-masked queues of other contexts in the process oversubscribe the hardware scheduler —
+// one schedule-1 evaluation at a time ran 23.3 evals/s beside three idle partitioned contexts
+// against 29.1 alone.
+void release_partition(lfm_ctx* ctx) {
+  for (hipStream_t* st : {&ctx->s3, &ctx->m3})
+    if (*st) {
+      hipStreamSynchronize(*st);
+      hipStreamDestroy(*st);
+      *st = nullptr;
+    }
+  ctx->side_cus = 0;
+}
+
+// Main + high-priority side stream (every CU), and for schedule 3 the CU-partitioned pair:
+// LFM_SIDE_CUS (default 32) CUs for the factor chain, the rest for the bulk
+// (hipExtStreamCreateWithCUMask). The documented knobs read here:
+//   LFM_SCHED            3 (default) or 1: the look-ahead schedule of the MLL factorisation
+//                        (1: no CU partition is created; lfm_ctx_set_schedule changes it later)
+//   LFM_SIDE_CUS         CUs reserved for the schedule-3 factor chain (0: schedule 1 only)
+//   LFM_S3_EVENTS        1: schedule 3 ordered by stream events (for rocprofv3 --pmc)
+//   LFM_DEBUG_SPIN_LIMIT poll bound of every device-side wait (tests force timeouts with 0)
+//   LFM_GRAD_DIRECT      1: the gradient's per-pair path even on a grid layout (cross-check)
+//   LFM_GRAM_FUSE        0: the full gram in its own kernel even where the first update could
+//                        generate it (cross-check: the MLL is bit-identical either way)
+hipError_t create_streams(lfm_ctx* ctx) {
+  ctx->sched = env_int_api("LFM_SCHED", 3) == 1 ? 1 : 3;
+  ctx->s3_events = env_int_api("LFM_S3_EVENTS", 0) != 0;
+  ctx->grad_direct = env_int_api("LFM_GRAD_DIRECT", 0) != 0;
+  ctx->gram_fuse = env_int_api("LFM_GRAM_FUSE", LFM_GRAM_FUSE_DEFAULT) != 0;
+  if (const char* sl = std::getenv("LFM_DEBUG_SPIN_LIMIT"))
+    ctx->spin_limit = (unsigned)std::strtoul(sl, nullptr, 10);
+  int least = 0, greatest = 0;
+  hipDeviceGetStreamPriorityRange(&least, &greatest);
+  ctx->side_req = env_int_api("LFM_SIDE_CUS", 32);
+  hipDeviceProp_t prop;
+  hipGetDeviceProperties(&prop, ctx->device);
+  if (prop.multiProcessorCount > 0) ctx->cus = prop.multiProcessorCount;
+  hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+  if (e == hipSuccess) e = hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest);
+  if (e != hipSuccess || ctx->sched != 3) return e;
+  return create_partition(ctx, ctx->side_req);
 }
 }  // namespace
 
@@ -581,6 +612,33 @@ int lfm_ctx_set_block(lfm_ctx* ctx, int nb) {
   if (!ctx) return LFM_E_ARG;
   if (nb != 0 && nb != 128) return set_err(ctx, LFM_E_ARG, "block size must be 128 (or 0)");
   ctx->nb = 128;
+  return LFM_OK;
+}
+
+int lfm_ctx_set_schedule(lfm_ctx* ctx, int schedule) {
+  if (!ctx) return LFM_E_ARG;
+  if (schedule == 0) schedule = env_int_api("LFM_SCHED", 3) == 1 ? 1 : 3;
+  if (schedule != 1 && schedule != 3)
+    return set_err(ctx, LFM_E_ARG, "schedule must be 1, 3 (or 0: the LFM_SCHED default)");
+  DeviceGuard g(ctx->device);
+  if (hipStreamSynchronize(ctx->stream) != hipSuccess)
+    return set_err(ctx, LFM_E_HIP, "lfm_ctx_set_schedule: stream synchronize failed");
+  if (schedule == 1) {
+    release_partition(ctx);
+  } else {
+    if (create_partition(ctx, ctx->side_req) != hipSuccess)
+      return set_err(ctx, LFM_E_HIP, "lfm_ctx_set_schedule: CU-masked stream creation failed");
+    if (ctx->side_cus <= 0)
+      return set_err(ctx, LFM_E_ARG, "schedule 3 needs the CU-partitioned stream pair, which "
+                                     "this device / LFM_SIDE_CUS did not provide");
+  }
+  ctx->sched = schedule;
+  return LFM_OK;
+}
+
+int lfm_ctx_get_schedule(const lfm_ctx* ctx, int* out) {
+  if (!ctx || !out) return LFM_E_ARG;
+  *out = ctx->sched == 3 && ctx->side_cus > 0 ? 3 : 1;
   return LFM_OK;
 }
 

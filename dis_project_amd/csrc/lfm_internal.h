@@ -58,6 +58,7 @@ struct lfm_ctx {
   hipStream_t side = nullptr;    // high-priority look-ahead stream: panel factor + solve
   hipStream_t m3 = nullptr;      // schedule 3: bulk stream (CUs outside the chain's)
   hipStream_t s3 = nullptr;      // schedule 3: factor-chain stream (LFM_SIDE_CUS CUs)
+  int side_req = 32;             // LFM_SIDE_CUS at creation: the reservation to (re)create
   int cus = 256;                 // compute units of the device
   std::vector<hipEvent_t> evs;   // cross-stream dependency events (timing disabled)
   std::string err;

@@ -11,7 +11,10 @@ every result to every rank. On MI355X the all-gather is RCCL over xGMI
 
 from __future__ import annotations
 
+import concurrent.futures as cf
+import itertools
 import math
+import threading
 from typing import Callable, Sequence
 
 import numpy as np
@@ -72,6 +75,9 @@ class TorchGather:
         out = [torch.empty_like(t) for _ in range(self.world)]
         self.dist.all_gather(out, t)
         return torch.cat(out).numpy()
+
+    def close(self):
+        pass
 
 
 class ResidentEvaluator:
@@ -173,15 +179,79 @@ class Farm:
                                                           [datasets[i] for i in idx]))
 
 
-def gpu_evaluator(ctx: _lib.Context, datasets, negative: bool = False):
+class ConcurrentEvaluator:
+    """Restart-farm throughput on one GPU (C3): ``workers`` contexts on factorisation schedule 1
+    (look-ahead on every CU, include/lfm.h ``lfm_ctx_set_schedule``), each with its own HIP
+    streams, workspace and resident copy of x / y, each driven by its own host thread (ctypes
+    releases the GIL inside the library calls), pulling the next hyperparameter set from a
+    shared counter. Several evaluations in flight fill the bubbles one evaluation's chain-bound
+    tail leaves on the chip (35-36 evals/s with 2-3 workers against 33.1 for one
+    schedule-3 evaluation at a time).
+
+    Worker 0 is the caller's context, switched to schedule 1 for the evaluator's lifetime and
+    restored by ``close()``: a schedule-3 context holds two CU-masked hardware queues even when
+    idle, and idle queues beside the workers oversubscribe the hardware scheduler (measured
+    -3 % with one, -10 % with two partitioned contexts idle). Schedule 3 itself is single tenant
+    -- two schedule-3 evaluations at once starve each other's co-resident factor chains -- so
+    the workers never use it. Results are per model and independent of which worker ran it
+    (schedule 1 is deterministic); not PD -> NaN, a device-side timeout raises in the caller."""
+
+    def __init__(self, ctx: _lib.Context, data, negative: bool = False, workers: int = 3):
+        self.ctx, self._restore = ctx, ctx.schedule
+        ctx.schedule = 1
+        self.own = [_lib.Context(ctx.device) for _ in range(max(1, int(workers)) - 1)]
+        for c in self.own:
+            c.schedule = 1
+        self.evs = [ResidentEvaluator(c, data, negative) for c in [ctx] + self.own]
+        self.pool = cf.ThreadPoolExecutor(max_workers=len(self.evs),
+                                          thread_name_prefix="lfm-worker")
+
+    def __call__(self, models) -> np.ndarray:
+        models = list(models)
+        if len(models) < 2:
+            return self.evs[0](models)
+        vals = np.empty(len(models))
+        counter, lock = itertools.count(), threading.Lock()
+
+        def work(ev):
+            while True:
+                with lock:
+                    i = next(counter)
+                if i >= len(models):
+                    return
+                vals[i] = ev([models[i]])[0]
+
+        futs = [self.pool.submit(work, ev) for ev in self.evs]
+        for f in futs:
+            f.result()  # re-raises a worker's LfmError here
+        return vals
+
+    def close(self):
+        if self.pool is None:
+            return
+        self.pool.shutdown(wait=True)
+        self.pool = None
+        for ev in self.evs:
+            ev.close()
+        for c in self.own:
+            c.close()
+        self.evs, self.own = [], []
+        self.ctx.schedule = self._restore
+
+
+def gpu_evaluator(ctx: _lib.Context, datasets, negative: bool = False, workers: int = 3):
     """The product evaluator of a farm round on this rank's GPU: problems sharing one large
-    dataset go through a ResidentEvaluator (x / y in HBM once); small ones through one
-    batched launch (``CustomConjMLL.batch``: one workgroup per problem, n <= 128)."""
+    dataset go through a ConcurrentEvaluator (x / y in HBM once per worker context, ``workers``
+    evaluations in flight; workers = 1: one ResidentEvaluator on ``ctx``); small ones through
+    one batched launch (``CustomConjMLL.batch``: one workgroup per problem, n <= 128)."""
     from .objectives import CustomConjMLL
 
     shared = len({id(d) for d in datasets}) == 1 and datasets[0].n > 128
     if shared:
-        res = ResidentEvaluator(ctx, datasets[0], negative)
+        if workers > 1:
+            res = ConcurrentEvaluator(ctx, datasets[0], negative, workers)
+        else:
+            res = ResidentEvaluator(ctx, datasets[0], negative)
         return (lambda models, data: res(models)), res.close
     mll = CustomConjMLL(negative=negative)
     return (lambda models, data: mll.batch(models, data)), (lambda: None)

@@ -101,6 +101,19 @@ const char* lfm_last_error(const lfm_ctx* ctx);
 int lfm_ctx_synchronize(lfm_ctx* ctx);
 /* Block size of the blocked Cholesky (64 or 128); 0 restores the default. */
 int lfm_ctx_set_block(lfm_ctx* ctx, int nb);
+/* Factorisation schedule of this context's MLL / gradient:
+ *   3  CU-partitioned stream pair: the factor chain on LFM_SIDE_CUS reserved CUs, the bulk on
+ *      the rest. Lowest latency of ONE evaluation; single tenant: two schedule-3 contexts
+ *      running at once on one GPU starve each other's co-resident chains (device-side wait
+ *      bound -> LFM_E_TIMEOUT).
+ *   1  look-ahead on every CU. Several schedule-1 contexts driven from separate host threads
+ *      share one GPU: the throughput mode of a restart farm (farm.ConcurrentEvaluator).
+ *   0  the process default (LFM_SCHED, else 3).
+ * Schedule 3 on a context without a CU partition -> LFM_E_ARG. Replaces no reference call:
+ * the reference's XLA executable has no schedule (src/objectives.py:43-46 is the whole MLL). */
+int lfm_ctx_set_schedule(lfm_ctx* ctx, int schedule);
+/* The schedule the next factorisation will run (1 or 3). */
+int lfm_ctx_get_schedule(const lfm_ctx* ctx, int* out);
 
 /* --------------------------------------------- ExactLFM surface (model.py) */
 /* mean_function (model.py:124-149): out[i] = (B/D)[i / (n / num_genes)] * int(x[i,2]). */

@@ -110,3 +110,73 @@ def test_farm_rccl_single_rank_liblfm(kind, kw):
         g.close()
         close()
     np.testing.assert_allclose(out, _oracle_eval(models, datasets), rtol=1e-9)
+
+
+@pytest.mark.gpu
+def test_schedule_setter():
+    """lfm_ctx_set_schedule / lfm_ctx_get_schedule: 1 and 3 round-trip, 0 restores the process
+    default, anything else is LFM_E_ARG with the context unchanged."""
+    from dis_project_amd import _lib
+
+    ctx = _lib.Context(0)
+    try:
+        ctx.schedule = 1
+        assert ctx.schedule == 1
+        ctx.schedule = 3
+        assert ctx.schedule == 3
+        for bad in (2, 4, -1):
+            with pytest.raises(_lib.LfmError):
+                ctx.schedule = bad
+            assert ctx.schedule == 3
+        ctx.schedule = 1
+        ctx.schedule = 0
+        assert ctx.schedule == (1 if os.environ.get("LFM_SCHED") == "1" else 3)
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_concurrent_evaluator_c3_full_size():
+    """C3 at full size (N = 16384) through the concurrent restart farm bench.py runs: three
+    schedule-1 workers in flight (the caller's context among them, switched to schedule 1 and
+    restored on close) against one schedule-3 evaluation and the C++ CPU restatement;
+    deterministic across calls and independent of which worker took which restart; a worker's
+    exception reaches the caller."""
+    from dis_project_amd import _lib
+
+    models, datasets = farm.workload("c3", 64, 256, 6)
+    s3 = _lib.Context(0)
+    try:
+        assert s3.schedule == (1 if os.environ.get("LFM_SCHED") == "1" else 3)
+        one = farm.ResidentEvaluator(s3, datasets[0])
+        single = one(models[:2])
+        one.close()
+    finally:
+        s3.close()
+    ctx = _lib.Context(0)
+    before = ctx.schedule
+    ev = farm.ConcurrentEvaluator(ctx, datasets[0], workers=3)
+    try:
+        assert ctx.schedule == 1
+        a = ev(models)
+        b = ev(models[::-1])[::-1]
+        np.testing.assert_array_equal(a, b)
+        assert np.all(np.isfinite(a))
+        np.testing.assert_allclose(a[:2], single, rtol=1e-10)
+
+        class Broken:
+            def hyp(self):
+                raise RuntimeError("bad hyperparameters")
+
+        with pytest.raises(RuntimeError, match="bad hyperparameters"):
+            ev([models[0], Broken(), models[1]])
+    finally:
+        ev.close()
+    assert ctx.schedule == before
+    ctx.close()
+    from oracle import lfm_cpu
+
+    m, d = models[0], datasets[0]
+    v, _ = lfm_cpu.mll(d.X, d.y, m.true_d, m.true_s, m.true_b, m.l, m.obs_stddev, m.jitter,
+                       negative=False, threads=16)
+    assert abs(a[0] - v) <= 1e-9 * abs(v)
