@@ -501,7 +501,7 @@ void release_partition(lfm_ctx* ctx) {
   ctx->side_cus = 0;
 }
 
-// Main + high-priority side stream (every CU), and for schedule 3 the CU-partitioned pair:
+// Main stream (every CU), and for schedule 3 the CU-partitioned pair:
 // LFM_SIDE_CUS (default 32) CUs for the factor chain, the rest for the bulk
 // (hipExtStreamCreateWithCUMask). The documented knobs read here:
 //   LFM_SCHED            3 (default) or 1: the look-ahead schedule of the MLL factorisation
@@ -519,14 +519,13 @@ hipError_t create_streams(lfm_ctx* ctx) {
   ctx->gram_fuse = env_int_api("LFM_GRAM_FUSE", LFM_GRAM_FUSE_DEFAULT) != 0;
   if (const char* sl = std::getenv("LFM_DEBUG_SPIN_LIMIT"))
     ctx->spin_limit = (unsigned)std::strtoul(sl, nullptr, 10);
-  int least = 0, greatest = 0;
-  hipDeviceGetStreamPriorityRange(&least, &greatest);
   ctx->side_req = env_int_api("LFM_SIDE_CUS", 32);
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, ctx->device);
   if (prop.multiProcessorCount > 0) ctx->cus = prop.multiProcessorCount;
+  // ctx->side (schedule 1's high-priority stream) is created on first use: schedule 3 never
+  // launches on it, and an idle hardware queue beside the running ones costs
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
-  if (e == hipSuccess) e = hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest);
   if (e != hipSuccess || ctx->sched != 3) return e;
   return create_partition(ctx, ctx->side_req);
 }
@@ -563,6 +562,11 @@ int lfm_ctx_create(int device, lfm_ctx** out) {
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->status, 64);
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->result, 64 * sizeof(double));
   if (e == hipSuccess) e = hipMalloc((void**)&ctx->psync, 64);
+  // Deliberately on the null stream, after the context's streams: the hardware queues of a
+  // process are opened in this order (stream, CU-masked pair, null stream), and the order
+  // matters for one C2 evaluation (scripts/ab_lib.py, 5 interleaved rounds each): without the
+  // null-stream queue 30.71 ms against 30.35; null queue first 30.29 and CU-masked pair
+  // first 30.31 against 29.97 on another box. DESIGN.md §9.
   if (e == hipSuccess) e = hipMemset(ctx->psync, 0, 64);
   if (e != hipSuccess) {
     lfm_ctx_destroy(ctx);
@@ -905,7 +909,8 @@ int lfm_mll_f64_dev(lfm_ctx* ctx, const double* d_x, const double* d_y, int64_t 
   if (e != hipSuccess) return hip_fail(ctx, e, "read back x for layout detection");
   if (n <= SMALL_MAX) {
     std::vector<double> yh((size_t)n);
-    e = hipMemcpy(yh.data(), d_y, n * 8, hipMemcpyDeviceToHost);
+    e = hipMemcpyAsync(yh.data(), d_y, n * 8, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) return hip_fail(ctx, e, "read back y");
     return lfm_mll_f64(ctx, xh.data(), yh.data(), n, hyp, negative, out);
   }
@@ -1137,12 +1142,15 @@ int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max)
       hipError_t e = hipMalloc((void**)&ctx->dbg_stamps, cnt * 8);
       if (e != hipSuccess) return hip_fail(ctx, e, "debug stamps");
     }
-    return hip_fail(ctx, hipMemset(ctx->dbg_stamps, 0, cnt * 8), "debug stamps");
+    hipError_t e = hipMemsetAsync(ctx->dbg_stamps, 0, cnt * 8, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return hip_fail(ctx, e, "debug stamps");
   }
   if (!ctx->dbg_stamps) return LFM_OK;
   finish(ctx);
-  hipError_t e = hipMemcpy(out, ctx->dbg_stamps, std::min<size_t>(cnt, (size_t)max) * 8,
-                           hipMemcpyDeviceToHost);
+  hipError_t e = hipMemcpyAsync(out, ctx->dbg_stamps, std::min<size_t>(cnt, (size_t)max) * 8,
+                                hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   hipFree(ctx->dbg_stamps);
   ctx->dbg_stamps = nullptr;
   return hip_fail(ctx, e, "debug stamps");

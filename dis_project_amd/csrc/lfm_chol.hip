@@ -2109,6 +2109,13 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     if (!r && fused) r = launch_gram_region(ctx, *gen, K10, std::min(K11, n), K10, K11, A, lda);
     if (r) return r;
   }
+  if (!s3 && !ctx->side) {
+    // schedule 1's high-priority side stream, created on first use (schedule 3 never needs it)
+    int least = 0, greatest = 0;
+    hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest) != hipSuccess)
+      return hip_fail(ctx, hipErrorOutOfMemory, "side stream creation");
+  }
   hipStream_t main = ctx->stream, side = ctx->side;
   hipEvent_t* ev = ctx->evs.data();  // [0]: inputs ready; E1_s = ev[1 + 2s]; E2_s = ev[2 + 2s]
   Launcher L{ctx, A, lda, bordered ? 2 * Mp : Mp, bordered ? Mp : 0};
