@@ -42,6 +42,14 @@ static constexpr int NB = 128;       // panel width (block column)
 static constexpr int IB = 16;        // inner block of the diagonal factor / panel solve
 static constexpr int ST = 128;       // SYRK output tile edge
 static constexpr int KB = 16;        // SYRK K-step staged through LDS
+#ifndef LFM_LDS_PAD
+#define LFM_LDS_PAD 2
+#endif
+// LDS row stride of a staged K stage: KS + LDP doubles. ds_read_b64 banks by (a / 4) mod 64
+// per 32-lane half: the MFMA fragment reads (16 rows x 4 k, and 4 rows x 4 k) are conflict-free
+// at a stride of 18 (and 66 for the chain's 64-deep stages); at 17 the 16-row reads were 2-way
+// conflicted. Measured: -0.57 ms per C2 evaluation (scripts/ab_lib.py, 5 rounds), same bits.
+static constexpr int LDP = LFM_LDS_PAD;
 static constexpr int STATUS_NONE = INT_MAX;
 constexpr int PANEL_TIMEOUT = STATUS_TIMEOUT;  // status: a bounded device-side wait ran out
 
@@ -753,7 +761,7 @@ __global__ __launch_bounds__(256) void trsm_kernel_v2(double* __restrict__ A, in
 // row stride ldi). pj: BT = false, row j0 of the j panel (k contiguous, row stride ldj);
 // BT = true, a K-major panel: element (k, j) at pj[k * ldj + j]. The SYRK callers hold -C in
 // acc (negated once at load / store instead of per fragment). sP: LDS staging, (TR + ST) rows
-// of KB + 1 doubles: rows [0, TR) panel i, rows [TR, TR + ST) panel j (j-major).
+// of KB + LDP doubles: rows [0, TR) panel i, rows [TR, TR + ST) panel j (j-major).
 // Every thread of the (256-thread) workgroup must call it.
 
 // KS: depth of one LDS stage (16 in the bulk kernels; 64 where one workgroup per CU has no
@@ -762,7 +770,7 @@ template <int TR, bool BT = false, bool COH = false, int KS = KB>
 __device__ __forceinline__ void gemm_accumulate(const double* __restrict__ pi, int64_t ldi,
                                                 const double* __restrict__ pj, int64_t ldj,
                                                 int kd, double (&acc)[TR / 8][4],
-                                                double (*__restrict__ sP)[KS + 1]) {
+                                                double (*__restrict__ sP)[KS + LDP]) {
   constexpr int IRN = TR / 8;
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));  // opaque: lane offsets are recomputed, not held live
@@ -887,7 +895,7 @@ __device__ __forceinline__ double ldc(const double* p) {
 template <bool CIO, int TR, int KS, bool LDCOH, bool CLOAD, bool GEN = false>
 __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, Panel P, int kd,
                                           int64_t i0, int64_t j0, bool diag, bool coh,
-                                          double (*__restrict__ sP)[KS + 1],
+                                          double (*__restrict__ sP)[KS + LDP],
                                           const GramGen* gen = nullptr) {
   constexpr int IRN = TR / 8;  // 4-row groups per wave (2 x 2 waves, TR/2 rows each)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -899,7 +907,7 @@ __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, P
   double acc[IRN][4];
   if constexpr (GEN) {
     constexpr int WIN = ST + TR - 1;
-    static_assert(4 * WIN + 3 * TR + 3 * ST <= (TR + ST) * (KS + 1), "gram windows in sP");
+    static_assert(4 * WIN + 3 * TR + 3 * ST <= (TR + ST) * (KS + LDP), "gram windows in sP");
     double* sWk = &sP[0][0];
     double* sXk = sWk + WIN;
     double* sWj = sXk + WIN;
@@ -995,7 +1003,7 @@ __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, P
 template <bool CIO, int TR, bool COH = false, int KS = KB, bool LDCOH = false>
 __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, int64_t s, Panel P,
                                           int kd, int T, int tj_lo, int tj_hi, int64_t b, int ti0,
-                                          double (*__restrict__ sP)[KS + 1], int coh_lim = 0,
+                                          double (*__restrict__ sP)[KS + LDP], int coh_lim = 0,
                                           int64_t pad_after = INT64_MAX,
                                           int64_t pad_end = INT64_MAX,
                                           int64_t zero_from = INT64_MAX,
@@ -1087,7 +1095,7 @@ template <bool CIO, int TR>
 __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
     double* __restrict__ A, int64_t lda, int64_t s, Panel P, int kd, int T, int tj_lo, int tj_hi,
     int prio, int xcd_remap, int ti0, int64_t skip) {
-  __shared__ double sP[TR + ST][KB + 1];
+  __shared__ double sP[TR + ST][KB + LDP];
   if (prio) __builtin_amdgcn_s_setprio(2);  // look-ahead bands: ahead of the bulk update
   int64_t b = blockIdx.x;
   if (xcd_remap && tj_hi - tj_lo > 8) {
@@ -1175,9 +1183,9 @@ __device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
 
 // (256, 4): 128 VGPRs, 4 waves / SIMD (the zero-C tile body would otherwise take 134)
 __global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) {
-  __shared__ double sPbuf[(64 + ST) * (LFM_STEP_KS + 1)];
-  double (*sP)[KB + 1] = reinterpret_cast<double (*)[KB + 1]>(sPbuf);
-  double (*sPu)[LFM_STEP_KS + 1] = reinterpret_cast<double (*)[LFM_STEP_KS + 1]>(sPbuf);
+  __shared__ double sPbuf[(64 + ST) * (LFM_STEP_KS + LDP)];
+  double (*sP)[KB + LDP] = reinterpret_cast<double (*)[KB + LDP]>(sPbuf);
+  double (*sPu)[LFM_STEP_KS + LDP] = reinterpret_cast<double (*)[LFM_STEP_KS + LDP]>(sPbuf);
   const int64_t b = blockIdx.x;
   // roles in blockIdx order: ahead (1), rest (2), tall (3), each padded to a multiple of 8
   const int cnt[3] = {g.na, g.nr, g.nt};
@@ -1317,7 +1325,7 @@ __global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) {
 // workgroups never hold the slots it needs; a bounded wait still ends every workgroup (status
 // PANEL_TIMEOUT) rather than hang.
 constexpr size_t PANEL_LDS = (size_t)MB_DOUBLES * sizeof(double);
-static_assert(MB_DOUBLES >= 64 * (NB + 1) && MB_DOUBLES >= (64 + ST) * (KB + 1), "LDS union");
+static_assert(MB_DOUBLES >= 64 * (NB + 1) && MB_DOUBLES >= (64 + ST) * (KB + LDP), "LDS union");
 
 __device__ __forceinline__ bool wait_counter(unsigned* p, unsigned target, unsigned limit) {
   __shared__ int ok;
@@ -1350,7 +1358,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
     for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = -Cb[ir * ld4 + jr * 16];
   if (pkd > 0)
     gemm_accumulate<64>(A + i0 * lda + pkb, lda, A + kb * lda + pkb, lda, pkd, acc,
-                        reinterpret_cast<double (*)[KB + 1]>(smem));
+                        reinterpret_cast<double (*)[KB + LDP]>(smem));
   if (b < 2) {
     // diagonal slab back to the matrix (the part above the diagonal is scratch)
 #pragma unroll
@@ -1483,7 +1491,7 @@ __device__ __forceinline__ bool grid_sync_light(unsigned* bar, unsigned target, 
 
 
 constexpr int CKS = 64;  // chain kernel GEMM stage depth
-static_assert(2 * MB_DOUBLES >= (64 + ST) * (CKS + 1), "chain LDS union");
+static_assert(2 * MB_DOUBLES >= (64 + ST) * (CKS + LDP), "chain LDS union");
 
 // Small-tile GEMM for the chain's latency-bound phases: one 32 x 32 output tile per
 // workgroup, so a 128-row block spreads over 16 workgroups instead of two 64 x 128 units
@@ -1969,14 +1977,22 @@ __global__ void fill_hash_kernel(double* a, int64_t cnt) {
 // slabs) over a T x T grid of 128-tiles with update depth kd. cio bit 0: C tile I/O (else the
 // MFMAs alone), bit 3: random operands (else zeros), bit 4: on schedule 3's CU-masked bulk
 // stream instead of every CU, bit 6: the step kernel's rest role (bit 5: without C loads).
+// With bit 6, the rest of a w = 1 step launch's structure (to bisect what a real step costs
+// beyond its rest triangle): bit 7 the ahead band (tile column 0 below the diagonal tile, the
+// rest triangle then over columns >= 1, coherent stores, a_done bumps), bit 8 the tall units
+// (X = A21 Bd at depth 128 for the rows below tile 0, no waits), bit 9 the panel read from a
+// separate 128-wide buffer (the real steps' X_s) instead of A's own columns.
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const int64_t n = (int64_t)T * ST + 512;
-  int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8);
+  const size_t xb = (cio & (512 | 256)) ? (size_t)n * 128 * 8 : 0;  // X_s / X_{s+1} slabs
+  int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8 + 2 * xb + 4096);
   if (r) return r;
   if (cio & 8)
-    hipLaunchKernelGGL(fill_hash_kernel, dim3(4096), dim3(256), 0, ctx->stream, ctx->A, n * n);
+    hipLaunchKernelGGL(fill_hash_kernel, dim3(4096), dim3(256), 0, ctx->stream, ctx->A,
+                       n * n + 2 * (int64_t)(xb / 8));
   else
-    hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8, ctx->stream);
+    hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8 + 2 * xb, ctx->stream);
+  hipMemsetAsync(ctx->A + (size_t)n * n + 2 * (xb / 8), 0, 4096, ctx->stream);
   const unsigned units = (unsigned)((int64_t)T * (T + 1));
   hipStream_t st = (cio & 16) && ctx->m3 ? ctx->m3 : ctx->stream;
   if (st != ctx->stream) {
@@ -2004,7 +2020,31 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
       g.spin = ctx->spin_limit;
       g.zero_from = (cio & 32) ? 0 : INT64_MAX;
       g.copy_from = INT64_MAX;
-      hipLaunchKernelGGL(step_kernel, dim3((units + 7) / 8 * 8), dim3(256), 0, st, g);
+      double* xs = ctx->A + (size_t)n * n;  // [X_s | X_{s+1} | counters]
+      unsigned* ctr = reinterpret_cast<unsigned*>(xs + 2 * (xb / 8));
+      if (cio & 512) g.px = Panel{xs, 128, 512};
+      unsigned grid = (units + 7) / 8 * 8;
+      if (cio & 128) {
+        g.wn = 1;
+        g.na = 2 * (T - 1);
+        g.nr = (T - 1) * T;
+        g.a_done = ctr;
+        grid = (g.na + 7) / 8 * 8 + (g.nr + 7) / 8 * 8;
+      }
+      if (cio & 256) {
+        g.tw = 1;
+        g.tr0 = 512 + ST;
+        g.tk0 = 0;
+        g.nt = 2 * (T - 1);
+        g.Bd = ctx->A;
+        g.X = xs + xb / 8;
+        g.zvec = xs;
+        g.a_done = nullptr;
+        grid = (g.na + 7) / 8 * 8 + (g.nr + 7) / 8 * 8 + (g.nt + 7) / 8 * 8;
+      }
+      // unit-duration stamps in step slot 0 while lfm_debug_stamps is on (scripts/unit_time.py)
+      g.stamps = ctx->dbg_stamps ? ctx->dbg_stamps + 256 * 16 : nullptr;
+      hipLaunchKernelGGL(step_kernel, dim3(grid), dim3(256), 0, st, g);
     } else if (cio & 1)
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(units), dim3(256), 0, st, ctx->A, n,
                          (int64_t)512, pan, kd, T, 0, T, 0, 1, 0, (int64_t)0);

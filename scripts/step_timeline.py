@@ -4,10 +4,11 @@ launch s (step s's trailing update + the tall solve of super-panel s + 1) the la
 the update units' span and rate, how long the tall units' last wait ran past the update
 (the chain-bound exposure), and the chain (s + 1)'s own span.
 
-    python scripts/step_timeline.py [--json out.json] [--grad]
+    python scripts/step_timeline.py [--json out.json] [--grad] [--genes G]
 
 --grad times value_and_grad's bordered factorisation (2Mp x 2Mp, every step updating the
-sliding Mp-row window) instead of the MLL's.
+sliding Mp-row window) instead of the MLL's. --genes G: the G x 256 grid (N = 256 G) instead
+of C2's 64 genes (its first steps then have the shape of C2's tail steps).
 """
 import ctypes
 import json
@@ -44,7 +45,8 @@ def plan(n, bordered=False):
 
 def main():
     grad = "--grad" in sys.argv
-    work = configs.c2()
+    G = int(sys.argv[sys.argv.index("--genes") + 1]) if "--genes" in sys.argv else 64
+    work = configs.c2(G)
     n = work.n
     x = np.ascontiguousarray(work.data.X)
     y = np.ascontiguousarray(work.data.y.reshape(-1))
@@ -91,7 +93,8 @@ def main():
     rows = []
     tot_exposed = 0.0
     print(f"N={n}: {S} steps, plain {plain_ms:.2f} ms/eval, stamped {stamped_ms:.2f} ms")
-    print(" s  w  m_tr   launch[us]  update[us] TF/s  exposed[us] chain(s+1)[us] clock[MHz]")
+    print(" s  w  m_tr   launch[us]  update[us] TF/s  exposed[us] chain(s+1)[us] clock[MHz] "
+          "rest unit[us]")
     for s in range(S - 1):
         k, w = steps[s]
         K1 = (k + w) * NB
@@ -108,12 +111,16 @@ def main():
         chain = (c[15] - c[0]) * 0.01 if c[0] and c[15] else float("nan")
         tf = alg / (upd * 1e-6) / 1e12 if upd > 0 else 0.0
         mhz = float(sp[s][4]) / float(sp[s][5]) * 100.0 if sp[s][5] else 0.0
+        T = (m + NB - 1) // NB if not grad else Mp // NB
+        nr = (T - wn) * (T - wn + 1)  # rest units (lfm_chol.hip update_args)
+        unit_us = float(sp[s][5]) * 0.01 / nr if nr > 0 else 0.0
         rows.append(dict(s=s, w=w, m=m, start_us=us(st0), launch_us=launch, update_us=upd,
                          update_tflops=tf, exposed_us=exposed, chain_next_us=chain,
                          chain_next_start_us=us(c[0]) if c[0] else None,
-                         chain_next_done_us=us(c[15]) if c[15] else None, update_clock_mhz=mhz))
+                         chain_next_done_us=us(c[15]) if c[15] else None, update_clock_mhz=mhz,
+                         rest_unit_us=unit_us))
         print(f"{s:2d} {w:2d} {m:6d} {launch:10.1f} {upd:10.1f} {tf:5.1f} {exposed:10.1f} {chain:10.1f} "
-              f"{mhz:7.0f}")
+              f"{mhz:7.0f} {unit_us:7.2f}")
     end_all = max(int(v) for v in sp[: S - 1, 3])
     print(f"span first unit -> last unit: {(end_all - int(first[0])) * 0.01:.1f} us; "
           f"chain-bound exposure (tall units waiting past the update) {tot_exposed:.1f} us")
