@@ -181,7 +181,9 @@ __device__ __forceinline__ void st1(double* p, double v) {
 // Two doubles at base + off (bytes, 16-B aligned) in one 16-B write-through (sc1) vector store:
 // the wide form of st1<true> (an 8-B sc1 store is one fabric write, ≈2.7x the 16-B time per
 // byte, MI355X_MICROARCH.md). base must be wave-uniform (a kernel argument or derived from one):
-// it becomes the buffer resource.
+// it becomes the buffer resource. Range: off + 16 <= 2^31 - 1 (num_records); a store past it is
+// dropped without a fault, so the helper serves the per-block workspaces only (the inverse,
+// X_D, the chain workspace: at most 4 W^2 doubles = 13 MB at W = 640), never the matrix.
 typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st2_wt(double* base, unsigned off, double a, double b) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(base, 0, 0x7fffffff, 0x00020000);
@@ -862,6 +864,10 @@ struct Panel {
 #ifndef LFM_WBULK
 #define LFM_WBULK 5
 #endif
+// the same for the gradient's bordered factorisation (its window keeps every step full width)
+#ifndef LFM_WBORD
+#define LFM_WBORD 4
+#endif
 // rest-triangle enumeration: tile rows in groups of Q, Q x Q supertiles within a group (1: row
 // by row)
 #ifndef LFM_SUPERTILE
@@ -1503,7 +1509,7 @@ static_assert(2 * MB_DOUBLES >= (64 + ST) * (CKS + LDP), "chain LDS union");
 // prefetched into registers while the current one is multiplied); the four waves each take
 // 32 k of a stage and their partial tiles are summed through LDS at the end.
 // LDS: smem[0, 2 * 32 * G32K) (operands) and then [0, 4 * 32 * 33) (partials, aliased).
-constexpr int G32K = 129;  // LDS row stride of a 128-deep operand row
+constexpr int G32K = 129;  // LDS row stride of a 128-deep operand row (130: same time, A/B)
 static_assert(2 * MB_DOUBLES >= 2 * 32 * G32K + 4 * 1024 && 2 * MB_DOUBLES >= 4 * 32 * 33,
               "gemm32 LDS (+ the in-chain solve's parked output tiles)");
 template <bool BT, bool COH = false, bool PAIR = false>
@@ -2121,7 +2127,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   // bulk width: 5 block columns (W = 640) for the MLL — its C traffic per flop is 4/5 of W = 512
   // and its chain still hides behind the update (A/B: -0.23..-0.26 ms per evaluation; W = 768
   // and 896 were slower, 1024 much slower); the bordered gradient keeps 4 (5 measured equal)
-  const int wbulk = s3 && !bordered ? LFM_WBULK : 4;
+  const int wbulk = s3 ? (bordered ? LFM_WBORD : LFM_WBULK) : 4;
   const int64_t w2min = env_int("LFM_W2_MIN", s3 ? 5120 : 4096);
   std::vector<std::pair<int64_t, int>> steps;
   for (int64_t k = 0; k < nblk;) {
