@@ -1987,7 +1987,8 @@ __global__ void fill_hash_kernel(double* a, int64_t cnt) {
 // beyond its rest triangle): bit 7 the ahead band (tile column 0 below the diagonal tile, the
 // rest triangle then over columns >= 1, coherent stores, a_done bumps), bit 8 the tall units
 // (X = A21 Bd at depth 128 for the rows below tile 0, no waits), bit 9 the panel read from a
-// separate 128-wide buffer (the real steps' X_s) instead of A's own columns.
+// separate 128-wide buffer (the real steps' X_s) instead of A's own columns. Bit 11 (instead
+// of bit 6): syrk_kernel's 128 x 128 units over the same triangle.
 int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
   const int64_t n = (int64_t)T * ST + 512;
   const size_t xb = (cio & (512 | 256)) ? (size_t)n * 128 * 8 : 0;  // X_s / X_{s+1} slabs
@@ -2051,7 +2052,11 @@ int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
       // unit-duration stamps in step slot 0 while lfm_debug_stamps is on (scripts/unit_time.py)
       g.stamps = ctx->dbg_stamps ? ctx->dbg_stamps + 256 * 16 : nullptr;
       hipLaunchKernelGGL(step_kernel, dim3(grid), dim3(256), 0, st, g);
-    } else if (cio & 1)
+    } else if (cio & 2048)
+      // 128 x 128 units (2 workgroups / CU, 64 x 64 per wave), the same triangle
+      hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(units / 2), dim3(256), 0, st, ctx->A, n,
+                         (int64_t)512, pan, kd, T, 0, T, 0, 1, 0, (int64_t)0);
+    else if (cio & 1)
       hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(units), dim3(256), 0, st, ctx->A, n,
                          (int64_t)512, pan, kd, T, 0, T, 0, 1, 0, (int64_t)0);
     else
