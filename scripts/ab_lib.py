@@ -5,6 +5,9 @@ every variant alike. Usage (libraries built in-tree, e.g. make OUT=../liblfm_x.s
 
     python scripts/ab_lib.py dis_project_amd/liblfm.so dis_project_amd/liblfm_ab0.so
 
+A variant may carry context-creation environment settings after '@', comma-separated:
+    python scripts/ab_lib.py dis_project_amd/liblfm.so dis_project_amd/liblfm.so@LFM_SIDE_CUS=16
+
 Prints per library: median / min ms per evaluation over the rounds and the MLL."""
 import json
 import os
@@ -15,7 +18,11 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(lib):
+def child(variant):
+    lib, _, env = variant.partition("@")
+    for kv in filter(None, env.split(",")):
+        k, v = kv.split("=", 1)
+        os.environ[k] = v
     os.environ["LFM_LIBRARY"] = lib
     sys.path.insert(0, ROOT)
     import numpy as np
@@ -33,7 +40,7 @@ def child(lib):
         v = ev([work.model])
         ctx.check(ctx.lib.lfm_ctx_synchronize(ctx.handle))
         ts.append((time.perf_counter() - t0) * 1e3)
-    print(json.dumps({"lib": lib, "ms": ts, "mll": float(v[0])}))
+    print(json.dumps({"lib": variant, "ms": ts, "mll": float(v[0])}))
     ev.close()
 
 
