@@ -70,6 +70,9 @@ def parse(argv=None):
     p.add_argument("--gather", choices=["rccl", "gloo"], default="rccl",
                    help="rehearsal only: gloo all-gather and ranks sharing the visible GPUs "
                         "(W ranks on fewer cards); the measured configuration is rccl")
+    p.add_argument("--share-gpus", action="store_true",
+                   help="rehearsal only: ranks share the visible GPUs (rank -> local %% count) "
+                        "with the RCCL all-gather")
     return p.parse_args(argv)
 
 
@@ -121,7 +124,7 @@ def main(argv=None):
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
     # one GPU per rank; the gloo rehearsal may put several ranks on one card
-    dev = local % max(1, _lib.device_count()) if a.gather == "gloo" else local
+    dev = local % max(1, _lib.device_count()) if a.gather == "gloo" or a.share_gpus else local
     ctx = _lib.get_context(dev)
     lib, h = ctx.lib, ctx.handle
 

@@ -1208,6 +1208,13 @@ __global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) {
   const int role = seg + 1;
   unsigned long long* const st = g.stamps;
   if (st) stamp_max(st, true);
+  // diagnostics: summed unit durations per role (rest [5], tall [6], ahead [7]; 100 MHz)
+  const unsigned long long t_unit = st ? __builtin_amdgcn_s_memrealtime() : 0;
+  auto add_dur = [&](int slot) {
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(st + slot, __builtin_amdgcn_s_memrealtime() - t_unit,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
   if (role == 1) {
     // device-coherent stores + a counter bump once they have completed: the tall units read
     // these rows with device-coherent loads (no L2 writeback / invalidate on either side)
@@ -1225,6 +1232,7 @@ __global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) {
     if (st) {
       stamp_max(st + 1);
       stamp_max(st + 3);
+      add_dur(7);
     }
     return;
   }
@@ -1292,6 +1300,7 @@ __global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) {
     if (st) {
       __syncthreads();
       stamp_max(st + 3);
+      add_dur(6);
     }
     return;
   }
@@ -1315,6 +1324,7 @@ __global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) {
   if (st) {
     __syncthreads();
     stamp_max(st + 3);
+    add_dur(6);
   }
 }
 

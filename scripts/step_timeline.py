@@ -21,6 +21,7 @@ import numpy as np  # noqa: E402
 from dis_project_amd import _lib, configs  # noqa: E402
 
 NB = 128
+SLOTS = 4 * 224  # resident step-kernel workgroups: 4 per main-stream CU (32 side CUs)
 
 
 def plan(n, bordered=False):
@@ -114,13 +115,27 @@ def main():
         T = (m + NB - 1) // NB if not grad else Mp // NB
         nr = (T - wn) * (T - wn + 1)  # rest units (lfm_chol.hip update_args)
         unit_us = float(sp[s][5]) * 0.01 / nr if nr > 0 else 0.0
+        na = 2 * wn * (T - wn)  # ahead units
+        # tall units of this launch (X_{s+1}): rows below the next diagonal block, identity
+        # padding rows (past n) skipped
+        K1n = K1 + wn * NB
+        rows_t = (Mp if not grad else 2 * Mp) - K1n
+        nt_all = rows_t // 64 * wn
+        nt = nt_all if grad else ((n + 1 - K1n + 63) // 64) * wn
+        tall_us = float(sp[s][6]) * 0.01 / nt if nt > 0 else 0.0
+        ahead_us = float(sp[s][7]) * 0.01 / na if na > 0 else 0.0
+        # slot occupancy over the launch: summed unit time / (slots x launch span)
+        busy = (float(sp[s][5]) + float(sp[s][6]) + float(sp[s][7])) * 0.01
+        occ = busy / (SLOTS * launch) if launch > 0 else 0.0
         rows.append(dict(s=s, w=w, m=m, start_us=us(st0), launch_us=launch, update_us=upd,
                          update_tflops=tf, exposed_us=exposed, chain_next_us=chain,
                          chain_next_start_us=us(c[0]) if c[0] else None,
                          chain_next_done_us=us(c[15]) if c[15] else None, update_clock_mhz=mhz,
-                         rest_unit_us=unit_us))
+                         rest_unit_us=unit_us, tall_unit_us=tall_us, ahead_unit_us=ahead_us,
+                         tall_units=nt, slot_occupancy=occ))
         print(f"{s:2d} {w:2d} {m:6d} {launch:10.1f} {upd:10.1f} {tf:5.1f} {exposed:10.1f} {chain:10.1f} "
-              f"{mhz:7.0f} {unit_us:7.2f}")
+              f"{mhz:7.0f} {unit_us:7.2f} tall {tall_us:6.2f} x{nt} ahead {ahead_us:6.2f} "
+              f"occ {occ:.3f}")
     end_all = max(int(v) for v in sp[: S - 1, 3])
     print(f"span first unit -> last unit: {(end_all - int(first[0])) * 0.01:.1f} us; "
           f"chain-bound exposure (tall units waiting past the update) {tot_exposed:.1f} us")
