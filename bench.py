@@ -183,7 +183,7 @@ def main(argv=None):
     t0 = time.perf_counter()
     for s in range(a.steps):
         if s < prof_steps:
-            ctx.profile(True, classes=["syrk", "gram_grid", "potrf"])
+            ctx.profile(True, classes=["syrk", "gram_grid", "potrf", "syrk_side"])
         timed.append(step())
         if s + 1 == prof_steps:
             ctx.profile(False)
@@ -293,6 +293,21 @@ def main(argv=None):
                 # the side stream's factor chain (its event span includes its device-side
                 # input waits, so only its algorithmic share is reported)
                 line["roofline"]["chain_flops_per_eval"] = chain["flops"] / prof_steps
+            # the whole evaluation: the factorisation's N^3/3 over the evaluation's wall time
+            # (the step kernel above runs on the 224 main CUs, the chain and the helper on 32)
+            line["roofline"]["evaluation_tflops"] = chol_flops / (ms_per_step * 1e-3) / 1e12
+            line["roofline"]["evaluation_frac"] = \
+                line["roofline"]["evaluation_tflops"] / FP64_MFMA_PEAK_TFLOPS
+            side = stats.get("syrk_side", {})
+            if side.get("launches"):
+                # the tail of long steps' trailing updates run on the 32 side CUs between
+                # chains (same kernel; its flops are not in flops_per_launch above)
+                line["roofline"]["side_helper"] = {
+                    "launches_per_eval": side["launches"] / prof_steps,
+                    "flops_per_eval": side["flops"] / prof_steps,
+                    "avg_launch_ms": side["total_ms"] / side["launches"],
+                    "achieved": side["flops"] / (side["total_ms"] * 1e-3) / 1e12,
+                }
         if gram.get("launches"):
             gbs = gram["bytes"] / (gram["total_ms"] * 1e-3) / 1e9
             # fused (the schedule-3 default on this layout): the gram kernel writes only the

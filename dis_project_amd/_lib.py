@@ -152,7 +152,7 @@ SIGNATURES = PRODUCT_SIGNATURES + DIAG_SIGNATURES
 
 # kernel classes in lfm_profile_read order (lfm_internal.h KClass)
 KCLASSES = ["tables", "gram_grid", "gram_direct", "augment", "potrf", "trsm", "syrk",
-            "finalize", "small_mll", "mean", "grad", "panel"]
+            "finalize", "small_mll", "mean", "grad", "panel", "syrk_side"]
 
 _lib = None
 _lib_lock = threading.Lock()

@@ -26,7 +26,8 @@ namespace lfm {
 const char* const kClassName[K_NCLASS] = {"tables",   "gram_grid", "gram_direct",
                                           "augment",  "potrf",     "trsm",
                                           "syrk",     "finalize",  "small_mll",
-                                          "mean",     "grad",      "panel"};
+                                          "mean",     "grad",      "panel",
+                                          "syrk_side"};
 
 int set_err(lfm_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;

@@ -1169,6 +1169,8 @@ struct StepArgs {
   int64_t zero_from;
   int64_t copy_from;
   GramGen gen;       // gen.tab != NULL: the first step's update units generate Sigma (fused gram)
+  int64_t rest_off;  // rest units of this launch are [rest_off, rest_off + nr) of the step's
+                     // enumeration (the side-CU helper launch takes the tail of it)
 };
 
 // Diagnostics: atomic max of the 100 MHz clock (or of its bitwise NOT: the earliest start)
@@ -1243,7 +1245,7 @@ __global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) {
       r0 = __builtin_amdgcn_s_memrealtime();
     }
     const bool lead = syrk_unit<true, 64, false, LFM_STEP_KS>(g.A, g.lda, g.s0, g.px, g.kd, g.T,
-                                                              g.wn, g.T, u, 0, sPu,
+                                                              g.wn, g.T, u + g.rest_off, 0, sPu,
                                                               g.xready ? g.wn + g.lead : 0, g.n,
                                                               g.pad_end, g.zero_from,
                                                               g.gen.tab ? &g.gen : nullptr);
@@ -1952,6 +1954,43 @@ struct Launcher {
   }
 };
 
+// Host mirror of syrk_unit's triangle enumeration (TR = 64, tile columns [tj_lo, T)): unit b ->
+// (64-row slab index ti, 128-column tile index tj) relative to the trailing matrix. Used only
+// to price the side-CU helper's share of a step's algorithmic flops.
+void rest_unit_tile(int64_t b, int T, int tj_lo, int* ti_out, int* tj_out) {
+  constexpr int SUB = 2, Q = LFM_SUPERTILE;
+  const int sub = (int)(b % SUB);
+  b /= SUB;
+  int a = (int)((std::sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
+  while ((int64_t)(a + 1) * (a + 2) / 2 <= b) ++a;
+  while ((int64_t)a * (a + 1) / 2 > b) --a;
+  int tj, ti;
+  if (Q > 1) {
+    const int R = a / Q, r0 = R * Q, qr = std::min(Q, T - tj_lo - r0);
+    const int64_t off = b - (int64_t)r0 * (r0 + 1) / 2;
+    const int64_t full = (int64_t)R * qr * Q;
+    int lr, lc;
+    if (off < full) {
+      const int C = (int)(off / (qr * Q)), t = (int)(off % (qr * Q));
+      lr = t / Q;
+      lc = C * Q + t % Q;
+    } else {
+      const int d = (int)(off - full);
+      lr = (int)((std::sqrt(8.0 * (double)d + 1.0) - 1.0) * 0.5);
+      while ((lr + 1) * (lr + 2) / 2 <= d) ++lr;
+      while (lr * (lr + 1) / 2 > d) --lr;
+      lc = r0 + d - lr * (lr + 1) / 2;
+    }
+    tj = lc + tj_lo;
+    ti = SUB * (r0 + lr + tj_lo) + sub;
+  } else {
+    tj = (int)(b - (int64_t)a * (a + 1) / 2) + tj_lo;
+    ti = SUB * (a + tj_lo) + sub;
+  }
+  *ti_out = ti;
+  *tj_out = tj;
+}
+
 int env_int(const char* name, int def) {
   const char* v = std::getenv(name);
   return v ? std::atoi(v) : def;
@@ -2278,7 +2317,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       const int64_t K1 = (steps[s].first + steps[s].second) * NB;
       return (int)((rows_end(K1) - K1) / 64 * steps[s].second);
     };
-    auto launch_step = [&](StepArgs& g) {
+    auto launch_step = [&](StepArgs& g, double alg_side = 0.0) {
       g.n = n;  // padding rows past n are skipped
       g.pad_end = pad_end;
       if (!g.zero_from) g.zero_from = INT64_MAX;
@@ -2306,6 +2345,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         const int64_t rows = bordered ? rows_end(g.tk0) - g.tr0 : n + 1 - g.tr0;
         alg += (double)std::max<int64_t>(0, rows) * W2 * W2;
       }
+      alg -= alg_side;  // the helper's share (its own kernel class)
       hipEvent_t pe;
       prof_begin(ctx, K_SYRK, &pe, main);
       hipLaunchKernelGGL(step_kernel, dim3((unsigned)grid), dim3(256), 0, main, g);
@@ -2346,6 +2386,24 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.na = 2 * wn * (T - wn);
       g.nr = (T - wn) * (T - wn + 1);  // 2 slabs per tile of the (T - wn)-tile triangle
       g.status = ctx->status;
+    };
+    // units of step s's rest triangle for the side-CU helper: the main launch of U unit-
+    // equivalents takes D0 = U t / (S_m o) alone; giving x units to the helper's S_h slots,
+    // which start after chain(s + 1) (Tc), balances at x t (1 / S_h + 1 / S_m) = o (D0 - Tc)
+    const int helper_on = mode == CHOL_MLL || bordered ? (int)env_int("LFM_HELPER", 1) : 0;
+    const double helper_tc = env_int("LFM_HELPER_TC", 700);    // chain(s + 1) + margin, us
+    const double helper_min = env_int("LFM_HELPER_MIN", 1200);  // smallest D0 helped, us
+    auto helper_units = [&](const StepArgs& g, int wnext) -> int64_t {
+      if (!helper_on) return 0;
+      const double t = 154.0 * g.kd / 640.0 + 4.0;  // one depth-kd unit, us (step timeline)
+      const double o = 0.9;
+      const double sm = 4.0 * (ctx->cus - ctx->side_cus), sh = 4.0 * ctx->side_cus;
+      const double tall_eq = (double)g.nt * (wnext + 1) / 2.0 * NB / g.kd;
+      const double units = g.na + g.nr + tall_eq;
+      const double d0 = units * t / (sm * o);
+      if (d0 < helper_min) return 0;
+      const double x = o * (d0 - helper_tc) / (t * (1.0 / sh + 1.0 / sm));
+      return std::max<int64_t>(0, std::min<int64_t>((int64_t)x, g.nr / 2));
     };
     // side: chain(0) after the gram; every later chain(s) follows chain(s - 1) in stream order
     // and waits on the device for its inputs (xready[s]) from the main launch in flight
@@ -2391,6 +2449,9 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         tall_args(g, 0);
         launch_step(g);
       }
+      hipEvent_t* evL = ev + 1;  // [S] launch s done (main)
+      hipEvent_t* evH = ev + 2;  // stride 2: helper(s) done (side)
+      bool helped = false;       // the previous step had a helper launch
       for (int s = 0; s + 1 < S; ++s) {
         chain(s + 1);
         StepArgs g{};
@@ -2403,7 +2464,50 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
           g.xready = xready + s + 2;
           g.lead = steps[s + 2].second;
         }
-        launch_step(g);
+        // Side-CU helper (LFM_HELPER): while the factor chain has slack (long launches), the
+        // side stream runs the tail of this step's rest units after chain(s + 1), sized so it
+        // ends with the main launch; launch s + 1 waits for it, chain(s + 2) follows it.
+        const int64_t hu = s >= 1 && s + 2 < S ? helper_units(g, steps[s + 1].second) : 0;
+        if (helped) hipStreamWaitEvent(main, evH[2 * (s - 1)], 0);
+        if (hu > 0) {
+          g.nr -= (int)hu;
+          // the helper's algorithmic flops (profiling only): 2 kd per updated lower element
+          // of its tiles, rows past n (identity padding) excluded
+          double alg_h = 0.0;
+          if (ctx->prof) {
+            for (int64_t b = g.nr; b < g.nr + hu; ++b) {
+              int ti, tj;
+              rest_unit_tile(b, g.T, g.wn, &ti, &tj);
+              const int64_t i0 = g.s0 + (int64_t)ti * 64, j0 = g.s0 + (int64_t)tj * ST;
+              // bordered: the whole window is algorithmic; MLL: rows past n are padding
+              for (int64_t r = i0; r < i0 + 64 && (bordered || r <= n); ++r)
+                alg_h += (double)std::max<int64_t>(0, std::min<int64_t>(ST, r - j0 + 1));
+            }
+            alg_h *= 2.0 * g.kd;
+          }
+          launch_step(g, alg_h);
+          hipEventRecord(evL[2 * s], main);
+          StepArgs h = g;
+          h.na = 0;
+          h.nt = 0;
+          h.rest_off = g.nr;
+          h.nr = (int)hu;
+          h.stamps = nullptr;
+          h.xready = nullptr;  // tail units: never the lead tiles
+          // X_s and step s's C input: launch s - 1 complete
+          hipStreamWaitEvent(side, evL[2 * (s - 1)], 0);
+          hipEvent_t pe;
+          prof_begin(ctx, K_SIDE_SYRK, &pe, side);
+          hipLaunchKernelGGL(step_kernel, dim3((unsigned)((hu + 7) / 8 * 8)), dim3(256), 0, side,
+                             h);
+          prof_end(ctx, K_SIDE_SYRK, pe, alg_h, 0, side, (double)hu * 64 * ST * 2.0 * g.kd);
+          hipEventRecord(evH[2 * s], side);
+          helped = true;
+        } else {
+          launch_step(g);
+          hipEventRecord(evL[2 * s], main);
+          helped = false;
+        }
       }
       if (bordered) {
         StepArgs g{};  // the last super-panel's update of the border block (-S_aug^{-1})

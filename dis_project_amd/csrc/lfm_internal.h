@@ -27,6 +27,7 @@ enum KClass {
   K_MEAN,         // mean_function
   K_GRAD,         // MLL gradient: W-weighted kernel-derivative reduction
   K_PANEL,        // fused pending update + diagonal factor + panel solve (one block column)
+  K_SIDE_SYRK,    // schedule 3: the tail of a step's trailing update on the side CUs (helper)
   K_NCLASS
 };
 

@@ -12,7 +12,12 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(lib):
+def child(variant):
+    # a variant may carry environment settings after '@' (as scripts/ab_lib.py)
+    lib, _, env = variant.partition("@")
+    for kv in filter(None, env.split(",")):
+        k, v = kv.split("=", 1)
+        os.environ[k] = v
     os.environ["LFM_LIBRARY"] = lib
     sys.path.insert(0, ROOT)
     from dis_project_amd import CustomConjMLL, configs
@@ -26,7 +31,7 @@ def child(lib):
         t0 = time.perf_counter()
         v, g = obj.value_and_grad(work.model, work.data)
         ts.append((time.perf_counter() - t0) * 1e3)
-    print(json.dumps({"lib": lib, "ms": ts, "value": v}))
+    print(json.dumps({"lib": variant, "ms": ts, "value": v}))
 
 
 def main():

@@ -245,3 +245,34 @@ def test_fused_gram_replicated_shuffled_genes(monkeypatch):
     assert out["1"] == out["0"]
     ref = O.mll(x, y, D, S, B, 2.2, 0.9, 1e-4, negative=False)
     assert abs(out["1"] - ref) <= MLL_RTOL * abs(ref), (out["1"], ref)
+
+
+def test_side_cu_helper_is_bit_identical_and_flops_conserved(c2_dev, monkeypatch):
+    """The side-CU helper (schedule 3, LFM_HELPER, the default: the tail of long steps'
+    trailing updates runs on the 32 chain CUs between chains) changes where units run, not
+    what they compute: the N = 16384 MLL is bit-identical with it off, and the algorithmic
+    flops the profiler books to the main step launches plus the helper launches equal the
+    main launches' alone without it (the host's mirror of the unit enumeration prices the
+    helper's share exactly)."""
+    from dis_project_amd import _lib
+
+    ctx, work, dx, dy = c2_dev
+    res = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("LFM_HELPER", on)  # read per call
+        v = np.empty(1)
+        ctx.check(ctx.lib.lfm_mll_f64_dev(ctx.handle, dx, dy, work.n, work.model.hyp().ref, 0,
+                                          _lib.dptr(v)))  # warm
+        ctx.profile_reset()
+        ctx.profile(True)
+        ctx.check(ctx.lib.lfm_mll_f64_dev(ctx.handle, dx, dy, work.n, work.model.hyp().ref, 0,
+                                          _lib.dptr(v)))
+        ctx.profile(False)
+        st = ctx.profile_read()
+        res[on] = (float(v[0]), st.get("syrk", {}).get("flops", 0.0),
+                   st.get("syrk_side", {}).get("flops", 0.0),
+                   st.get("syrk_side", {}).get("launches", 0))
+    (m1, f1, h1, n1), (m0, f0, h0, n0) = res["1"], res["0"]
+    assert np.isfinite(m1) and m1 == m0
+    assert n1 > 0 and n0 == 0 and h0 == 0.0
+    assert f1 + h1 == pytest.approx(f0, rel=1e-12)
