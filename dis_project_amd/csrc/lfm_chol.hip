@@ -1189,8 +1189,7 @@ __device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
 }
 
 
-// (256, 4): 128 VGPRs, 4 waves / SIMD (the zero-C tile body would otherwise take 134)
-__global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) {
+__device__ __forceinline__ void step_body(const StepArgs& g) {
   __shared__ double sPbuf[(64 + ST) * (LFM_STEP_KS + LDP)];
   double (*sP)[KB + LDP] = reinterpret_cast<double (*)[KB + LDP]>(sPbuf);
   double (*sPu)[LFM_STEP_KS + LDP] = reinterpret_cast<double (*)[LFM_STEP_KS + LDP]>(sPbuf);
@@ -1329,6 +1328,12 @@ __global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) {
     add_dur(6);
   }
 }
+
+// (256, 4): 128 VGPRs, 4 waves / SIMD (the zero-C tile body would otherwise take 134)
+__global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) { step_body(g); }
+// The side-CU helper's launches (rest units only): the same body under its own name, so
+// traces and counters keep the main-stream step launches apart
+__global__ __launch_bounds__(256, 4) void helper_update_kernel(StepArgs g) { step_body(g); }
 
 // ---------------------------------------------------------- fused panel
 // One block column of the look-ahead chain in one launch (w = 1 steps):
@@ -2498,8 +2503,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
           hipStreamWaitEvent(side, evL[2 * (s - 1)], 0);
           hipEvent_t pe;
           prof_begin(ctx, K_SIDE_SYRK, &pe, side);
-          hipLaunchKernelGGL(step_kernel, dim3((unsigned)((hu + 7) / 8 * 8)), dim3(256), 0, side,
-                             h);
+          hipLaunchKernelGGL(helper_update_kernel, dim3((unsigned)((hu + 7) / 8 * 8)), dim3(256),
+                             0, side, h);
           prof_end(ctx, K_SIDE_SYRK, pe, alg_h, 0, side, (double)hu * 64 * ST * 2.0 * g.kd);
           hipEventRecord(evH[2 * s], side);
           helped = true;

@@ -106,7 +106,18 @@ def main():
                   f"- step_kernel time per evaluation {kern_ms:.2f} ms; the traced run's wall "
                   f"{traced['ms_per_step']:.2f} ms per evaluation (consecutive step launches overlap "
                   "at their boundaries, so the kernel sum can exceed the wall)"]
+        helper = next((r for r in rows if short(r["Name"]).startswith("helper_update_kernel")),
+                      None)
+        n = traced.get("config", {}).get("N", 16384)
+        ev_tf = n ** 3 / 3.0 / (traced["ms_per_step"] * 1e-3) / 1e12
+        lines += [f"- whole evaluation: N^3/3 = {n ** 3 / 3.0:.4e} flop over the traced wall = "
+                  f"{ev_tf:.2f} TFLOP/s = **{ev_tf / 78.6:.3f}** of 78.6"]
+        if helper is not None:
+            lines += [f"- side-CU helper (helper_update_kernel, the tail of long steps' updates on "
+                      f"the 32 chain CUs): {int(helper['Calls']) / evals_traced:.0f} launches per "
+                      f"evaluation, {float(helper['AverageNs']) / 1e3:.1f} us average"]
         json.dump({"round": rnd, "step_kernel_avg_us": avg_s * 1e6, "calls_per_eval": calls_per_eval,
+                   "evaluation_tflops": ev_tf, "evaluation_frac": ev_tf / 78.6,
                    "flops_per_launch": rf["flops_per_launch"], "achieved_tflops": ach,
                    "frac": ach / 78.6, "bench_traced_frac": rf["frac"],
                    "step_kernel_ms_per_eval": kern_ms, "traced_wall_ms_per_eval": traced["ms_per_step"]},
