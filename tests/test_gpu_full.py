@@ -276,3 +276,27 @@ def test_side_cu_helper_is_bit_identical_and_flops_conserved(c2_dev, monkeypatch
     assert np.isfinite(m1) and m1 == m0
     assert n1 > 0 and n0 == 0 and h0 == 0.0
     assert f1 + h1 == pytest.approx(f0, rel=1e-12)
+
+
+def test_side_cu_helper_gradient_bit_identical(monkeypatch):
+    """The bordered factorisation of value_and_grad (trainer.py:126) with and without the
+    side-CU helper at N = 16384: the same value bit for bit; the gradient to 1e-12 of its
+    largest component (its reduction accumulates per-workgroup partial sums with atomics, so
+    it is not bit-reproducible from run to run in any case)."""
+    from dis_project_amd import _lib, configs
+
+    work = configs.c2()
+    x = np.ascontiguousarray(work.data.X)
+    y = np.ascontiguousarray(work.data.y.reshape(-1))
+    ctx = _lib.get_context(0)
+    G = work.model.num_genes
+    out = {}
+    for on in ("1", "0"):
+        monkeypatch.setenv("LFM_HELPER", on)
+        gv, val = np.empty(3 * G + 2), np.empty(1)
+        ctx.check(ctx.lib.lfm_mll_grad_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
+                                           work.model.hyp().ref, 1, _lib.dptr(val), _lib.dptr(gv)))
+        out[on] = (float(val[0]), gv.copy())
+    assert np.isfinite(out["1"][0]) and out["1"][0] == out["0"][0]
+    g1, g0 = out["1"][1], out["0"][1]
+    assert np.max(np.abs(g1 - g0)) <= 1e-12 * np.max(np.abs(g0))
