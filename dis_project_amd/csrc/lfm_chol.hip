@@ -2454,8 +2454,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         tall_args(g, 0);
         launch_step(g);
       }
-      hipEvent_t* evL = ev + 1;  // [S] launch s done (main)
-      hipEvent_t* evH = ev + 2;  // stride 2: helper(s) done (side)
+      hipEvent_t* evL = ev + 1;  // evL[2 s] = ev[1 + 2 s]: launch s done (main)
+      hipEvent_t* evH = ev + 2;  // evH[2 s] = ev[2 + 2 s]: helper(s) done (side)
       bool helped = false;       // the previous step had a helper launch
       for (int s = 0; s + 1 < S; ++s) {
         chain(s + 1);
