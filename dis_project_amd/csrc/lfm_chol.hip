@@ -152,6 +152,9 @@ __device__ __forceinline__ void pin16(double (&p)[16]) {
 #ifndef LFM_COH_NT
 #define LFM_COH_NT 1
 #endif
+#ifndef LFM_LEAF_SHARE
+#define LFM_LEAF_SHARE 1
+#endif
 #ifndef LFM_KK_UNROLL
 #define LFM_KK_UNROLL 1
 #endif
@@ -514,6 +517,10 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
     if (nr == 0) break;
     // (3) wave 0: next diagonal block, then its leaf; waves 1-3: the other trailing tiles
     const int nrb = nr / IB;
+    // the early panels' wide trailing triangles: wave 0 takes its last k0 tiles after the leaf
+    // (28 tiles -> 4, 21 -> 2, 15 -> 1), so the four waves reach the barrier together
+    const int ntiles = nrb * (nrb + 1) / 2;
+    const int k0 = LFM_LEAF_SHARE ? max(0, (ntiles - 11) / 4) : 0;
     if (w == 0) {
       if (PH & 4) {
         tile_update(c0 + IB, c0 + IB, c0);
@@ -522,14 +529,20 @@ __device__ __forceinline__ void potrf_block(double* __restrict__ Mb, double* __r
       lstamp(ib, 3, 0);
       if (PH & 1) leaf(ib + 1);
       lstamp(ib, 4, 0);
+      if (PH & 4) {
+        for (int tc = ntiles - k0; tc < ntiles; ++tc) {
+          int ti, tj;
+          tri_tile(tc, &ti, &tj);
+          tile_update(c0 + IB + ti * IB, c0 + IB + tj * IB, c0);
+        }
+      }
     } else if (PH & 4) {
-      const int ntiles = nrb * (nrb + 1) / 2;
       const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform: scalar tile walk
-      for (int t = wu; t < ntiles; t += 6) {
+      for (int t = wu; t < ntiles - k0; t += 6) {
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
           const int tc = t + 3 * u;
-          if (tc >= ntiles) break;
+          if (tc >= ntiles - k0) break;
           int ti, tj;
           tri_tile(tc, &ti, &tj);
           tile_update(c0 + IB + ti * IB, c0 + IB + tj * IB, c0);
