@@ -300,3 +300,32 @@ def test_side_cu_helper_gradient_bit_identical(monkeypatch):
     assert np.isfinite(out["1"][0]) and out["1"][0] == out["0"][0]
     g1, g0 = out["1"][1], out["0"][1]
     assert np.max(np.abs(g1 - g0)) <= 1e-12 * np.max(np.abs(g0))
+
+
+@pytest.mark.parametrize("G,T", [(16, 256), (10, 200)])
+def test_side_cu_helper_forced_on_every_step(monkeypatch, G, T):
+    """The side-CU helper forced onto every eligible step (LFM_HELPER_MIN=0, LFM_HELPER_TC=0:
+    half of each step's rest triangle on the side CUs, including the w = 2 and w = 1 steps
+    where the chain is critical) at N = 4096 (aligned grid, fused gram) and N = 2000 (padded,
+    unaligned): slower, but the MLL is bit-identical to the helper off."""
+    from dis_project_amd import _lib, configs
+
+    work = configs.grid_workload("helper", G, T, seed_params=2, seed_y=3)
+    x = np.ascontiguousarray(work.data.X)
+    y = np.ascontiguousarray(work.data.y.reshape(-1))
+    ctx = _lib.get_context(0)
+    out = {}
+    for env in ({"LFM_HELPER": "0"},
+                {"LFM_HELPER": "1", "LFM_HELPER_MIN": "0", "LFM_HELPER_TC": "0"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        v = np.empty(1)
+        ctx.profile_reset()
+        ctx.profile(True)
+        ctx.check(ctx.lib.lfm_mll_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
+                                      work.model.hyp().ref, 0, _lib.dptr(v)))
+        ctx.profile(False)
+        helpers = ctx.profile_read().get("syrk_side", {}).get("launches", 0)
+        out[env["LFM_HELPER"]] = (float(v[0]), helpers)
+    assert out["0"][1] == 0 and out["1"][1] > 0  # the forced run used helper launches
+    assert np.isfinite(out["1"][0]) and out["1"][0] == out["0"][0]
