@@ -2,35 +2,46 @@
 SIM latent force model at N = 16384 (BASELINE.json configs[1]: 64 genes x 256 timepoints,
 fp64, one MLL evaluation per step), plus the fp64 Cholesky rate.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
 
-One process per GPU. Workloads:
-  c2 (default)  a step = one complete MLL evaluation on each rank (gram fill, Sigma assembly,
-                blocked Cholesky with the residual row, logdet + quadratic form) on x / y
-                resident in HBM, then the RCCL all-gather of the per-rank results (one fp64 slot
-                per rank). Weak scaling: value = evaluations by all ranks / wall.
-  c3            configs[2]: a step = the 32 random restarts of C2, statically partitioned over
-                the ranks (farm.partition, ceil(32/W) slots per rank), one RCCL all-gather of
-                the NaN-padded slots. Strong scaling: value = 32 x steps / wall. Each rank keeps
-                --workers (3) evaluations in flight (farm.ConcurrentEvaluator).
-  c5            configs[4]: a step = the 15 replicate x leave-one-gene-out problems (N = 28),
-                each rank's share in one batched launch, then the all-gather. Strong scaling.
+One process per GPU. Started as a plain command with --gpus N > 1 (no WORLD_SIZE in the
+environment), this process is only a launcher: it never touches a GPU, starts N fresh rank
+processes of itself with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set,
+forwards their output and exits with the first non-zero exit code (the other ranks are then
+stopped). Workloads; the default is c2 on one GPU and c3 on several:
+  c2  configs[1]: a step = one complete MLL evaluation on each rank (gram fill, Sigma
+      assembly, blocked Cholesky with the residual row, logdet + quadratic form) on x / y
+      resident in HBM, then the RCCL all-gather of the per-rank results (one fp64 slot per
+      rank). Weak scaling: value = evaluations by all ranks / wall.
+  c3  configs[2]: a step = the 32 random restarts of C2, statically partitioned over the
+      ranks (farm.partition, ceil(32/W) slots per rank), one RCCL all-gather of the NaN-padded
+      slots. Strong scaling: value = 32 x steps / wall. Each rank keeps --workers evaluations
+      in flight (farm.ConcurrentEvaluator; default: farm.choose_workers for its share).
+  c4  configs[3]: a step = one fp32 lower-triangle gram fill at N = 65536 (256 genes x 256
+      timepoints, 8.6 GB written) into a 17.2 GB device buffer; the HBM roofline of the fill.
+      One GPU (replicas at N > 1: every rank fills its own; weak scaling).
+  c5  configs[4]: a step = the 15 replicate x leave-one-gene-out problems (N = 28), each
+      rank's share in one batched launch, then the all-gather. Strong scaling.
 torch.distributed (gloo, CPU) is only the control plane: barrier, max-over-ranks timing and
 shipping the RCCL unique id.
 
-Rank 0 prints ONE JSON line; ``value`` = evaluations completed by all ranks / the slowest
-rank's wall time of the K timed steps. Every result of the timed steps must be finite, and
-(c2, one rank) the GPU MLL is checked against the C++ CPU restatement on the same inputs.
+Rank 0 prints ONE JSON line; ``value`` = work completed by all ranks / the slowest rank's
+wall time of the K timed steps. Every result of the timed steps must be finite and identical
+across steps, and (one rank) the GPU values are checked against the C++ CPU restatement on
+the same inputs in the cpu_baseline leg.
 """
 
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
-import math
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
@@ -49,6 +60,7 @@ FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix, AMD spec (not in the 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "log-marginal-likelihood evals/sec + fp64 Cholesky GFLOP/s at N=16384"
 PARITY_RTOL = 1e-9             # GPU vs C++ CPU restatement (north_star: 1e-5)
+EPS64 = np.finfo(np.float64).eps
 
 
 def parse(argv=None):
@@ -56,13 +68,15 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=["c2", "c3", "c5"], default="c2")
-    p.add_argument("--genes", type=int, default=64)
+    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default=None,
+                   help="default: c2 on one GPU, c3 (configs[2], the multi-GPU config) on several")
+    p.add_argument("--genes", type=int, default=None)
     p.add_argument("--timepoints", type=int, default=256)
     p.add_argument("--restarts", type=int, default=32)
-    p.add_argument("--workers", type=int, default=3,
+    p.add_argument("--workers", type=int, default=0,
                    help="c3: evaluations in flight per GPU (farm.ConcurrentEvaluator, schedule-1 "
-                        "worker contexts); 1 = one schedule-3 context, one evaluation at a time")
+                        "worker contexts); 1 = one schedule-3 context, one evaluation at a time; "
+                        "0 (default) = farm.choose_workers for the rank's share")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-profile", action="store_true",
@@ -71,18 +85,90 @@ def parse(argv=None):
                    help="rehearsal only: gloo all-gather and ranks sharing the visible GPUs "
                         "(W ranks on fewer cards); the measured configuration is rccl")
     p.add_argument("--share-gpus", action="store_true",
-                   help="rehearsal only: ranks share the visible GPUs (rank -> local %% count) "
-                        "with the RCCL all-gather")
-    return p.parse_args(argv)
+                   help="rehearsal only: ranks share the visible GPUs (rank -> local %% count)")
+    a = p.parse_args(argv)
+    if a.workload is None:
+        a.workload = "c2" if a.gpus == 1 else "c3"
+    if a.genes is None:
+        a.genes = 256 if a.workload == "c4" else 64
+    return a
 
 
+# ------------------------------------------------------------------ launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_gpus() -> int:
+    """GPUs this process could use, counted without initialising the HIP runtime."""
+    return torch.cuda.device_count()
+
+
+def self_launch(a, argv, script=None) -> int:
+    """Start a.gpus rank processes of this script (never touching a GPU here) and wait for
+    them. Returns the first non-zero exit code (the other ranks are then stopped), else 0."""
+    n = a.gpus
+    if n < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        return 2
+    if not (a.share_gpus or a.gather == "gloo"):
+        vis = visible_gpus()
+        if vis < n:
+            print(f"bench.py: --gpus {n} requested but only {vis} GPU(s) are visible "
+                  "(rehearsal on fewer cards: --share-gpus --gather gloo)", file=sys.stderr)
+            return 3
+    port = _free_port()
+    script = script or os.path.abspath(__file__)
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, "-u", script] + list(argv), env=env))
+    rc = 0
+    try:
+        while procs:
+            for p in list(procs):
+                code = p.poll()
+                if code is None:
+                    continue
+                procs.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    print(f"bench.py: rank process {p.pid} exited with {code}; stopping the "
+                          "others", file=sys.stderr)
+                    _stop(procs)
+            time.sleep(0.05)
+    except KeyboardInterrupt:
+        _stop(procs)
+        raise
+    return rc
+
+
+def _stop(procs, grace=30.0):
+    for p in procs:
+        if p.poll() is None:
+            p.send_signal(signal.SIGTERM)
+    t_end = time.monotonic() + grace
+    for p in procs:
+        try:
+            p.wait(timeout=max(0.1, t_end - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+
+
+# ------------------------------------------------------------- CPU baselines
 def cpu_threads(a):
-    t = a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or \
-        len(os.sched_getaffinity(0))
-    return max(1, min(t, 64))
+    return max(1, a.cpu_threads or int(os.environ.get("OMP_NUM_THREADS", "0")) or
+               len(os.sched_getaffinity(0)))
 
 
-def cpu_baseline(work, threads, gpu_value):
+def cpu_baseline_c2(work, threads, gpu_value):
     """The C++ / OpenMP CPU restatement (oracle/lfm_cpu.cpp, 'port') of ONE complete C2
     evaluation on the box's host cores, timed in full and not extrapolated: the reference's
     gram formula (every kernel branch, std::erf) on the real inputs, Sigma, a blocked fp64
@@ -96,7 +182,6 @@ def cpu_baseline(work, threads, gpu_value):
                           negative=False, threads=threads)
     total = time.perf_counter() - t0
     n = work.n
-    rel = abs(v - gpu_value) / abs(v)
     return {
         "value": 1.0 / total,
         "unit": "MLL evals/s",
@@ -109,27 +194,173 @@ def cpu_baseline(work, threads, gpu_value):
         "host_cpus": os.cpu_count(),
         "cholesky_gflops": (n**3 / 3.0) / info["t_chol"] / 1e9,
         "mll": v,
-        "gpu_vs_cpu_rel": rel,
+        "gpu_vs_cpu_rel": abs(v - gpu_value) / abs(v),
     }
 
 
+def cpu_baseline_c3(models, data, threads, gpu_values):
+    """C3 on the CPU: ONE full evaluation of restart 0 (the C++ restatement, all allowed cores)
+    timed and extrapolated to the 32 restarts (every restart is the same N = 16384 work);
+    its MLL checks the GPU farm's restart-0 value."""
+    from oracle import lfm_cpu
+
+    m = models[0]
+    t0 = time.perf_counter()
+    v, info = lfm_cpu.mll(data.X, data.y, m.true_d, m.true_s, m.true_b, m.l, m.obs_stddev,
+                          m.jitter, negative=False, threads=threads)
+    t = time.perf_counter() - t0
+    P = len(models)
+    return {
+        "value": 1.0 / t,
+        "unit": "MLL evals/s",
+        "cores": int(info["threads"]),
+        "kind": "port",
+        "sample": (f"oracle/lfm_cpu.cpp: one full evaluation of restart 0 at N={data.n} "
+                   f"({t:.2f} s on {int(info['threads'])} OpenMP threads of {os.cpu_count()} "
+                   f"host CPUs), extrapolated: {P} restarts x {t:.2f} s = {P * t:.1f} s per step"),
+        "extrapolated": True,
+        "seconds_per_step": P * t,
+        "host_cpus": os.cpu_count(),
+        "mll": v,
+        "gpu_vs_cpu_rel": abs(v - gpu_values[0]) / abs(v),
+    }
+
+
+def cpu_baseline_c5(models, datasets, gpu_values, min_seconds=2.0):
+    """C5 on the CPU: the 15 problems evaluated sequentially on ONE core by the C++
+    restatement, timed in full and repeated until min_seconds have passed (a step is 15
+    evaluations of microseconds each); every value checks the GPU batch's."""
+    from oracle import lfm_cpu
+
+    vals, rounds = [], 0
+    t0 = time.perf_counter()
+    while True:
+        vals = [lfm_cpu.mll(d.X, d.y, m.true_d, m.true_s, m.true_b, m.l, m.obs_stddev,
+                            m.jitter, negative=False, threads=1)[0]
+                for m, d in zip(models, datasets)]
+        rounds += 1
+        if time.perf_counter() - t0 >= min_seconds:
+            break
+    t = time.perf_counter() - t0
+    ref = np.asarray(vals)
+    rel = np.abs(ref - np.asarray(gpu_values)) / np.abs(ref)
+    return {
+        "value": rounds * len(models) / t,
+        "unit": "MLL evals/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"oracle/lfm_cpu.cpp: the {len(models)} problems (N={datasets[0].n}) "
+                   f"sequentially on 1 thread, {rounds} full rounds in {t:.2f} s; "
+                   "timed in full, not extrapolated"),
+        "host_cpus": os.cpu_count(),
+        "gpu_vs_cpu_rel": float(rel.max()),
+    }
+
+
+def cpu_baseline_c4(work, threads, gpu_rows, check_rows):
+    """C4 on the CPU: the reference formula (fp64, every kernel branch, std::erf; stored as
+    float) over every 4th row of the N = 65536 lower triangle (a quarter of the rows, ~1/4 of
+    the pairs), all allowed cores, extrapolated to the full fill by pair count. Checks the
+    GPU's fp32 rows `check_rows` (a subset of the sample) within 16 eps64 M + 4e-6 max|K|
+    (tests/test_gpu_regimes.py's C4 bound; M = the reference formula's intermediate
+    magnitude, oracle.gram_error_scale)."""
+    from oracle import lfm_cpu
+    from oracle import lfm_oracle as O
+
+    m, x = work.model, np.ascontiguousarray(work.data.X)
+    n = work.n
+    rows = np.arange(0, n, 4, dtype=np.int64)
+    t0 = time.perf_counter()
+    ref = lfm_cpu.gram_rows_f32(x, m.true_d, m.true_s, m.l, rows, 0.0, threads)
+    t = time.perf_counter() - t0
+    pairs_sample = float(np.sum(rows + 1))
+    pairs_full = n * (n + 1) / 2.0
+    t_full = t * pairs_full / pairs_sample
+    # parity of the GPU rows against the sample (rows are multiples of 4)
+    idx = np.searchsorted(rows, check_rows)
+    assert np.all(rows[idx] == check_rows)
+    scale = O.gram_error_scale(x[check_rows], x, m.true_d, m.true_s, m.l)
+    kmax = float(np.abs(ref[idx]).max())
+    worst = 0.0
+    for q, r in enumerate(check_rows):
+        tol = 16 * EPS64 * scale[q, : r + 1] + 4e-6 * kmax
+        err = np.abs(gpu_rows[q, : r + 1].astype(np.float64) - ref[idx[q], : r + 1])
+        worst = max(worst, float((err / tol).max()))
+    return {
+        "value": 1.0 / t_full,
+        "unit": "fp32 gram fills/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"oracle/lfm_cpu.cpp gram: every 4th row of the N={n} lower triangle "
+                   f"({rows.size} rows, {pairs_sample:.3g} of {pairs_full:.3g} pairs) in "
+                   f"{t:.2f} s on {threads} OpenMP threads of {os.cpu_count()} host CPUs, "
+                   f"extrapolated by pair count to {t_full:.1f} s per fill"),
+        "extrapolated": True,
+        "host_cpus": os.cpu_count(),
+        "gpu_rows_checked": int(len(check_rows)),
+        "gpu_vs_cpu_err_over_tol": worst,
+    }
+
+
+# ------------------------------------------------------------------ workloads
+def c4_setup(ctx, a):
+    """Device buffers of the C4 fill: x (N x 3) and the N x N fp32 output."""
+    work = configs.c4(a.genes, a.timepoints)
+    x = np.ascontiguousarray(work.data.X)
+    n = work.n
+    lib, h = ctx.lib, ctx.handle
+    dx, dK = _lib.c_void_p(), _lib.c_void_p()
+    ctx.check(lib.lfm_dev_alloc(h, x.nbytes, _lib.ctypes.byref(dx)))
+    ctx.check(lib.lfm_dev_alloc(h, n * n * 4, _lib.ctypes.byref(dK)))
+    ctx.check(lib.lfm_memcpy_h2d(h, dx, x.ctypes.data, x.nbytes))
+    hp = work.model.hyp()
+
+    def step():
+        ctx.check(lib.lfm_gram_f32_dev(h, dx, n, hp.ref, 0.0, _lib.LFM_UPLO_LOWER, dK, n))
+        # a checksum-free scalar per step: the last diagonal element (a device read of 4 B)
+        out = np.empty(1, np.float32)
+        ctx.check(lib.lfm_memcpy_d2h(h, out.ctypes.data,
+                                     _lib.c_void_p(dK.value + (n * n - 1) * 4), 4))
+        return np.array([float(out[0])])
+
+    def rows(rr):
+        got = np.empty((len(rr), n), np.float32)
+        for i, r in enumerate(rr):
+            ctx.check(lib.lfm_memcpy_d2h(h, got[i].ctypes.data,
+                                         _lib.c_void_p(dK.value + int(r) * n * 4), n * 4))
+        return got
+
+    def close():
+        lib.lfm_dev_free(h, dK)
+        lib.lfm_dev_free(h, dx)
+
+    return work, step, rows, close
+
+
 def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     a = parse(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return self_launch(a, argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus and world == 1:
-        raise SystemExit("--gpus > 1 needs torch.distributed.run (one process per GPU)")
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: one process per GPU")
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=900))
 
-    # one GPU per rank; the gloo rehearsal may put several ranks on one card
-    dev = local % max(1, _lib.device_count()) if a.gather == "gloo" or a.share_gpus else local
+    # one GPU per rank; the rehearsal may put several ranks on one card
+    rehearsal = a.gather == "gloo" or a.share_gpus
+    ndev = _lib.device_count()
+    if not rehearsal and local >= ndev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {ndev} GPU(s) visible")
+    dev = local % max(1, ndev) if rehearsal else local
     ctx = _lib.get_context(dev)
     lib, h = ctx.lib, ctx.handle
 
-    # RCCL farm communicator (replicas-only exchange of per-rank results)
-    gather = None
+    # farm communicator (replicas-only exchange of per-rank results)
     if world > 1 and a.gather == "gloo":
         gather = farm.TorchGather(world)
     elif world > 1:
@@ -140,6 +371,8 @@ def main(argv=None):
         gather = lambda send: np.asarray(send, np.float64).copy()  # noqa: E731
     fm = farm.Farm(world, rank, gather)
 
+    workers = None
+    c4_rows = None
     if a.workload == "c2":
         work = configs.grid_workload(f"synthetic_{a.genes}x{a.timepoints}_fp64", a.genes,
                                      a.timepoints, seed_params=2, seed_y=3)
@@ -151,11 +384,19 @@ def main(argv=None):
         def step():
             # one evaluation per rank, gathered: P = world problems, one slot each
             return fm.run(world, lambda idx: ev([work.model]))
+    elif a.workload == "c4":
+        work, one_fill, c4_rows, close = c4_setup(ctx, a)
+        n = work.n
+        per_step = world
+
+        def step():
+            return fm.run(world, lambda idx: one_fill())
     else:
         models, datasets = farm.workload(a.workload, a.genes, a.timepoints, a.restarts)
         n = datasets[0].n
-        evaluate, close = farm.gpu_evaluator(ctx, datasets, negative=False,
-                                           workers=a.workers)
+        mine = len(farm.partition(len(models), world, rank))
+        workers = a.workers if a.workers > 0 else farm.choose_workers(mine)
+        evaluate, close = farm.gpu_evaluator(ctx, datasets, negative=False, workers=workers)
         per_step = len(models)
 
         def step():
@@ -170,21 +411,26 @@ def main(argv=None):
 
     for _ in range(a.warmup):
         results.append(step())
-    prof = not a.no_profile and a.workload == "c2"
-    # HIP events around the priced kernels' launches of the FIRST timed step only: an event
-    # record between two dependent launches widens the dispatch gap, ≈ 0.5 ms per evaluation
-    # with all 65 step launches instrumented; one instrumented step of K costs 0.5 / K ms
-    prof_steps = 1 if prof else 0
+    # HIP events around the priced kernels' launches: c2 in the FIRST timed step only (an
+    # event record between two dependent launches widens the dispatch gap, ≈ 0.5 ms per
+    # evaluation with all step launches instrumented; one instrumented step of K costs
+    # 0.5 / K ms); c4 in every step (one fill launch per step)
+    prof = not a.no_profile and a.workload in ("c2", "c4")
+    prof_steps = (1 if a.workload == "c2" else a.steps) if prof else 0
+    classes = (["syrk", "gram_grid", "potrf", "syrk_side"] if a.workload == "c2"
+               else ["gram_grid", "tables"])
     if prof:
         ctx.profile(False)
         ctx.profile_reset()
-    timed = []
+    timed, step_ms = [], []
     barrier()
     t0 = time.perf_counter()
     for s in range(a.steps):
-        if s < prof_steps:
-            ctx.profile(True, classes=["syrk", "gram_grid", "potrf", "syrk_side"])
+        if s < prof_steps and s == 0:
+            ctx.profile(True, classes=classes)
+        ts = time.perf_counter()
         timed.append(step())
+        step_ms.append((time.perf_counter() - ts) * 1e3)
         if s + 1 == prof_steps:
             ctx.profile(False)
     barrier()
@@ -196,7 +442,7 @@ def main(argv=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     # the exchange step alone (collective latency reported separately): the same
-    # RCCL all-gather of this workload's NaN-padded slots, outside the timed region
+    # all-gather of this workload's NaN-padded slots, outside the timed region
     collective = None
     if world > 1:
         slots = max(farm.slots_per_rank(per_step, world), 1)
@@ -214,53 +460,68 @@ def main(argv=None):
     # the timed region's results: all finite, every step the same values (same inputs)
     res = np.array(timed)
     if not np.all(np.isfinite(res)):
-        raise SystemExit(f"non-finite MLL in the timed region: {res[~np.isfinite(res)][:4]}")
+        raise SystemExit(f"non-finite result in the timed region: {res[~np.isfinite(res)][:4]}")
     if not np.all(res == res[0]):
-        raise SystemExit("timed steps disagree (the same inputs gave different MLLs)")
+        raise SystemExit("timed steps disagree (the same inputs gave different results)")
 
-    evals = per_step * a.steps
-    value = evals / elapsed
+    value = per_step * a.steps / elapsed
     ms_per_step = elapsed / a.steps * 1e3
     chol_flops = n**3 / 3.0
-    strong = a.workload != "c2"
+    scaling = "strong" if a.workload in ("c3", "c5") else "weak"
     if a.workload == "c2":
         wl = (f"configs[1]: one MLL eval per rank, {a.genes} genes x {a.timepoints} timepoints, "
               f"N={n}, fp64")
     elif a.workload == "c3":
         wl = (f"configs[2]: {len(res[0])} random restarts of the {a.genes}x{a.timepoints} grid "
               f"(N={n}, fp64) per step, farmed over {world} GPU(s), "
-              + (f"{a.workers} concurrent schedule-1 evaluations per GPU" if a.workers > 1
+              + (f"{workers} concurrent schedule-1 evaluations per GPU" if workers > 1
                  else "one schedule-3 evaluation at a time per GPU"))
+    elif a.workload == "c4":
+        wl = (f"configs[3]: one fp32 lower-triangle gram fill per rank, {a.genes} genes x "
+              f"{a.timepoints} timepoints, N={n} (Sigma stored as an N x N fp32 buffer)")
     else:
         wl = (f"configs[4]: 3 replicates x 5 leave-one-gene-out ablations (N={n}) per step, "
               f"farmed over {world} GPU(s), one batched launch per rank")
+    c4 = a.workload == "c4"
     line = {
-        "metric": METRIC,
+        "metric": METRIC if not c4 else "fp32 gram fills/sec at N=65536 (configs[3])",
         "value": value,
-        "unit": "MLL evals/s",
+        "unit": "MLL evals/s" if not c4 else "fp32 gram fills/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": ms_per_step,
+        "median_ms_per_step": float(np.median(step_ms)),
         "higher_is_better": True,
-        "scaling": "strong" if strong else "weak",
+        "scaling": scaling,
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": "f64" if not c4 else "f32",
         "data": "synthetic (seeded numpy: D~U[.2,1], S~U[.5,1.5], B~U[.01,.1], y = B/D + "
                 "0.5 N(0,1), t = linspace(0,12,T))",
         "config": {"workload": wl, "N": n,
                    "genes": a.genes if a.workload != "c5" else 4,
                    "timepoints": a.timepoints if a.workload != "c5" else 7,
                    "problems_per_step": per_step, "parallelism": f"replicas{world}",
-                   "exchange": "RCCL all-gather of NaN-padded per-rank result slots"
+                   "exchange": ("RCCL all-gather of NaN-padded per-rank result slots"
+                                if a.gather == "rccl" else "gloo all-gather (rehearsal)")
                                if world > 1 else "none"},
-        "mll_first": float(res[0][0]),
+        "result_first": float(res[0][0]),
     }
+    if workers is not None:
+        line["config"]["workers_per_gpu"] = workers
     if collective:
         line["collective"] = collective
-    if a.workload == "c2":
-        line["cholesky_gflops_per_gpu"] = chol_flops / (ms_per_step * 1e-3) / 1e9
-    if prof and rank == 0:
+    if a.workload in ("c2", "c3"):
+        line["cholesky_gflops_per_gpu"] = chol_flops * value / world / 1e9
+    if a.workload == "c3":
+        # the whole factorisation's N^3/3 per evaluation over the wall time, per GPU: the farm's
+        # schedule-1 workers interleave several kernels, so no single kernel is priced here
+        ach = chol_flops * value / world / 1e12
+        line["roofline"] = {
+            "kernel": "whole evaluation (N^3/3 flop per MLL over the wall time, per GPU)",
+            "bound": "mfma", "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None}
+    if prof and rank == 0 and a.workload == "c2":
         syrk = stats.get("syrk", {})
         gram = stats.get("gram_grid", {})
         chain = stats.get("potrf", {})
@@ -268,19 +529,27 @@ def main(argv=None):
                                       for k, v in stats.items() if v["launches"]}
         if syrk.get("launches"):
             ach = syrk["flops"] / (syrk["total_ms"] * 1e-3) / 1e12
-            traffic = None
+            traffic, tsrc = None, None
             tf = os.path.join(ROOT, "profiles", "syrk_traffic.json")
             if os.path.exists(tf):
                 try:
-                    # PMC bytes per evaluation over this run's launches per evaluation
-                    per_eval = json.load(open(tf)).get("hbm_bytes_per_eval")
+                    rec = json.load(open(tf))
+                    per_eval = rec.get("hbm_bytes_per_eval")
                     traffic = per_eval / (syrk["launches"] / prof_steps) if per_eval else None
+                    tsrc = ("PMC (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction) bytes "
+                            "per evaluation from profiles/syrk_traffic.json, measured on the "
+                            "event-ordered schedule 3 (LFM_S3_EVENTS=1, no side-CU helper: "
+                            f"{rec.get('launches_per_eval', 'n/a')} step launches per eval) - "
+                            "device-side cross-stream waits cannot run under the counters' "
+                            "serialised dispatch - divided by this run's "
+                            f"{syrk['launches'] // prof_steps} launches per evaluation")
                 except Exception:
                     traffic = None
             line["roofline"] = {
                 "kernel": "step_kernel (fp64 MFMA trailing update + tall panel solve)",
                 "bound": "mfma", "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                "traffic_source": tsrc,
                 "launches": syrk["launches"],
                 "avg_launch_ms": syrk["total_ms"] / syrk["launches"],
                 "flops_per_launch": syrk["flops"] / syrk["launches"],
@@ -309,36 +578,54 @@ def main(argv=None):
                     "achieved": side["flops"] / (side["total_ms"] * 1e-3) / 1e12,
                 }
         if gram.get("launches"):
-            gbs = gram["bytes"] / (gram["total_ms"] * 1e-3) / 1e9
             # fused (the schedule-3 default on this layout): the gram kernel writes only the
             # first block column and the next super-panel's diagonal block; the first trailing
             # update generates every other Sigma tile from the tables
-            fused = gram["bytes"] < 0.5 * 8.0 * n * (n + 1) / 2 * prof_steps
-            if fused:
-                # no HBM roofline to claim: the fill is no longer a kernel of its own
-                line["gram"] = {
-                    "fused": True,
-                    "kernel": "gram_region_kernel (first block column + next diagonal block; "
-                              "the rest of Sigma is generated inside the first trailing update)",
-                    "bytes_per_eval": gram["bytes"] / prof_steps,
-                    "ms_per_eval": gram["total_ms"] / prof_steps,
-                    "unfused_bytes": 8.0 * n * (n + 1) / 2,
-                }
-            else:
-                line["gram_roofline"] = {
-                    "kernel": "gram_grid_aligned_kernel (lower-triangle fp64 fill)",
-                    "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": gbs / HBM_PEAK_GBS,
-                    "bytes_per_launch": gram["bytes"] / gram["launches"],
-                    "avg_launch_ms": gram["total_ms"] / gram["launches"],
-                }
-    if rank == 0 and world == 1 and a.workload == "c2" and not a.no_cpu_baseline:
-        cb = cpu_baseline(work, cpu_threads(a), float(res[0][0]))
+            line["gram"] = {
+                "fused": gram["bytes"] < 0.5 * 8.0 * n * (n + 1) / 2 * prof_steps,
+                "kernel": "gram_region_kernel (first block column + next diagonal block; "
+                          "the rest of Sigma is generated inside the first trailing update)",
+                "bytes_per_eval": gram["bytes"] / prof_steps,
+                "ms_per_eval": gram["total_ms"] / prof_steps,
+                "unfused_bytes": 8.0 * n * (n + 1) / 2,
+            }
+    if prof and rank == 0 and c4:
+        gram = stats.get("gram_grid", {})
+        tab = stats.get("tables", {})
+        if gram.get("launches"):
+            gbs = gram["bytes"] / (gram["total_ms"] * 1e-3) / 1e9
+            line["roofline"] = {
+                "kernel": "gram_grid_aligned_kernel (fp32 lower-triangle fill)",
+                "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": gbs / HBM_PEAK_GBS, "traffic": None,
+                "bytes_per_launch": gram["bytes"] / gram["launches"],
+                "bytes_basis": "algorithmic: 4 B per lower element incl. the diagonal, "
+                               "4 N (N + 1) / 2",
+                "launches": gram["launches"],
+                "avg_launch_ms": gram["total_ms"] / gram["launches"],
+            }
+            if tab.get("launches"):
+                line["roofline"]["tables_ms_per_fill"] = tab["total_ms"] / tab["launches"]
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        thr = cpu_threads(a)
+        if a.workload == "c2":
+            cb = cpu_baseline_c2(work, thr, float(res[0][0]))
+            bad = not cb["gpu_vs_cpu_rel"] <= PARITY_RTOL
+        elif a.workload == "c3":
+            cb = cpu_baseline_c3(models, datasets[0], thr, res[0])
+            bad = not cb["gpu_vs_cpu_rel"] <= PARITY_RTOL
+        elif a.workload == "c5":
+            cb = cpu_baseline_c5(models, datasets, res[0])
+            bad = not cb["gpu_vs_cpu_rel"] <= PARITY_RTOL
+        else:
+            check = np.array([0, 4, 256, 32768, n - 4, 4 * 5000, 4 * 9999, 4 * 16000])
+            cb = cpu_baseline_c4(work, thr, c4_rows(check), check)
+            bad = not cb["gpu_vs_cpu_err_over_tol"] <= 1.0
         line["cpu_baseline"] = cb
-        if not cb["gpu_vs_cpu_rel"] <= PARITY_RTOL:
+        if bad:
             print(json.dumps(line), flush=True)
-            raise SystemExit(f"GPU MLL {res[0][0]!r} differs from the CPU restatement "
-                             f"{cb['mll']!r} by {cb['gpu_vs_cpu_rel']:.2e} relative")
+            raise SystemExit(f"GPU result differs from the CPU restatement beyond tolerance: "
+                             f"{ {k: v for k, v in cb.items() if 'gpu_vs' in k} }")
     if rank == 0:
         print(json.dumps(line), flush=True)
     close()
@@ -346,7 +633,8 @@ def main(argv=None):
         gather.close()
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

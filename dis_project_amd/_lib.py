@@ -21,6 +21,9 @@ import numpy as np
 
 LIB_NAME = "liblfm.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# diagnostics (include/lfm_diag.h): a library of their own, linked against liblfm.so
+DIAG_NAME = "liblfm_diag.so"
+DIAG_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), DIAG_NAME)
 
 LFM_OK = 0
 LFM_E_ARG = 1
@@ -136,9 +139,12 @@ PRODUCT_SIGNATURES = [
     ("lfm_farm_destroy", c_int, [_c_ctx]),
 ]
 
-# include/lfm_diag.h: probes and phase stamps (measurement / known-answer tests only)
+# include/lfm_diag.h (liblfm_diag.so): probes, phase stamps and the schedule-3 tenancy state
+# (measurement / known-answer tests only)
 DIAG_SIGNATURES = [
     ("lfm_debug_stamps", c_int, [_c_ctx, c_int, POINTER(ctypes.c_ulonglong), c_int]),
+    ("lfm_debug_last_schedule", c_int, [_c_ctx, POINTER(c_int)]),
+    ("lfm_debug_lock_path", c_int, [_c_ctx, ctypes.c_char_p, c_int]),
     ("lfm_probe_rsq", c_int, [_c_ctx, c_void_p, c_int64, c_void_p]),
     ("lfm_probe_mfma_f64_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr]),
     ("lfm_probe_mfma4_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr, _dptr]),
@@ -148,13 +154,12 @@ DIAG_SIGNATURES = [
     ("lfm_probe_syrk", c_int, [_c_ctx, c_int, c_int, c_int, c_int, _dptr]),
 ]
 
-SIGNATURES = PRODUCT_SIGNATURES + DIAG_SIGNATURES
-
 # kernel classes in lfm_profile_read order (lfm_internal.h KClass)
 KCLASSES = ["tables", "gram_grid", "gram_direct", "augment", "potrf", "trsm", "syrk",
             "finalize", "small_mll", "mean", "grad", "panel", "syrk_side"]
 
 _lib = None
+_diag = None
 _lib_lock = threading.Lock()
 
 
@@ -172,7 +177,7 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
                 " or make -C dis_project_amd/csrc). There is no CPU fallback.",
             )
         lib = ctypes.CDLL(p)
-        for name, res, args in SIGNATURES:
+        for name, res, args in PRODUCT_SIGNATURES:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
@@ -181,6 +186,24 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
         if path is None:
             _lib = lib
         return lib
+
+
+def load_diag() -> ctypes.CDLL:
+    """Load liblfm_diag.so (after liblfm.so, whose contexts it takes) and declare the
+    include/lfm_diag.h signatures. Measurement scripts and tests only."""
+    global _diag
+    load_library()
+    with _lib_lock:
+        if _diag is None:
+            if not os.path.exists(DIAG_PATH):
+                raise LfmError(LFM_E_STATE, f"{DIAG_PATH} not found: make -C dis_project_amd/csrc")
+            lib = ctypes.CDLL(DIAG_PATH)
+            for name, res, args in DIAG_SIGNATURES:
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _diag = lib
+        return _diag
 
 
 def as_f64(a, shape=None) -> np.ndarray:
@@ -248,6 +271,11 @@ class Context:
             self.close()
         except Exception:
             pass
+
+    @property
+    def diag(self) -> ctypes.CDLL:
+        """liblfm_diag.so (include/lfm_diag.h), loaded on first use."""
+        return load_diag()
 
     # -- factorisation schedule (include/lfm.h: lfm_ctx_set_schedule)
     @property

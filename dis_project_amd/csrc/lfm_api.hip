@@ -4,7 +4,10 @@
 // Every entry point binds the ctx's device, enqueues on the ctx's stream and is
 // synchronous at return (one hipStreamSynchronize per call).
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <rccl/rccl.h>
+#include <sys/file.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <climits>
@@ -12,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <mutex>
 
 #include "lfm_internal.h"
 
@@ -235,6 +239,81 @@ struct DeviceGuard {
   DeviceGuard(int dev) { hipSetDevice(dev); }
 };
 
+// ------------------------------------------------------ schedule-3 tenancy
+// Schedule 3 is single tenant per GPU: its factor chain needs all of its workgroups resident on
+// the reserved CUs, and two chains on the same CUs starve each other at their grid barriers
+// until the bounded waits fire (LFM_E_TIMEOUT). A schedule-3 factorisation therefore holds
+//   * a per-device mutex of this process for the whole call (enqueue to the final
+//     synchronise): threads of one process take turns — each evaluation runs the same
+//     schedule-3 arithmetic, so its result is bit-identical to running alone;
+//   * an advisory flock on /tmp/lfm_gpu_<PCI bus id>.lock (TMPDIR if set), tried without
+//     blocking: if another process holds it, this call runs schedule 1 instead (look-ahead on
+//     every CU, no device-side waits between streams; equal to the schedule-3 value to
+//     rounding, tests/test_gpu_farm_tenancy.py), so neither process stalls.
+// The key is the PCI bus id, not the device ordinal, which depends on each process's
+// HIP_VISIBLE_DEVICES.
+constexpr int kMaxDevices = 64;
+std::mutex g_dev_mutex[kMaxDevices];
+std::mutex g_fd_mutex;
+int g_lock_fd[kMaxDevices] = {};        // 0: not opened yet; -1: unavailable
+std::string g_lock_path[kMaxDevices];
+
+int device_lock_fd(int dev) {
+  std::lock_guard<std::mutex> lk(g_fd_mutex);
+  if (g_lock_fd[dev] != 0) return g_lock_fd[dev];
+  char bus[64] = {0};
+  int fd = -1;
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) == hipSuccess) {
+    for (char* c = bus; *c; ++c)
+      if (*c == ':' || *c == '.') *c = '_';
+    const char* tmp = std::getenv("TMPDIR");
+    g_lock_path[dev] = std::string(tmp && *tmp ? tmp : "/tmp") + "/lfm_gpu_" + bus + ".lock";
+    fd = ::open(g_lock_path[dev].c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  }
+  g_lock_fd[dev] = fd >= 0 ? fd : -1;
+  return g_lock_fd[dev];
+}
+
+}  // namespace
+
+namespace lfm {
+std::string tenancy_lock_path(int dev) {
+  if (dev < 0 || dev >= kMaxDevices) return std::string();
+  device_lock_fd(dev);
+  std::lock_guard<std::mutex> lk(g_fd_mutex);
+  return g_lock_path[dev];
+}
+}  // namespace lfm
+
+namespace {
+
+class S3Tenancy {
+ public:
+  explicit S3Tenancy(lfm_ctx* ctx) : ctx_(ctx) {
+    ctx->s3_yield = false;
+    if (!s3_on(ctx) || ctx->device < 0 || ctx->device >= kMaxDevices) return;
+    mu_ = &g_dev_mutex[ctx->device];
+    mu_->lock();
+    fd_ = device_lock_fd(ctx->device);
+    if (fd_ >= 0 && ::flock(fd_, LOCK_EX | LOCK_NB) != 0) {
+      ctx->s3_yield = true;  // another process's schedule-3 evaluation: run schedule 1
+      fd_ = -1;
+    }
+  }
+  ~S3Tenancy() {
+    if (fd_ >= 0) ::flock(fd_, LOCK_UN);
+    if (mu_) mu_->unlock();
+    ctx_->s3_yield = false;
+  }
+  S3Tenancy(const S3Tenancy&) = delete;
+  S3Tenancy& operator=(const S3Tenancy&) = delete;
+
+ private:
+  lfm_ctx* ctx_;
+  std::mutex* mu_ = nullptr;
+  int fd_ = -1;
+};
+
 int finish(lfm_ctx* ctx) {
   hipError_t e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) return hip_fail(ctx, e, "stream synchronize");
@@ -254,6 +333,7 @@ int mll_blocked(lfm_ctx* ctx, const Staged& st, const double* d_x, const double*
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)Mp * Mp * sizeof(double));
   if (r) return r;
   const double noise = hyp->obs_stddev * hyp->obs_stddev;  // objectives.py:66
+  S3Tenancy tenancy(ctx);  // held to the final synchronise (finish)
   GramGen gen;
   const bool fuse = chol_fuses_gram(ctx, CHOL_MLL, st.lay, n);
   if (st.lay.ok) {
@@ -797,6 +877,7 @@ int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
   r = ensure(ctx, (void**)&ctx->gacc, &ctx->gacc_bytes, (size_t)(5 * G + 3) * sizeof(double));
   if (r) return r;
   const double noise = hyp->obs_stddev * hyp->obs_stddev;  // objectives.py:66
+  S3Tenancy tenancy(ctx);  // held to the final synchronise (finish)
   GramGen gen;
   const bool fuse = chol_fuses_gram(ctx, CHOL_INVERSE, st.lay, n);
   if (st.lay.ok) {
@@ -1038,6 +1119,7 @@ int lfm_log_prob_f64(lfm_ctx* ctx, const double* loc, const double* scale, int64
   HypDev h{nullptr, nullptr, nullptr, 1, 1.0};
   r = launch_augment(ctx, h, nullptr, ctx->xin + n, ctx->xin, n, ctx->A, Mp, Mp);
   if (r) return r;
+  S3Tenancy tenancy(ctx);  // held to the final synchronise (finish)
   r = chol_factor_solve(ctx, ctx->A, Mp, n, Mp, 0, ctx->result);
   if (r) return r;
   double* hres = ctx->hpin + (ctx->hpin_bytes / 8 - 8);
@@ -1123,38 +1205,6 @@ int lfm_profile_read(lfm_ctx* ctx, lfm_kstat* stats, int max, int* count) {
   *count = K_NCLASS;
   for (int i = 0; i < std::min(max, (int)K_NCLASS); ++i) stats[i] = ctx->stats[i];
   return LFM_OK;
-}
-
-int lfm_probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y) {
-  if (!ctx || !x || !y || n < 1) return LFM_E_ARG;
-  DeviceGuard g(ctx->device);
-  return probe_rsq(ctx, x, n, y);
-}
-
-// Diagnostics: enable = 1 turns on s_memrealtime (100 MHz) stamps of the schedule-3 chain
-// kernel's phases (16 per super-panel step, 256 steps); enable = 0 copies them out (max
-// values) and turns them off.
-int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max) {
-  if (!ctx) return LFM_E_ARG;
-  DeviceGuard g(ctx->device);
-  const size_t cnt = 256 * 24;  // 256 chain rows of 16, then 256 step-launch rows of 8
-  if (enable) {
-    if (!ctx->dbg_stamps) {
-      hipError_t e = hipMalloc((void**)&ctx->dbg_stamps, cnt * 8);
-      if (e != hipSuccess) return hip_fail(ctx, e, "debug stamps");
-    }
-    hipError_t e = hipMemsetAsync(ctx->dbg_stamps, 0, cnt * 8, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    return hip_fail(ctx, e, "debug stamps");
-  }
-  if (!ctx->dbg_stamps) return LFM_OK;
-  finish(ctx);
-  hipError_t e = hipMemcpyAsync(out, ctx->dbg_stamps, std::min<size_t>(cnt, (size_t)max) * 8,
-                                hipMemcpyDeviceToHost, ctx->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-  hipFree(ctx->dbg_stamps);
-  ctx->dbg_stamps = nullptr;
-  return hip_fail(ctx, e, "debug stamps");
 }
 
 // ------------------------------------------------------------- RCCL farm
@@ -1249,44 +1299,6 @@ int lfm_farm_destroy(lfm_ctx* ctx) {
   ctx->nranks = 0;
   ctx->rank = -1;
   return LFM_OK;
-}
-
-int lfm_probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double* ms) {
-  if (!ctx || !tflops || !ms || nblocks < 1 || iters < 1) return LFM_E_ARG;
-  DeviceGuard g(ctx->device);
-  return probe_mfma_f64(ctx, nblocks, iters, tflops, ms);
-}
-
-int lfm_probe_mfma_f64_cycles(lfm_ctx* ctx, int nblocks, int iters, double* cyc_per_mfma,
-                              double* mhz) {
-  if (!ctx || !cyc_per_mfma || !mhz || nblocks < 1 || iters < 1) return LFM_E_ARG;
-  DeviceGuard g(ctx->device);
-  return probe_mfma_f64_cycles(ctx, nblocks, iters, cyc_per_mfma, mhz);
-}
-
-int lfm_probe_mfma4_layout(lfm_ctx* ctx, const double* a, const double* b, const double* c,
-                           double* d) {
-  if (!ctx || !a || !b || !c || !d) return LFM_E_ARG;
-  DeviceGuard g(ctx->device);
-  return probe_mfma4_layout(ctx, a, b, c, d);
-}
-
-int lfm_probe_rate(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflops) {
-  if (!ctx || !tflops || nblocks < 1 || iters < 1) return LFM_E_ARG;
-  DeviceGuard g(ctx->device);
-  return probe_rates(ctx, which, nblocks, iters, tflops);
-}
-
-int lfm_probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
-  if (!ctx || !us || T < 1 || reps < 1 || kd < 16 || kd > 2048 || kd % 16) return LFM_E_ARG;
-  DeviceGuard g(ctx->device);
-  return probe_syrk(ctx, T, kd, cio, reps, us);
-}
-
-int lfm_probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d) {
-  if (!ctx || !a || !b || !d) return LFM_E_ARG;
-  DeviceGuard g(ctx->device);
-  return probe_mfma_f64_layout(ctx, a, b, d);
 }
 
 }  // extern "C"

@@ -199,15 +199,6 @@ __device__ __forceinline__ double ld1(const double* p) {
   return *p;
 }
 
-// 1/sqrt(x) to ~1 ulp: v_rsq_f64 estimate + two Newton steps (a pivot and its inverse
-// come from one estimate instead of a correctly rounded sqrt followed by a divide).
-// One Newton step: the pivot's relative error stays far below the 1e-9 MLL tolerance (a
-// perturbation of the pivot by a factor (1 + e) is a backward error e in that column).
-__device__ __forceinline__ double rsqrt_1nr(double x) {
-  const double h = -0.5 * x;
-  const double y = __builtin_amdgcn_rsq(x);
-  return y * fma(h * y, y, 1.5);
-}
 __device__ __forceinline__ double rsqrt_nr(double x) {
   double y = __builtin_amdgcn_rsq(x);
   y = y * fma(-0.5 * x * y, y, 1.5);
@@ -2015,140 +2006,79 @@ int env_int(const char* name, int def) {
 }
 }  // namespace
 
-// Diagnostic: the pivot reciprocal square root of the diagonal factor (v_rsq_f64 + one
-// Newton step) over host values x[n] -> y[n] (tests bound its relative error).
-__global__ void rsq_probe_kernel(const double* x, double* y, int64_t n) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < n) y[i] = rsqrt_1nr(x[i]);
-}
-
-int probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y) {
-  double* d = nullptr;
-  hipError_t e = hipMalloc((void**)&d, 2 * n * sizeof(double));
-  if (e != hipSuccess) return hip_fail(ctx, e, "probe rsq");
-  hipMemcpyAsync(d, x, n * 8, hipMemcpyHostToDevice, ctx->stream);
-  hipLaunchKernelGGL(rsq_probe_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
-                     d, d + n, n);
-  hipMemcpyAsync(y, d + n, n * 8, hipMemcpyDeviceToHost, ctx->stream);
-  e = hipStreamSynchronize(ctx->stream);
-  hipFree(d);
-  return hip_fail(ctx, e, "probe rsq");
-}
-
-// Pseudo-random doubles in [-1/32, 1/32) (probe data: MFMA power, hence clocks, depends on it).
-__global__ void fill_hash_kernel(double* a, int64_t cnt) {
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) {
-    uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull;
-    h ^= h >> 31;
-    h *= 0xBF58476D1CE4E5B9ull;
-    h ^= h >> 29;
-    a[i] = ((double)(h >> 11) * 0x1.0p-53 - 0.5) * 0.0625;
-  }
-}
-
-// Diagnostic: average duration (us) of one full-lower-triangle trailing-update launch (64-row
-// slabs) over a T x T grid of 128-tiles with update depth kd. cio bit 0: C tile I/O (else the
-// MFMAs alone), bit 3: random operands (else zeros), bit 4: on schedule 3's CU-masked bulk
-// stream instead of every CU, bit 6: the step kernel's rest role (bit 5: without C loads).
-// With bit 6, the rest of a w = 1 step launch's structure (to bisect what a real step costs
-// beyond its rest triangle): bit 7 the ahead band (tile column 0 below the diagonal tile, the
-// rest triangle then over columns >= 1, coherent stores, a_done bumps), bit 8 the tall units
-// (X = A21 Bd at depth 128 for the rows below tile 0, no waits), bit 9 the panel read from a
-// separate 128-wide buffer (the real steps' X_s) instead of A's own columns. Bit 11 (instead
-// of bit 6): syrk_kernel's 128 x 128 units over the same triangle.
-int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
-  const int64_t n = (int64_t)T * ST + 512;
-  const size_t xb = (cio & (512 | 256)) ? (size_t)n * 128 * 8 : 0;  // X_s / X_{s+1} slabs
-  int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8 + 2 * xb + 4096);
-  if (r) return r;
-  if (cio & 8)
-    hipLaunchKernelGGL(fill_hash_kernel, dim3(4096), dim3(256), 0, ctx->stream, ctx->A,
-                       n * n + 2 * (int64_t)(xb / 8));
-  else
-    hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8 + 2 * xb, ctx->stream);
-  hipMemsetAsync(ctx->A + (size_t)n * n + 2 * (xb / 8), 0, 4096, ctx->stream);
+// Diagnostics hook (liblfm_diag.so's lfm_probe_syrk, include/lfm_diag.h): ONE launch of the
+// trailing-update kernel over a full lower triangle of T x T 128-tiles at depth kd on the
+// n x n matrix ctx->A (operands prepared by the caller; X_s / X_{s+1} / counters after it).
+// cio bit 0: C tile I/O (else the MFMAs alone), bit 4: on schedule 3's CU-masked bulk stream
+// instead of every CU, bit 6: the step kernel's rest role (bit 5: without C loads). With bit
+// 6, the rest of a w = 1 step launch's structure: bit 7 the ahead band (tile column 0 below
+// the diagonal tile, the rest triangle then over columns >= 1, coherent stores, a_done
+// bumps), bit 8 the tall units (X = A21 Bd at depth 128 for the rows below tile 0, no waits),
+// bit 9 the panel read from a separate 128-wide buffer (the real steps' X_s) instead of A's
+// own columns. Bit 11 (instead of bit 6): syrk_kernel's 128 x 128 units. Launches only: no
+// kernel of its own, no allocation.
+int probe_update_launch(lfm_ctx* ctx, hipStream_t st, int T, int kd, int cio, int64_t n,
+                        size_t xb) {
   const unsigned units = (unsigned)((int64_t)T * (T + 1));
-  hipStream_t st = (cio & 16) && ctx->m3 ? ctx->m3 : ctx->stream;
-  if (st != ctx->stream) {
-    hipEvent_t f;
-    hipEventCreate(&f);
-    hipEventRecord(f, ctx->stream);
-    hipStreamWaitEvent(st, f, 0);
-    hipEventDestroy(f);
-  }
   const Panel pan{ctx->A, n, 0};
-  auto go = [&]() {
-    if (cio & 64) {
-      // the schedule-3 step kernel's rest role alone (the production unit: 16-deep stages,
-      // 4 workgroups / CU, supertile order); bit 5: no C loads (C = 0, stores kept)
-      StepArgs g{};
-      g.A = ctx->A;
-      g.lda = n;
-      g.s0 = 512;
-      g.px = pan;
-      g.kd = kd;
-      g.T = T;
-      g.nr = (int)units;
-      g.n = n;
-      g.pad_end = INT64_MAX;
-      g.spin = ctx->spin_limit;
-      g.zero_from = (cio & 32) ? 0 : INT64_MAX;
-      g.copy_from = INT64_MAX;
-      double* xs = ctx->A + (size_t)n * n;  // [X_s | X_{s+1} | counters]
-      unsigned* ctr = reinterpret_cast<unsigned*>(xs + 2 * (xb / 8));
-      if (cio & 512) g.px = Panel{xs, 128, 512};
-      unsigned grid = (units + 7) / 8 * 8;
-      if (cio & 128) {
-        g.wn = 1;
-        g.na = 2 * (T - 1);
-        g.nr = (T - 1) * T;
-        g.a_done = ctr;
-        grid = (g.na + 7) / 8 * 8 + (g.nr + 7) / 8 * 8;
-      }
-      if (cio & 256) {
-        g.tw = 1;
-        g.tr0 = 512 + ST;
-        g.tk0 = 0;
-        g.nt = 2 * (T - 1);
-        g.Bd = ctx->A;
-        g.X = xs + xb / 8;
-        g.zvec = xs;
-        g.a_done = nullptr;
-        grid = (g.na + 7) / 8 * 8 + (g.nr + 7) / 8 * 8 + (g.nt + 7) / 8 * 8;
-      }
-      // unit-duration stamps in step slot 0 while lfm_debug_stamps is on (scripts/unit_time.py)
-      g.stamps = ctx->dbg_stamps ? ctx->dbg_stamps + 256 * 16 : nullptr;
-      hipLaunchKernelGGL(step_kernel, dim3(grid), dim3(256), 0, st, g);
-    } else if (cio & 2048)
-      // 128 x 128 units (2 workgroups / CU, 64 x 64 per wave), the same triangle
-      hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(units / 2), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, pan, kd, T, 0, T, 0, 1, 0, (int64_t)0);
-    else if (cio & 1)
-      hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(units), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, pan, kd, T, 0, T, 0, 1, 0, (int64_t)0);
-    else
-      hipLaunchKernelGGL((syrk_kernel<false, 64>), dim3(units), dim3(256), 0, st, ctx->A, n,
-                         (int64_t)512, pan, kd, T, 0, T, 0, 1, 0, (int64_t)0);
-  };
-  go();
-  hipEvent_t a, b;
-  hipEventCreate(&a);
-  hipEventCreate(&b);
-  hipEventRecord(a, st);
-  for (int i = 0; i < reps; ++i) go();
-  hipEventRecord(b, st);
-  hipError_t e = hipStreamSynchronize(st);
-  float ms = 0;
-  hipEventElapsedTime(&ms, a, b);
-  hipEventDestroy(a);
-  hipEventDestroy(b);
-  *us = ms * 1e3 / reps;
-  return hip_fail(ctx, e, "probe_syrk");
+  if (cio & 64) {
+    // the schedule-3 step kernel's rest role alone (the production unit: 16-deep stages,
+    // 4 workgroups / CU, supertile order); bit 5: no C loads (C = 0, stores kept)
+    StepArgs g{};
+    g.A = ctx->A;
+    g.lda = n;
+    g.s0 = 512;
+    g.px = pan;
+    g.kd = kd;
+    g.T = T;
+    g.nr = (int)units;
+    g.n = n;
+    g.pad_end = INT64_MAX;
+    g.spin = ctx->spin_limit;
+    g.zero_from = (cio & 32) ? 0 : INT64_MAX;
+    g.copy_from = INT64_MAX;
+    double* xs = ctx->A + (size_t)n * n;  // [X_s | X_{s+1} | counters]
+    unsigned* ctr = reinterpret_cast<unsigned*>(xs + 2 * (xb / 8));
+    if (cio & 512) g.px = Panel{xs, 128, 512};
+    unsigned grid = (units + 7) / 8 * 8;
+    if (cio & 128) {
+      g.wn = 1;
+      g.na = 2 * (T - 1);
+      g.nr = (T - 1) * T;
+      g.a_done = ctr;
+      grid = (g.na + 7) / 8 * 8 + (g.nr + 7) / 8 * 8;
+    }
+    if (cio & 256) {
+      g.tw = 1;
+      g.tr0 = 512 + ST;
+      g.tk0 = 0;
+      g.nt = 2 * (T - 1);
+      g.Bd = ctx->A;
+      g.X = xs + xb / 8;
+      g.zvec = xs;
+      g.a_done = nullptr;
+      grid = (g.na + 7) / 8 * 8 + (g.nr + 7) / 8 * 8 + (g.nt + 7) / 8 * 8;
+    }
+    // unit-duration stamps in step slot 0 while lfm_debug_stamps is on (scripts/unit_time.py)
+    g.stamps = ctx->dbg_stamps ? ctx->dbg_stamps + 256 * 16 : nullptr;
+    hipLaunchKernelGGL(step_kernel, dim3(grid), dim3(256), 0, st, g);
+  } else if (cio & 2048) {
+    // 128 x 128 units (2 workgroups / CU, 64 x 64 per wave), the same triangle
+    hipLaunchKernelGGL((syrk_kernel<true, 128>), dim3(units / 2), dim3(256), 0, st, ctx->A, n,
+                       (int64_t)512, pan, kd, T, 0, T, 0, 1, 0, (int64_t)0);
+  } else if (cio & 1) {
+    hipLaunchKernelGGL((syrk_kernel<true, 64>), dim3(units), dim3(256), 0, st, ctx->A, n,
+                       (int64_t)512, pan, kd, T, 0, T, 0, 1, 0, (int64_t)0);
+  } else {
+    hipLaunchKernelGGL((syrk_kernel<false, 64>), dim3(units), dim3(256), 0, st, ctx->A, n,
+                       (int64_t)512, pan, kd, T, 0, T, 0, 1, 0, (int64_t)0);
+  }
+  return hip_fail(ctx, hipGetLastError(), "probe_update_launch");
 }
 
 bool chol_fuses_gram(const lfm_ctx* ctx, int mode, const GridLayout& lay, int64_t n) {
   return ctx->gram_fuse && lay.ok && lay.T % 256 == 0 && n % 256 == 0 && n >= 1024 &&
-         ctx->sched == 3 && ctx->side_cus > 0 && mode != CHOL_SCHUR;
+         s3_on(ctx) && mode != CHOL_SCHUR;
 }
 
 int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,
@@ -2181,7 +2111,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   if (r) return r;
   // schedule 3 for the MLL and for the bordered inverse (gradient); the Schur-complement
   // posterior keeps schedule 1
-  const bool s3 = ctx->sched == 3 && ctx->side_cus > 0 && mode != CHOL_SCHUR;
+  const bool s3 = s3_on(ctx) && mode != CHOL_SCHUR;
+  ctx->last_sched = s3 ? 3 : 1;
   // the bordered matrix's bottom rows [I, 0]: in memory for schedule 1; schedule 3 never reads
   // them before its window reaches them (StepArgs zero_from / copy_from)
   if (bordered && !s3) {
@@ -2485,7 +2416,22 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         // Side-CU helper (LFM_HELPER): while the factor chain has slack (long launches), the
         // side stream runs the tail of this step's rest units after chain(s + 1), sized so it
         // ends with the main launch; launch s + 1 waits for it, chain(s + 2) follows it.
-        const int64_t hu = s >= 1 && s + 2 < S ? helper_units(g, steps[s + 1].second) : 0;
+        int64_t hu = s >= 1 && s + 2 < S ? helper_units(g, steps[s + 1].second) : 0;
+        if (hu > 0) {
+          // The helper's units, the tail [nr - hu, nr) of the rest enumeration, store without
+          // write-through and bump no xready: none may be a lead tile of chain(s + 2) (tile rows
+          // < wn + lead). In the supertile order every unit of triangle rows < lead comes
+          // before the first unit of supertile row ceil(lead / Q), so cap the tail there.
+          const int Q = LFM_SUPERTILE > 1 ? LFM_SUPERTILE : 1;
+          const int64_t r0e = std::min<int64_t>((g.lead + Q - 1) / Q * Q, g.T - g.wn);
+          hu = std::min<int64_t>(hu, g.nr - 2 * r0e * (r0e + 1) / 2);
+          // (checked on the host mirror of the enumeration: no helper rather than a lead tile)
+          for (int64_t b = g.nr - std::max<int64_t>(hu, 0); b < g.nr; ++b) {
+            int ti, tj;
+            rest_unit_tile(b, g.T, g.wn, &ti, &tj);
+            if (ti / 2 < g.wn + g.lead && tj < g.wn + g.lead) hu = 0;
+          }
+        }
         if (helped) hipStreamWaitEvent(main, evH[2 * (s - 1)], 0);
         if (hu > 0) {
           g.nr -= (int)hu;

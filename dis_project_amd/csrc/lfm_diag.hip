@@ -1,7 +1,15 @@
-// lfm_probe.hip — diagnostics for the fp64 matrix-core path used by the Cholesky:
-// (1) the lane maps of v_mfma_f64_16x16x4_f64 (checked against a host product with an
-//     asymmetric B), (2) its sustained issue rate (TFLOP/s) with independent accumulators.
-#include "lfm_internal.h"
+// lfm_diag.hip — liblfm_diag.so, the diagnostics of include/lfm_diag.h, built apart from the
+// product library (liblfm.so, which it links against and whose contexts it takes):
+// (1) the lane maps of v_mfma_f64_16x16x4_f64 / 4x4x4_4b (checked against host products),
+// (2) their sustained issue rates (TFLOP/s) with independent accumulators, (3) the pivot
+// rsqrt, (4) the trailing-update kernel alone (through liblfm's launch hook), (5) phase stamps
+// of the schedule-3 factorisation, (6) the schedule-3 tenancy state. No product call path
+// loads this library.
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+#include "lfm_math.h"
 
 namespace lfm {
 
@@ -233,4 +241,173 @@ int probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double*
   return LFM_OK;
 }
 
+// Diagnostic: the pivot reciprocal square root of the diagonal factor (v_rsq_f64 + one
+// Newton step) over host values x[n] -> y[n] (tests bound its relative error).
+__global__ void rsq_probe_kernel(const double* x, double* y, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] = rsqrt_1nr(x[i]);
+}
+
+int probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y) {
+  double* d = nullptr;
+  hipError_t e = hipMalloc((void**)&d, 2 * n * sizeof(double));
+  if (e != hipSuccess) return hip_fail(ctx, e, "probe rsq");
+  hipMemcpyAsync(d, x, n * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipLaunchKernelGGL(rsq_probe_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream,
+                     d, d + n, n);
+  hipMemcpyAsync(y, d + n, n * 8, hipMemcpyDeviceToHost, ctx->stream);
+  e = hipStreamSynchronize(ctx->stream);
+  hipFree(d);
+  return hip_fail(ctx, e, "probe rsq");
+}
+
+// Pseudo-random doubles in [-1/32, 1/32) (probe data: MFMA power, hence clocks, depends on it).
+__global__ void fill_hash_kernel(double* a, int64_t cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) {
+    uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull;
+    h ^= h >> 31;
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 29;
+    a[i] = ((double)(h >> 11) * 0x1.0p-53 - 0.5) * 0.0625;
+  }
+}
+
+// Average duration (us) of one full-lower-triangle trailing-update launch over a T x T grid of
+// 128-tiles with update depth kd (the launch itself: probe_update_launch in liblfm, whose
+// comment lists the cio bits; bit 3 here: random operands, else zeros).
+int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
+  constexpr int64_t TILE = 128;
+  const int64_t n = (int64_t)T * TILE + 512;
+  const size_t xb = (cio & (512 | 256)) ? (size_t)n * 128 * 8 : 0;  // X_s / X_{s+1} slabs
+  int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * 8 + 2 * xb + 4096);
+  if (r) return r;
+  if (cio & 8)
+    hipLaunchKernelGGL(fill_hash_kernel, dim3(4096), dim3(256), 0, ctx->stream, ctx->A,
+                       n * n + 2 * (int64_t)(xb / 8));
+  else
+    hipMemsetAsync(ctx->A, 0, (size_t)n * n * 8 + 2 * xb, ctx->stream);
+  hipMemsetAsync(ctx->A + (size_t)n * n + 2 * (xb / 8), 0, 4096, ctx->stream);
+  hipStream_t st = (cio & 16) && ctx->m3 ? ctx->m3 : ctx->stream;
+  if (st != ctx->stream) {
+    hipEvent_t f;
+    hipEventCreate(&f);
+    hipEventRecord(f, ctx->stream);
+    hipStreamWaitEvent(st, f, 0);
+    hipEventDestroy(f);
+  }
+  r = probe_update_launch(ctx, st, T, kd, cio, n, xb);
+  if (r) return r;
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  hipEventRecord(a, st);
+  for (int i = 0; i < reps && !r; ++i) r = probe_update_launch(ctx, st, T, kd, cio, n, xb);
+  hipEventRecord(b, st);
+  hipError_t e = hipStreamSynchronize(st);
+  float ms = 0;
+  hipEventElapsedTime(&ms, a, b);
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  if (r) return r;
+  *us = ms * 1e3 / reps;
+  return hip_fail(ctx, e, "probe_syrk");
+}
+
 }  // namespace lfm
+
+using namespace lfm;
+
+namespace {
+struct DeviceGuard {
+  DeviceGuard(int dev) { hipSetDevice(dev); }
+};
+}  // namespace
+
+extern "C" {
+
+int lfm_probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y) {
+  if (!ctx || !x || !y || n < 1) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_rsq(ctx, x, n, y);
+}
+
+// enable = 1 turns on s_memrealtime (100 MHz) stamps of the schedule-3 chain kernel's phases
+// (16 per super-panel step, 256 steps) and of the step launches; enable = 0 copies them out
+// and turns them off. The product kernels write them only while ctx->dbg_stamps is set.
+int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max) {
+  if (!ctx) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  const size_t cnt = 256 * 24;  // 256 chain rows of 16, then 256 step-launch rows of 8
+  if (enable) {
+    if (!ctx->dbg_stamps) {
+      hipError_t e = hipMalloc((void**)&ctx->dbg_stamps, cnt * 8);
+      if (e != hipSuccess) return hip_fail(ctx, e, "debug stamps");
+    }
+    hipError_t e = hipMemsetAsync(ctx->dbg_stamps, 0, cnt * 8, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return hip_fail(ctx, e, "debug stamps");
+  }
+  if (!ctx->dbg_stamps) return LFM_OK;
+  hipError_t e = hipStreamSynchronize(ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(out, ctx->dbg_stamps, std::min<size_t>(cnt, (size_t)std::max(max, 0)) * 8,
+                       hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  hipFree(ctx->dbg_stamps);
+  ctx->dbg_stamps = nullptr;
+  return hip_fail(ctx, e, "debug stamps");
+}
+
+int lfm_debug_last_schedule(const lfm_ctx* ctx, int* out) {
+  if (!ctx || !out) return LFM_E_ARG;
+  *out = ctx->last_sched;
+  return LFM_OK;
+}
+
+int lfm_debug_lock_path(const lfm_ctx* ctx, char* buf, int len) {
+  if (!ctx || !buf || len < 1) return LFM_E_ARG;
+  const std::string p = tenancy_lock_path(ctx->device);
+  if ((int)p.size() + 1 > len) return LFM_E_ARG;
+  std::memcpy(buf, p.c_str(), p.size() + 1);
+  return LFM_OK;
+}
+
+int lfm_probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double* ms) {
+  if (!ctx || !tflops || !ms || nblocks < 1 || iters < 1) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_mfma_f64(ctx, nblocks, iters, tflops, ms);
+}
+
+int lfm_probe_mfma_f64_cycles(lfm_ctx* ctx, int nblocks, int iters, double* cyc_per_mfma,
+                              double* mhz) {
+  if (!ctx || !cyc_per_mfma || !mhz || nblocks < 1 || iters < 1) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_mfma_f64_cycles(ctx, nblocks, iters, cyc_per_mfma, mhz);
+}
+
+int lfm_probe_mfma4_layout(lfm_ctx* ctx, const double* a, const double* b, const double* c,
+                           double* d) {
+  if (!ctx || !a || !b || !c || !d) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_mfma4_layout(ctx, a, b, c, d);
+}
+
+int lfm_probe_rate(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflops) {
+  if (!ctx || !tflops || nblocks < 1 || iters < 1) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_rates(ctx, which, nblocks, iters, tflops);
+}
+
+int lfm_probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us) {
+  if (!ctx || !us || T < 1 || reps < 1 || kd < 16 || kd > 2048 || kd % 16) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_syrk(ctx, T, kd, cio, reps, us);
+}
+
+int lfm_probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d) {
+  if (!ctx || !a || !b || !d) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_mfma_f64_layout(ctx, a, b, d);
+}
+
+}  // extern "C"

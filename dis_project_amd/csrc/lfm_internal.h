@@ -84,6 +84,9 @@ struct lfm_ctx {
   unsigned panel_epoch = 0;                      // fused panel launches so far
   int side_cus = 0;                              // CUs reserved for the side stream (LFM_SIDE_CUS)
   int sched = 3;                                 // look-ahead schedule 1 or 3 (LFM_SCHED)
+  bool s3_yield = false;                         // this call runs schedule 1: another process
+                                                 // holds the device's schedule-3 tenancy
+  int last_sched = 0;                            // schedule the last factorisation ran (diag)
   bool s3_events = false;                        // schedule 3 ordered by events (LFM_S3_EVENTS)
   unsigned spin_limit = 1u << 26;                // device-side wait bound (LFM_DEBUG_SPIN_LIMIT)
   bool grad_direct = false;                      // gradient: per-pair path only (LFM_GRAD_DIRECT)
@@ -121,6 +124,12 @@ constexpr int STATUS_TIMEOUT = -2;
 // LFM_OK, LFM_E_NOT_PD (pivot index in the message) or LFM_E_TIMEOUT for a status word.
 int status_code(lfm_ctx* ctx, double st);
 
+// The next factorisation on ctx runs schedule 3 (the CU-partitioned pair exists, and the
+// call holds the device's schedule-3 tenancy: lfm_api.hip S3Tenancy).
+inline bool s3_on(const lfm_ctx* ctx) {
+  return ctx->sched == 3 && ctx->side_cus > 0 && !ctx->s3_yield;
+}
+
 int set_err(lfm_ctx* ctx, int code, const std::string& msg);
 int hip_fail(lfm_ctx* ctx, hipError_t e, const char* what);
 int ensure(lfm_ctx* ctx, void** p, size_t* cap, size_t bytes);
@@ -136,7 +145,6 @@ int prof_flush(lfm_ctx* ctx);
 
 GridLayout detect_grid(const double* x, int64_t n, int64_t G);
 int chain_coresident(lfm_ctx* ctx, hipStream_t st, int G, bool* good);
-int probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y);
 int gene_clamp_host(double g, int64_t G);
 
 // device-side gene index semantics: trunc toward zero, negative wraps, clamp
@@ -231,14 +239,13 @@ int launch_grad(lfm_ctx* ctx, const HypDev& h, const double* d_x, int64_t n, con
 int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn,
                        int negative, double* d_out, int* d_status);
 
-// diagnostics (lfm_probe.hip)
-int probe_mfma_f64(lfm_ctx* ctx, int nblocks, int iters, double* tflops, double* ms);
-int probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d);
-int probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us);
-int probe_mfma4_layout(lfm_ctx* ctx, const double* a, const double* b, const double* c,
-                       double* d);
-int probe_rates(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflops);
-int probe_mfma_f64_cycles(lfm_ctx* ctx, int nblocks, int iters, double* cyc_per_mfma,
-                          double* mhz);
+// Path of the advisory lock file behind schedule 3's cross-process tenancy (lfm_api.hip;
+// empty if the device has no PCI bus id)
+std::string tenancy_lock_path(int dev);
+
+// Hook of the diagnostics library (liblfm_diag.so, lfm_diag.hip): one launch of the
+// trailing-update kernel over a full triangle (lfm_chol.hip; launch only, no kernel of its own)
+int probe_update_launch(lfm_ctx* ctx, hipStream_t st, int T, int kd, int cio, int64_t n,
+                        size_t xb);
 
 }  // namespace lfm

@@ -83,4 +83,14 @@ __device__ __forceinline__ double mean_at(const HypDev& p, const double* x, int6
   return (p.B[g] / p.D[g]) * (double)flag_int(x[i * 3 + 2]);
 }
 
+// 1/sqrt(x): v_rsq_f64 estimate + one Newton step (a pivot and its inverse come from one
+// estimate instead of a correctly rounded sqrt followed by a divide). The pivot's relative
+// error stays far below the 1e-9 MLL tolerance (a perturbation of the pivot by a factor
+// (1 + e) is a backward error e in that column); tests/test_gpu_parity.py bounds it.
+__device__ __forceinline__ double rsqrt_1nr(double x) {
+  const double h = -0.5 * x;
+  const double y = __builtin_amdgcn_rsq(x);
+  return y * fma(h * y, y, 1.5);
+}
+
 }  // namespace lfm

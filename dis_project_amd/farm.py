@@ -84,7 +84,9 @@ class ResidentEvaluator:
     """MLL evaluations of many hyperparameter sets on ONE dataset held in HBM (the C3 random
     restarts; bench.py's C2 step): x / y are uploaded and their layout analysed once
     (``lfm_data_create``), each evaluation uploads only the 3G + 3 hyperparameters
-    (``lfm_mll_f64_data``). Not PD -> NaN (JAX semantics); a device-side timeout raises."""
+    (``lfm_mll_f64_data``). Not PD -> NaN (JAX semantics); a device-side timeout raises.
+    ``m.hyp()`` is read on every evaluation (microseconds beside a 29 ms MLL), so a model
+    whose fields change between calls is evaluated with its current values."""
 
     def __init__(self, ctx: _lib.Context, data, negative: bool = False):
         self.ctx, self.negative = ctx, bool(negative)
@@ -93,32 +95,38 @@ class ResidentEvaluator:
         y = np.ascontiguousarray(data.y, dtype=np.float64).reshape(-1)
         self.n = x.shape[0]
         self.dx, self.dy, self.data = _lib.c_void_p(), _lib.c_void_p(), _lib.c_void_p()
-        ctx.check(lib.lfm_dev_alloc(h, x.nbytes, _lib.ctypes.byref(self.dx)))
-        ctx.check(lib.lfm_dev_alloc(h, y.nbytes, _lib.ctypes.byref(self.dy)))
-        ctx.check(lib.lfm_memcpy_h2d(h, self.dx, x.ctypes.data, x.nbytes))
-        ctx.check(lib.lfm_memcpy_h2d(h, self.dy, y.ctypes.data, y.nbytes))
-        ctx.check(lib.lfm_data_create(h, self.dx, self.dy, self.n, _lib.ctypes.byref(self.data)))
-        self._hyps = {}
+        try:
+            ctx.check(lib.lfm_dev_alloc(h, x.nbytes, _lib.ctypes.byref(self.dx)))
+            ctx.check(lib.lfm_dev_alloc(h, y.nbytes, _lib.ctypes.byref(self.dy)))
+            ctx.check(lib.lfm_memcpy_h2d(h, self.dx, x.ctypes.data, x.nbytes))
+            ctx.check(lib.lfm_memcpy_h2d(h, self.dy, y.ctypes.data, y.nbytes))
+            ctx.check(lib.lfm_data_create(h, self.dx, self.dy, self.n,
+                                          _lib.ctypes.byref(self.data)))
+        except Exception:
+            self.close()
+            raise
         self._out = np.empty(1)
 
     def __call__(self, models) -> np.ndarray:
         vals = np.empty(len(models))
         for i, m in enumerate(models):
-            hp = self._hyps.get(id(m))
-            if hp is None:
-                hp = self._hyps[id(m)] = (m, m.hyp())  # keeps m alive: id() stays unique
-            rc = self.ctx.lib.lfm_mll_f64_data(self.ctx.handle, self.data, hp[1].ref,
+            hp = m.hyp()  # keeps the hyperparameter buffers alive through the call
+            rc = self.ctx.lib.lfm_mll_f64_data(self.ctx.handle, self.data, hp.ref,
                                                int(self.negative), _lib.dptr(self._out))
             self.ctx.check(rc, allow_not_pd=True)
             vals[i] = self._out[0]
         return vals
 
     def close(self):
+        lib, h = self.ctx.lib, self.ctx.handle
         if self.data:
-            self.ctx.lib.lfm_data_destroy(self.data)
-            self.ctx.lib.lfm_dev_free(self.ctx.handle, self.dx)
-            self.ctx.lib.lfm_dev_free(self.ctx.handle, self.dy)
+            lib.lfm_data_destroy(self.data)
             self.data = None
+        for p in ("dx", "dy"):
+            ptr = getattr(self, p, None)
+            if ptr:
+                lib.lfm_dev_free(h, ptr)
+                setattr(self, p, None)
 
 
 def workload(kind: str, genes: int = 64, timepoints: int = 256, restarts: int = 32):
@@ -179,58 +187,99 @@ class Farm:
                                                           [datasets[i] for i in idx]))
 
 
+# Measured C3 throughput on one MI355X at N = 16384, evaluations / s with c
+# schedule-1 evaluations in flight, and one schedule-3 evaluation at a time
+_S1_RATE = {1: 29.1, 2: 35.8, 3: 37.3, 4: 37.0}
+_S3_RATE = 34.6
+
+
+def predicted_seconds(k: int, workers: int) -> float:
+    """Model of a rank's wall time for k restarts with ``workers`` in flight (shared counter:
+    full rounds of ``workers`` at the concurrent rate, then the remainder at its own)."""
+    if k <= 0:
+        return 0.0
+    if workers <= 1:
+        return k / _S3_RATE
+    full, rem = divmod(k, workers)
+    t = full * workers / _S1_RATE[min(workers, 4)]
+    return t + (rem / _S1_RATE[rem] if rem else 0.0)
+
+
+def choose_workers(k: int, max_workers: int = 4) -> int:
+    """Evaluations in flight for a rank that owns k restarts of one large dataset: the count
+    with the shortest predicted wall time (ties: fewer contexts). 32 -> 3, 16 / 8 / 4 -> 4 (so
+    the 8-GPU split's 4 restarts per rank run as one round of 4, not 3 then 1)."""
+    best = 1
+    for w in range(2, max(1, min(max_workers, k)) + 1):
+        if predicted_seconds(k, w) < predicted_seconds(k, best) - 1e-9:
+            best = w
+    return best
+
+
 class ConcurrentEvaluator:
     """Restart-farm throughput on one GPU (C3): ``workers`` contexts on factorisation schedule 1
     (look-ahead on every CU, include/lfm.h ``lfm_ctx_set_schedule``), each with its own HIP
     streams, workspace and resident copy of x / y, each driven by its own host thread (ctypes
     releases the GIL inside the library calls), pulling the next hyperparameter set from a
     shared counter. Several evaluations in flight fill the bubbles one evaluation's chain-bound
-    tail leaves on the chip (35-36 evals/s with 2-3 workers against 33.1 for one
+    tail leaves on the chip (36-37 evals/s with 3-4 workers against 34.6 for one
     schedule-3 evaluation at a time).
 
     Worker 0 is the caller's context, switched to schedule 1 for the evaluator's lifetime and
-    restored by ``close()``: a schedule-3 context holds two CU-masked hardware queues even when
-    idle, and idle queues beside the workers oversubscribe the hardware scheduler (measured
-    -3 % with one, -10 % with two partitioned contexts idle). Schedule 3 itself is single tenant
-    -- two schedule-3 evaluations at once starve each other's co-resident factor chains -- so
-    the workers never use it. Results are per model and independent of which worker ran it
-    (schedule 1 is deterministic); not PD -> NaN, a device-side timeout raises in the caller."""
+    restored by ``close()`` (also when construction fails part-way): a schedule-3 context holds
+    two CU-masked hardware queues even when idle, and idle queues beside the workers
+    oversubscribe the hardware scheduler (measured -3 % with one, -10 % with two partitioned
+    contexts idle). Results are per model and independent of which worker ran it (schedule 1
+    is deterministic); not PD -> NaN. A worker's exception (e.g. LFM_E_TIMEOUT) stops the
+    others at their next pull, and is re-raised in the caller once every worker has returned,
+    so no worker thread outlives the call on these non-thread-safe contexts."""
 
     def __init__(self, ctx: _lib.Context, data, negative: bool = False, workers: int = 3):
         self.ctx, self._restore = ctx, ctx.schedule
-        ctx.schedule = 1
-        self.own = [_lib.Context(ctx.device) for _ in range(max(1, int(workers)) - 1)]
-        for c in self.own:
-            c.schedule = 1
-        self.evs = [ResidentEvaluator(c, data, negative) for c in [ctx] + self.own]
-        self.pool = cf.ThreadPoolExecutor(max_workers=len(self.evs),
-                                          thread_name_prefix="lfm-worker")
+        self.own, self.evs, self.pool = [], [], None
+        try:
+            ctx.schedule = 1
+            for _ in range(max(1, int(workers)) - 1):
+                c = _lib.Context(ctx.device)
+                self.own.append(c)
+                c.schedule = 1
+            for c in [ctx] + self.own:
+                self.evs.append(ResidentEvaluator(c, data, negative))
+            self.pool = cf.ThreadPoolExecutor(max_workers=len(self.evs),
+                                              thread_name_prefix="lfm-worker")
+        except BaseException:
+            self._release()
+            raise
 
     def __call__(self, models) -> np.ndarray:
         models = list(models)
         if len(models) < 2:
             return self.evs[0](models)
         vals = np.empty(len(models))
-        counter, lock = itertools.count(), threading.Lock()
+        counter, lock, stop = itertools.count(), threading.Lock(), threading.Event()
 
         def work(ev):
-            while True:
+            while not stop.is_set():
                 with lock:
                     i = next(counter)
                 if i >= len(models):
                     return
-                vals[i] = ev([models[i]])[0]
+                try:
+                    vals[i] = ev([models[i]])[0]
+                except BaseException:
+                    stop.set()
+                    raise
 
         futs = [self.pool.submit(work, ev) for ev in self.evs]
+        cf.wait(futs)  # every worker has returned before anything is re-raised
         for f in futs:
-            f.result()  # re-raises a worker's LfmError here
+            f.result()  # re-raises the first worker's exception here
         return vals
 
-    def close(self):
-        if self.pool is None:
-            return
-        self.pool.shutdown(wait=True)
-        self.pool = None
+    def _release(self):
+        if self.pool is not None:
+            self.pool.shutdown(wait=True)
+            self.pool = None
         for ev in self.evs:
             ev.close()
         for c in self.own:
@@ -238,16 +287,24 @@ class ConcurrentEvaluator:
         self.evs, self.own = [], []
         self.ctx.schedule = self._restore
 
+    def close(self):
+        if self.pool is None and not self.evs and not self.own:
+            return
+        self._release()
+
 
 def gpu_evaluator(ctx: _lib.Context, datasets, negative: bool = False, workers: int = 3):
     """The product evaluator of a farm round on this rank's GPU: problems sharing one large
     dataset go through a ConcurrentEvaluator (x / y in HBM once per worker context, ``workers``
-    evaluations in flight; workers = 1: one ResidentEvaluator on ``ctx``); small ones through
-    one batched launch (``CustomConjMLL.batch``: one workgroup per problem, n <= 128)."""
+    evaluations in flight; workers = 1: one ResidentEvaluator on ``ctx``, schedule 3;
+    workers = 0: ``choose_workers`` for this rank's share); small ones through one batched
+    launch (``CustomConjMLL.batch``: one workgroup per problem, n <= 128)."""
     from .objectives import CustomConjMLL
 
     shared = len({id(d) for d in datasets}) == 1 and datasets[0].n > 128
     if shared:
+        if workers <= 0:
+            workers = choose_workers(len(datasets))
         if workers > 1:
             res = ConcurrentEvaluator(ctx, datasets[0], negative, workers)
         else:

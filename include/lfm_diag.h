@@ -1,10 +1,13 @@
 /*
- * lfm_diag.h — diagnostics of liblfm.so, kept out of the product ABI (include/lfm.h).
+ * lfm_diag.h — diagnostics, exported by liblfm_diag.so (dis_project_amd/csrc/lfm_diag.hip),
+ * a library of its own beside the product liblfm.so (include/lfm.h), which it links against
+ * and whose contexts it takes.
  *
- * Hardware probes (MFMA lane maps and issue rates, the trailing-update kernel alone) and
- * phase timestamps of the schedule-3 factor chain. They back the measurements quoted in
- * DESIGN.md and the layout / pivot known-answer tests; no product call path uses them.
- * Same conventions as lfm.h (LFM_OK / LFM_E_* return codes, synchronous at return).
+ * Hardware probes (MFMA lane maps and issue rates, the trailing-update kernel alone), phase
+ * timestamps of the schedule-3 factor chain and the schedule-3 tenancy state. They back the
+ * measurements quoted in DESIGN.md and the layout / pivot / tenancy tests; no product call
+ * path loads this library. Same conventions as lfm.h (LFM_OK / LFM_E_* return codes,
+ * synchronous at return).
  */
 #ifndef LFM_DIAG_H
 #define LFM_DIAG_H
@@ -26,6 +29,13 @@ extern "C" {
  * is [4] / [5] x 100 MHz. enable = 1 arms them; enable = 0 copies up to max (<= 256 * 24)
  * values out and disarms. */
 int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max);
+
+/* The schedule (1 or 3) the context's last factorisation ran; 0 before the first. A schedule-3
+ * context runs schedule 1 for a call while another process holds the device's tenancy lock. */
+int lfm_debug_last_schedule(const lfm_ctx* ctx, int* out);
+
+/* The advisory lock file of the context's device (schedule-3 tenancy across processes). */
+int lfm_debug_lock_path(const lfm_ctx* ctx, char* buf, int len);
 
 /* The diagonal factor's pivot reciprocal square root (v_rsq_f64 + one Newton step) on x[n]. */
 int lfm_probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y);
@@ -53,7 +63,8 @@ int lfm_probe_rate(lfm_ctx* ctx, int which, int nblocks, int iters, double* tflo
 
 /* The trailing-update kernel alone (64-row slabs) on a T x T grid of 128-tiles, depth kd:
  * average us per launch. cio bit 0: C tile I/O (else MFMAs only), bit 3: random operands,
- * bit 4: on schedule 3's CU-masked bulk stream. */
+ * bit 4: on schedule 3's CU-masked bulk stream, bit 6: the step kernel's rest role (the other
+ * bits: lfm_chol.hip probe_update_launch). */
 int lfm_probe_syrk(lfm_ctx* ctx, int T, int kd, int cio, int reps, double* us);
 
 #ifdef __cplusplus

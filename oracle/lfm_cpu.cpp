@@ -274,6 +274,30 @@ int lfm_cpu_gram(const double* x, int64_t n, int64_t G, const double* D, const d
   return 0;
 }
 
+// Sampled rows of the lower triangle: out[q * n + j] = K(x[rows[q]], x[j]) + diag_add [j ==
+// rows[q]] for j <= rows[q] (fp64 arithmetic, stored as float: bench.py's C4 CPU baseline,
+// the reference formula on a bounded sample of the fp32 fill's rows); j > rows[q] untouched.
+int lfm_cpu_gram_rows_f32(const double* x, int64_t n, int64_t G, const double* D, const double* S,
+                          double l, double diag_add, const int64_t* rows, int64_t nrows,
+                          float* out, int threads) {
+  if (!x || !D || !S || !rows || !out || n < 1 || G < 1 || nrows < 0) return 1;
+  for (int64_t q = 0; q < nrows; ++q)
+    if (rows[q] < 0 || rows[q] >= n) return 1;
+  if (threads > 0) omp_set_num_threads(threads);
+  const Hyp p{D, S, G, l};
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int64_t q = 0; q < nrows; ++q) {
+    const int64_t i = rows[q];
+    float* o = out + q * n;
+    for (int64_t j = 0; j <= i; ++j) {
+      double v = kernel(p, x + 3 * i, x + 3 * j);
+      if (i == j) v = v + diag_add;
+      o[j] = (float)v;
+    }
+  }
+  return 0;
+}
+
 // In-place lower Cholesky of the leading n x n of A; returns -1 or the first failing pivot.
 int64_t lfm_cpu_potrf(double* A, int64_t n, int64_t lda, int threads) {
   if (threads > 0) omp_set_num_threads(threads);

@@ -29,6 +29,10 @@ def load():
         lib.lfm_cpu_gram.restype = c_int
         lib.lfm_cpu_gram.argtypes = [_dp, c_int64, c_int64, _dp, _dp, c_double, c_double, _dp,
                                      c_int64, c_int]
+        lib.lfm_cpu_gram_rows_f32.restype = c_int
+        lib.lfm_cpu_gram_rows_f32.argtypes = [_dp, c_int64, c_int64, _dp, _dp, c_double,
+                                              c_double, POINTER(c_int64), c_int64,
+                                              POINTER(ctypes.c_float), c_int]
         lib.lfm_cpu_potrf.restype = c_int64
         lib.lfm_cpu_potrf.argtypes = [_dp, c_int64, c_int64, c_int]
         lib.lfm_cpu_mll.restype = c_double
@@ -78,6 +82,23 @@ def gram_lower(x, D, S, l, diag_add=0.0, threads=0):
     if rc:
         raise ValueError("lfm_cpu_gram: bad arguments")
     return K
+
+
+def gram_rows_f32(x, D, S, l, rows, diag_add=0.0, threads=0):
+    """Rows `rows` of the lower triangle of K(x, x) + diag_add I in fp64 arithmetic, stored as
+    float32 [len(rows), n] (entries above the diagonal zero)."""
+    lib = load()
+    x, D, S = (_f64(v) for v in (x, D, S))
+    x = x.reshape(-1, 3)
+    n = x.shape[0]
+    rows = np.ascontiguousarray(np.asarray(rows, np.int64))
+    out = np.zeros((rows.size, n), np.float32)
+    rc = lib.lfm_cpu_gram_rows_f32(_p(x), n, D.size, _p(D), _p(S), float(l), float(diag_add),
+                                   rows.ctypes.data_as(POINTER(c_int64)), rows.size,
+                                   out.ctypes.data_as(POINTER(ctypes.c_float)), int(threads))
+    if rc:
+        raise ValueError("lfm_cpu_gram_rows_f32: bad arguments")
+    return out
 
 
 def potrf(A, threads=0):

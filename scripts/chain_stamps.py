@@ -24,10 +24,10 @@ out = np.empty(1)
 hp = work.model.hyp()
 for _ in range(3):
     ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, x.shape[0], hp.ref, 0, _lib.dptr(out)))
-ctx.check(lib.lfm_debug_stamps(h, 1, None, 0))
+ctx.check(ctx.diag.lfm_debug_stamps(h, 1, None, 0))
 ctx.check(lib.lfm_mll_f64_dev(h, dx, dy, x.shape[0], hp.ref, 0, _lib.dptr(out)))
 buf = (ctypes.c_ulonglong * (256 * 24))()
-ctx.check(lib.lfm_debug_stamps(h, 0, buf, 256 * 24))
+ctx.check(ctx.diag.lfm_debug_stamps(h, 0, buf, 256 * 24))
 st = np.frombuffer(buf, dtype=np.uint64)[:256 * 16].reshape(256, 16).astype(np.int64)
 for s in range(256):
     row = st[s]

@@ -15,6 +15,6 @@ reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
 T = int(os.environ.get("PMC_T", "126"))
 kd = int(os.environ.get("PMC_KD", "512"))
 cio = int(os.environ.get("PMC_CIO", "9"))
-ctx.check(ctx.lib.lfm_probe_syrk(ctx.handle, T, kd, cio, reps, _lib.ctypes.byref(us)))
+ctx.check(ctx.diag.lfm_probe_syrk(ctx.handle, T, kd, cio, reps, _lib.ctypes.byref(us)))
 print(f"T {T} kd {kd} cio {cio}: us/launch {us.value:.1f}  TF/s "
       f"{T * (T + 1) / 2 * 128 * 128 * kd * 2 / (us.value * 1e-6) / 1e12:.2f}")

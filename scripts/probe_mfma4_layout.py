@@ -14,7 +14,7 @@ ctx = _lib.get_context(0)
 def run(a, b, c):
     a, b, c = (np.ascontiguousarray(v, dtype=np.float64) for v in (a, b, c))
     d = np.empty(5 * 64)
-    ctx.check(ctx.lib.lfm_probe_mfma4_layout(ctx.handle, _lib.dptr(a), _lib.dptr(b), _lib.dptr(c),
+    ctx.check(ctx.diag.lfm_probe_mfma4_layout(ctx.handle, _lib.dptr(a), _lib.dptr(b), _lib.dptr(c),
                                              _lib.dptr(d)))
     return d.reshape(5, 64)
 

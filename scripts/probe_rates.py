@@ -15,6 +15,6 @@ for rep in range(2):
     for which in (2, 3):
         for nblocks in (256, 512, 1024):
             tf = _lib.c_double()
-            ctx.check(ctx.lib.lfm_probe_rate(ctx.handle, which, nblocks, 4000, _lib.ctypes.byref(tf)))
+            ctx.check(ctx.diag.lfm_probe_rate(ctx.handle, which, nblocks, 4000, _lib.ctypes.byref(tf)))
             print(json.dumps({"probe": names[which], "blocks": nblocks, "tflops": round(tf.value, 2)}),
                   flush=True)

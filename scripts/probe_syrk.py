@@ -16,7 +16,7 @@ for T in TS:
     for kd in KDS:
         for cio in CIOS:
             us = _lib.c_double()
-            ctx.check(ctx.lib.lfm_probe_syrk(ctx.handle, T, kd, cio, 5, _lib.ctypes.byref(us)))
+            ctx.check(ctx.diag.lfm_probe_syrk(ctx.handle, T, kd, cio, 5, _lib.ctypes.byref(us)))
             tiles = T * (T + 1) // 2  # 128-tiles (two 64-row slabs each)
             tf = tiles * 128 * 128 * kd * 2 / (us.value * 1e-6) / 1e12
             print(json.dumps({"T": T, "kd": kd, "c_io": cio, "us": round(us.value, 1),

@@ -76,12 +76,12 @@ def main():
     for _ in range(5):
         run()
     plain_ms = (time.perf_counter() - t0) / 5 * 1e3
-    ctx.check(lib.lfm_debug_stamps(h, 1, None, 0))
+    ctx.check(ctx.diag.lfm_debug_stamps(h, 1, None, 0))
     t0 = time.perf_counter()
     run()
     stamped_ms = (time.perf_counter() - t0) * 1e3
     buf = (ctypes.c_ulonglong * (256 * 24))()
-    ctx.check(lib.lfm_debug_stamps(h, 0, buf, 256 * 24))
+    ctx.check(ctx.diag.lfm_debug_stamps(h, 0, buf, 256 * 24))
     allst = np.frombuffer(buf, dtype=np.uint64)
     ch = allst[: 256 * 16].reshape(256, 16).astype(np.int64)
     sp = allst[256 * 16:].reshape(256, 8).copy()

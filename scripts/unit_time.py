@@ -21,11 +21,11 @@ def main():
     for T in [int(v) for v in os.environ.get("PROBE_T", "35").split(",")]:
         for kd in [int(v) for v in os.environ.get("PROBE_KD", "128").split(",")]:
             for cio in [int(v) for v in os.environ.get("PROBE_CIO", "88,984").split(",")]:
-                ctx.check(ctx.lib.lfm_debug_stamps(ctx.handle, 1, None, 0))
+                ctx.check(ctx.diag.lfm_debug_stamps(ctx.handle, 1, None, 0))
                 us = ctypes.c_double(0)
-                ctx.check(ctx.lib.lfm_probe_syrk(ctx.handle, T, kd, cio, REPS, ctypes.byref(us)))
+                ctx.check(ctx.diag.lfm_probe_syrk(ctx.handle, T, kd, cio, REPS, ctypes.byref(us)))
                 buf = (ctypes.c_ulonglong * (256 * 24))()
-                ctx.check(ctx.lib.lfm_debug_stamps(ctx.handle, 0, buf, 256 * 24))
+                ctx.check(ctx.diag.lfm_debug_stamps(ctx.handle, 0, buf, 256 * 24))
                 sp = np.frombuffer(buf, dtype=np.uint64)[256 * 16:].reshape(256, 8)
                 nr = (T - 1) * T if cio & 128 else T * (T + 1)
                 unit = float(sp[0][5]) * 0.01 / ((REPS + 1) * nr)

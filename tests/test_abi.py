@@ -1,5 +1,6 @@
 """CPU checks of the drop-in boundary: liblfm.so loads, exports exactly what
-include/lfm.h declares, and fails loudly (no CPU fallback) without a GPU."""
+include/lfm.h declares, and fails loudly (no CPU fallback) without a GPU; the diagnostics of
+include/lfm_diag.h live in liblfm_diag.so and nowhere in the product library."""
 
 import ctypes
 import os
@@ -27,8 +28,9 @@ def test_library_builds_and_loads():
 @pytest.mark.parametrize("header,sigs", [("lfm.h", "PRODUCT_SIGNATURES"),
                                          ("lfm_diag.h", "DIAG_SIGNATURES")])
 def test_every_header_symbol_is_exported_and_bound(header, sigs):
-    """lfm.h declares the product ABI only; the probes and stamps live in lfm_diag.h."""
-    lib = _lib.load_library()
+    """lfm.h declares the product ABI only; the probes and stamps live in lfm_diag.h, exported
+    by liblfm_diag.so."""
+    lib = _lib.load_library() if header == "lfm.h" else _lib.load_diag()
     declared = header_functions(header)
     bound = {name for name, _, _ in getattr(_lib, sigs)}
     for name in declared:
@@ -42,8 +44,15 @@ def test_every_header_symbol_is_exported_and_bound(header, sigs):
 
 def test_exports_are_c_symbols():
     out = os.popen(f"nm -D --defined-only {_lib.LIB_PATH}").read()
-    for name in header_functions() + header_functions("lfm_diag.h"):
+    for name in header_functions():
         assert re.search(rf"\bT {name}$", out, re.M), f"{name} is not an extern \"C\" symbol"
+    diag = os.popen(f"nm -D --defined-only {_lib.DIAG_PATH}").read()
+    for name in header_functions("lfm_diag.h"):
+        assert re.search(rf"\bT {name}$", diag, re.M), f"{name} is not exported by liblfm_diag.so"
+        # the product library carries no diagnostic entry point (and no probe kernel)
+        assert not re.search(rf"\b{name}$", out, re.M), f"{name} is in the product liblfm.so"
+    for kernel in ("rsq_probe_kernel", "fill_hash_kernel", "mfma_rate_kernel"):
+        assert kernel not in out and kernel not in os.popen(f"nm {_lib.LIB_PATH}").read()
 
 
 def test_struct_layouts_match_header():

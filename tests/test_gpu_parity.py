@@ -49,7 +49,7 @@ def test_mfma_f64_layout(lfm):
     b = rng.integers(-4, 5, (4, 16)).astype(np.float64) + np.arange(16) * 0.5
     d = np.empty((16, 16))
     ctx = get_context()
-    ctx.check(ctx.lib.lfm_probe_mfma_f64_layout(ctx.handle, dptr(a), dptr(b), dptr(d)))
+    ctx.check(ctx.diag.lfm_probe_mfma_f64_layout(ctx.handle, dptr(a), dptr(b), dptr(d)))
     np.testing.assert_array_equal(d, a @ b)
 
 
@@ -65,7 +65,7 @@ def test_mfma4_layout(lfm):
     a, b, c = (rng.integers(-4, 5, 64).astype(np.float64) for _ in range(3))
     d = np.empty(5 * 64)
     ctx = get_context()
-    ctx.check(ctx.lib.lfm_probe_mfma4_layout(ctx.handle, dptr(a), dptr(b), dptr(c), dptr(d)))
+    ctx.check(ctx.diag.lfm_probe_mfma4_layout(ctx.handle, dptr(a), dptr(b), dptr(c), dptr(d)))
     d = d.reshape(5, 64)
     for g in range(4):
         A = np.array([[a[16 * k + 4 * g + i] for k in range(4)] for i in range(4)])
@@ -297,7 +297,7 @@ def test_pivot_rsqrt_one_newton_step(lfm):
                         np.array([1.0, 2.0, 1e-300, 1e300])])
     y = np.empty_like(x)
     ctx = _lib.get_context(0)
-    ctx.check(ctx.lib.lfm_probe_rsq(ctx.handle, x.ctypes.data, x.size, y.ctypes.data))
+    ctx.check(ctx.diag.lfm_probe_rsq(ctx.handle, x.ctypes.data, x.size, y.ctypes.data))
     ref = 1.0 / np.sqrt(x)
     rel = np.abs(y - ref) / ref
     assert rel.max() <= 1e-14, rel.max()
