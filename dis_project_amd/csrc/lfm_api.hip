@@ -148,41 +148,6 @@ int prof_flush(lfm_ctx* ctx) {
 // -------------------------------------------------------- layout detect
 int gene_clamp_host(double g, int64_t G) { return gene_index(g, (int)G); }
 
-GridLayout detect_grid(const double* x, int64_t n, int64_t G) {
-  GridLayout L;
-  if (n < 1 || G < 1 || n > INT_MAX) return L;
-  const int g0 = gene_index(x[1], (int)G);
-  int64_t T = 1;
-  while (T < n && gene_index(x[3 * T + 1], (int)G) == g0) ++T;
-  if (n % T != 0) return L;
-  const int64_t nblk = n / T;
-  L.times.resize(T);
-  for (int64_t t = 0; t < T; ++t) L.times[t] = x[3 * t];
-  L.block_gene.resize(nblk);
-  for (int64_t b = 0; b < nblk; ++b) {
-    const int gb = gene_index(x[3 * b * T + 1], (int)G);
-    L.block_gene[b] = gb;
-    for (int64_t t = 0; t < T; ++t) {
-      const double* r = x + 3 * (b * T + t);
-      if (r[2] != 1.0) return L;                        // all rows gene rows (flag 1)
-      if (gene_index(r[1], (int)G) != gb) return L;     // one gene per block
-      if (std::memcmp(&r[0], &L.times[t], sizeof(double)) != 0) return L;  // shared times
-    }
-  }
-  const double t0 = L.times[0];
-  const double dt = T > 1 ? (L.times[T - 1] - t0) / (double)(T - 1) : 0.0;
-  double scale = 1.0;
-  for (double t : L.times) scale = std::max(scale, std::fabs(t));
-  for (int64_t t = 0; t < T; ++t)
-    if (!(std::fabs(L.times[t] - (t0 + (double)t * dt)) <= 1e-12 * scale)) return L;
-  L.T = (int)T;
-  L.nblk = (int)nblk;
-  L.t0 = t0;
-  L.dt = dt;
-  L.ok = true;
-  return L;
-}
-
 }  // namespace lfm
 
 // ------------------------------------------------------------- staging

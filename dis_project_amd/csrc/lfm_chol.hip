@@ -1963,43 +1963,6 @@ struct Launcher {
   }
 };
 
-// Host mirror of syrk_unit's triangle enumeration (TR = 64, tile columns [tj_lo, T)): unit b ->
-// (64-row slab index ti, 128-column tile index tj) relative to the trailing matrix. Used only
-// to price the side-CU helper's share of a step's algorithmic flops.
-void rest_unit_tile(int64_t b, int T, int tj_lo, int* ti_out, int* tj_out) {
-  constexpr int SUB = 2, Q = LFM_SUPERTILE;
-  const int sub = (int)(b % SUB);
-  b /= SUB;
-  int a = (int)((std::sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
-  while ((int64_t)(a + 1) * (a + 2) / 2 <= b) ++a;
-  while ((int64_t)a * (a + 1) / 2 > b) --a;
-  int tj, ti;
-  if (Q > 1) {
-    const int R = a / Q, r0 = R * Q, qr = std::min(Q, T - tj_lo - r0);
-    const int64_t off = b - (int64_t)r0 * (r0 + 1) / 2;
-    const int64_t full = (int64_t)R * qr * Q;
-    int lr, lc;
-    if (off < full) {
-      const int C = (int)(off / (qr * Q)), t = (int)(off % (qr * Q));
-      lr = t / Q;
-      lc = C * Q + t % Q;
-    } else {
-      const int d = (int)(off - full);
-      lr = (int)((std::sqrt(8.0 * (double)d + 1.0) - 1.0) * 0.5);
-      while ((lr + 1) * (lr + 2) / 2 <= d) ++lr;
-      while (lr * (lr + 1) / 2 > d) --lr;
-      lc = r0 + d - lr * (lr + 1) / 2;
-    }
-    tj = lc + tj_lo;
-    ti = SUB * (r0 + lr + tj_lo) + sub;
-  } else {
-    tj = (int)(b - (int64_t)a * (a + 1) / 2) + tj_lo;
-    ti = SUB * (a + tj_lo) + sub;
-  }
-  *ti_out = ti;
-  *tj_out = tj;
-}
-
 int env_int(const char* name, int def) {
   const char* v = std::getenv(name);
   return v ? std::atoi(v) : def;
@@ -2132,19 +2095,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   // and 896 were slower, 1024 much slower); the bordered gradient keeps 4 (5 measured equal)
   const int wbulk = s3 ? (bordered ? LFM_WBORD : LFM_WBULK) : 4;
   const int64_t w2min = env_int("LFM_W2_MIN", s3 ? 5120 : 4096);
-  std::vector<std::pair<int64_t, int>> steps;
-  for (int64_t k = 0; k < nblk;) {
-    const int64_t m = bordered ? Mp + NB : Mp - k * NB;
-    int w = 1;
-    // the first bulk super-panel stays 4 wide: its chain runs beside the shallow first update
-    const int wk = steps.size() == 1 ? 4 : wbulk;
-    if (m >= w4min && k + wk <= nblk) w = wk;
-    else if (m >= w4min && k + 4 <= nblk) w = 4;
-    else if (m >= w2min && k + 2 <= nblk) w = 2;
-    if (k == 0 && s3) w = 1;
-    steps.emplace_back(k, w);
-    k += w;
-  }
+  const std::vector<std::pair<int64_t, int>> steps =
+      plan_steps(nblk, Mp, NB, bordered, s3, wbulk, w4min, w2min);
   const int S = (int)steps.size();
   r = ensure_events(ctx, 2 * (size_t)S + 3);
   if (r) return r;
@@ -2342,17 +2294,10 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     const int helper_on = mode == CHOL_MLL || bordered ? (int)env_int("LFM_HELPER", 1) : 0;
     const double helper_tc = env_int("LFM_HELPER_TC", 700);    // chain(s + 1) + margin, us
     const double helper_min = env_int("LFM_HELPER_MIN", 1200);  // smallest D0 helped, us
-    auto helper_units = [&](const StepArgs& g, int wnext) -> int64_t {
+    auto helper_share = [&](const StepArgs& g, int wnext) -> int64_t {
       if (!helper_on) return 0;
-      const double t = 154.0 * g.kd / 640.0 + 4.0;  // one depth-kd unit, us (step timeline)
-      const double o = 0.9;
-      const double sm = 4.0 * (ctx->cus - ctx->side_cus), sh = 4.0 * ctx->side_cus;
-      const double tall_eq = (double)g.nt * (wnext + 1) / 2.0 * NB / g.kd;
-      const double units = g.na + g.nr + tall_eq;
-      const double d0 = units * t / (sm * o);
-      if (d0 < helper_min) return 0;
-      const double x = o * (d0 - helper_tc) / (t * (1.0 / sh + 1.0 / sm));
-      return std::max<int64_t>(0, std::min<int64_t>((int64_t)x, g.nr / 2));
+      return helper_units(g.kd, g.na, g.nr, g.nt, wnext, NB, ctx->cus, ctx->side_cus, helper_tc,
+                          helper_min);
     };
     // side: chain(0) after the gram; every later chain(s) follows chain(s - 1) in stream order
     // and waits on the device for its inputs (xready[s]) from the main launch in flight
@@ -2416,22 +2361,12 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         // Side-CU helper (LFM_HELPER): while the factor chain has slack (long launches), the
         // side stream runs the tail of this step's rest units after chain(s + 1), sized so it
         // ends with the main launch; launch s + 1 waits for it, chain(s + 2) follows it.
-        int64_t hu = s >= 1 && s + 2 < S ? helper_units(g, steps[s + 1].second) : 0;
-        if (hu > 0) {
-          // The helper's units, the tail [nr - hu, nr) of the rest enumeration, store without
-          // write-through and bump no xready: none may be a lead tile of chain(s + 2) (tile rows
-          // < wn + lead). In the supertile order every unit of triangle rows < lead comes
-          // before the first unit of supertile row ceil(lead / Q), so cap the tail there.
-          const int Q = LFM_SUPERTILE > 1 ? LFM_SUPERTILE : 1;
-          const int64_t r0e = std::min<int64_t>((g.lead + Q - 1) / Q * Q, g.T - g.wn);
-          hu = std::min<int64_t>(hu, g.nr - 2 * r0e * (r0e + 1) / 2);
-          // (checked on the host mirror of the enumeration: no helper rather than a lead tile)
-          for (int64_t b = g.nr - std::max<int64_t>(hu, 0); b < g.nr; ++b) {
-            int ti, tj;
-            rest_unit_tile(b, g.T, g.wn, &ti, &tj);
-            if (ti / 2 < g.wn + g.lead && tj < g.wn + g.lead) hu = 0;
-          }
-        }
+        // the helper's units (the tail of the rest enumeration) store without write-through and
+        // bump no xready, so they never include a lead tile of chain(s + 2)
+        const int64_t hu = s >= 1 && s + 2 < S
+                               ? helper_clamp(helper_share(g, steps[s + 1].second), g.nr, g.T,
+                                              g.wn, g.lead, LFM_SUPERTILE)
+                               : 0;
         if (helped) hipStreamWaitEvent(main, evH[2 * (s - 1)], 0);
         if (hu > 0) {
           g.nr -= (int)hu;
@@ -2441,7 +2376,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
           if (ctx->prof) {
             for (int64_t b = g.nr; b < g.nr + hu; ++b) {
               int ti, tj;
-              rest_unit_tile(b, g.T, g.wn, &ti, &tj);
+              rest_unit_tile(b, g.T, g.wn, LFM_SUPERTILE, &ti, &tj);
               const int64_t i0 = g.s0 + (int64_t)ti * 64, j0 = g.s0 + (int64_t)tj * ST;
               // bordered: the whole window is algorithmic; MLL: rows past n are padding
               for (int64_t r = i0; r < i0 + 64 && (bordered || r <= n); ++r)

@@ -1,0 +1,127 @@
+// lfm_host.cpp — host-only logic of liblfm (lfm_host.h): plain C++, compiled into liblfm.so and
+// into the host sanitizer check (tests/native/host_check.cpp).
+#include "lfm_host.h"
+
+#include <algorithm>
+#include <climits>
+#include <cstring>
+
+namespace lfm {
+
+GridLayout detect_grid(const double* x, int64_t n, int64_t G) {
+  GridLayout L;
+  if (!x || n < 1 || G < 1 || n > INT_MAX || G > INT_MAX) return L;
+  const int g0 = gene_index(x[1], (int)G);
+  int64_t T = 1;
+  while (T < n && gene_index(x[3 * T + 1], (int)G) == g0) ++T;
+  if (n % T != 0) return L;
+  const int64_t nblk = n / T;
+  L.times.resize(T);
+  for (int64_t t = 0; t < T; ++t) L.times[t] = x[3 * t];
+  L.block_gene.resize(nblk);
+  for (int64_t b = 0; b < nblk; ++b) {
+    const int gb = gene_index(x[3 * b * T + 1], (int)G);
+    L.block_gene[b] = gb;
+    for (int64_t t = 0; t < T; ++t) {
+      const double* r = x + 3 * (b * T + t);
+      if (r[2] != 1.0) return GridLayout();                    // all rows gene rows (flag 1)
+      if (gene_index(r[1], (int)G) != gb) return GridLayout(); // one gene per block
+      if (std::memcmp(&r[0], &L.times[t], sizeof(double)) != 0) return GridLayout();  // shared
+    }
+  }
+  const double t0 = L.times[0];
+  const double dt = T > 1 ? (L.times[T - 1] - t0) / (double)(T - 1) : 0.0;
+  double scale = 1.0;
+  for (double t : L.times) scale = std::max(scale, std::fabs(t));
+  for (int64_t t = 0; t < T; ++t)
+    if (!(std::fabs(L.times[t] - (t0 + (double)t * dt)) <= 1e-12 * scale)) return GridLayout();
+  L.T = (int)T;
+  L.nblk = (int)nblk;
+  L.t0 = t0;
+  L.dt = dt;
+  L.ok = true;
+  return L;
+}
+
+std::vector<std::pair<int64_t, int>> plan_steps(int64_t nblk, int64_t Mp, int nb, bool bordered,
+                                                bool s3, int wbulk, int64_t w4min,
+                                                int64_t w2min) {
+  std::vector<std::pair<int64_t, int>> steps;
+  for (int64_t k = 0; k < nblk;) {
+    const int64_t m = bordered ? Mp + nb : Mp - k * nb;
+    int w = 1;
+    // the first bulk super-panel stays 4 wide: its chain runs beside the shallow first update
+    const int wk = steps.size() == 1 ? 4 : wbulk;
+    if (m >= w4min && k + wk <= nblk) w = wk;
+    else if (m >= w4min && k + 4 <= nblk) w = 4;
+    else if (m >= w2min && k + 2 <= nblk) w = 2;
+    if (k == 0 && s3) w = 1;
+    steps.emplace_back(k, w);
+    k += w;
+  }
+  return steps;
+}
+
+void rest_unit_tile(int64_t b, int T, int tj_lo, int Q, int* ti_out, int* tj_out) {
+  constexpr int SUB = 2;  // 64-row slabs per 128-row tile
+  const int sub = (int)(b % SUB);
+  b /= SUB;
+  int a = (int)((std::sqrt(8.0 * (double)b + 1.0) - 1.0) * 0.5);
+  while ((int64_t)(a + 1) * (a + 2) / 2 <= b) ++a;
+  while ((int64_t)a * (a + 1) / 2 > b) --a;
+  int tj, ti;
+  if (Q > 1) {
+    const int R = a / Q, r0 = R * Q, qr = std::min(Q, T - tj_lo - r0);
+    const int64_t off = b - (int64_t)r0 * (r0 + 1) / 2;
+    const int64_t full = (int64_t)R * qr * Q;
+    int lr, lc;
+    if (off < full) {
+      const int C = (int)(off / (qr * Q)), t = (int)(off % (qr * Q));
+      lr = t / Q;
+      lc = C * Q + t % Q;
+    } else {
+      const int d = (int)(off - full);
+      lr = (int)((std::sqrt(8.0 * (double)d + 1.0) - 1.0) * 0.5);
+      while ((lr + 1) * (lr + 2) / 2 <= d) ++lr;
+      while (lr * (lr + 1) / 2 > d) --lr;
+      lc = r0 + d - lr * (lr + 1) / 2;
+    }
+    tj = lc + tj_lo;
+    ti = SUB * (r0 + lr + tj_lo) + sub;
+  } else {
+    tj = (int)(b - (int64_t)a * (a + 1) / 2) + tj_lo;
+    ti = SUB * (a + tj_lo) + sub;
+  }
+  *ti_out = ti;
+  *tj_out = tj;
+}
+
+int64_t helper_units(int kd, int na, int nr, int nt, int wnext, int nb, int cus, int side_cus,
+                     double tc, double dmin) {
+  if (kd <= 0 || side_cus <= 0 || cus <= side_cus) return 0;
+  const double t = 154.0 * kd / 640.0 + 4.0;  // one depth-kd unit, us (step timeline)
+  const double o = 0.9;
+  const double sm = 4.0 * (cus - side_cus), sh = 4.0 * side_cus;
+  const double tall_eq = (double)nt * (wnext + 1) / 2.0 * nb / kd;
+  const double units = (double)na + nr + tall_eq;
+  const double d0 = units * t / (sm * o);
+  if (d0 < dmin) return 0;
+  const double x = o * (d0 - tc) / (t * (1.0 / sh + 1.0 / sm));
+  return std::max<int64_t>(0, std::min<int64_t>((int64_t)x, nr / 2));
+}
+
+int64_t helper_clamp(int64_t hu, int nr, int T, int wn, int lead, int Q) {
+  if (hu <= 0) return 0;
+  Q = std::max(Q, 1);
+  const int64_t r0e = std::min<int64_t>((int64_t)(lead + Q - 1) / Q * Q, (int64_t)T - wn);
+  hu = std::min<int64_t>(hu, (int64_t)nr - r0e * (r0e + 1));  // 2 slabs per triangle tile
+  if (hu <= 0) return 0;
+  for (int64_t b = nr - hu; b < nr; ++b) {
+    int ti, tj;
+    rest_unit_tile(b, T, wn, Q, &ti, &tj);
+    if (ti / 2 < wn + lead && tj < wn + lead) return 0;
+  }
+  return hu;
+}
+
+}  // namespace lfm

@@ -1,0 +1,81 @@
+// lfm_host.h — host-only logic of liblfm: x-layout detection, the factorisation's step plan,
+// the host mirror of the trailing update's unit enumeration and the side-CU helper's sizing.
+// Plain C++ (no HIP types), so lfm_host.cpp also builds into the host sanitizer check
+// (tests/native, `make -C tests/native asan`) with g++ -fsanitize=address,undefined.
+#pragma once
+
+#include <cmath>
+#include <cstdint>
+#include <utility>
+#include <vector>
+
+#if defined(__HIPCC__)
+#define LFM_HD __host__ __device__
+#else
+#define LFM_HD
+#endif
+
+namespace lfm {
+
+// JAX gather semantics for a gene index stored as a float: trunc toward zero, negative wraps
+// by +G, clamp to [0, G - 1] (NaN -> 0).
+LFM_HD inline int gene_index(double g, int G) {
+  double tg = trunc(g);
+  if (tg < 0) tg += (double)G;
+  if (!(tg >= 0)) tg = 0;  // also catches NaN
+  if (tg > (double)(G - 1)) tg = (double)(G - 1);
+  return (int)tg;
+}
+// int(flag) as the reference's switches read it (trunc; NaN -> 0; saturated)
+LFM_HD inline long long flag_int(double f) {
+  double tf = trunc(f);
+  if (!(tf == tf)) return 0;
+  if (tf > 4e18) tf = 4e18;
+  if (tf < -4e18) tf = -4e18;
+  return (long long)tf;
+}
+
+// Structure of x detected on the host: rows come in blocks of T consecutive rows that share
+// one uniform time vector t[tau] = t0 + tau*dt, one gene index per block and flag 1 — the
+// layout dataset_3d (src/dataset.py:358-399) produces.
+struct GridLayout {
+  bool ok = false;
+  int T = 0;          // timepoints per block
+  int nblk = 0;       // number of blocks (= n / T)
+  double t0 = 0, dt = 0;
+  std::vector<double> times;   // [T]  the actual time values of block 0
+  std::vector<int> block_gene; // [nblk] clamped gene index per block
+};
+
+GridLayout detect_grid(const double* x, int64_t n, int64_t G);
+
+// Super-panel plan of a blocked factorisation over nblk block columns of width nb: (first
+// block column, width in block columns) per step. Width wbulk (the first bulk step 4) while
+// the trailing matrix has >= w4min rows, 4 if wbulk does not fit, 2 down to w2min rows, else
+// 1; schedule 3 starts with a one-column super-panel. Bordered (the gradient's inverse): the
+// trailing window is a constant Mp + nb rows.
+std::vector<std::pair<int64_t, int>> plan_steps(int64_t nblk, int64_t Mp, int nb, bool bordered,
+                                                bool s3, int wbulk, int64_t w4min,
+                                                int64_t w2min);
+
+// Host mirror of the step kernel's rest-triangle enumeration (64-row slabs x 128-column tiles,
+// Q x Q supertiles; lfm_chol.hip syrk_unit): unit b -> (64-row slab ti, 128-column tile tj)
+// relative to the trailing matrix, tile columns [tj_lo, T).
+void rest_unit_tile(int64_t b, int T, int tj_lo, int Q, int* ti_out, int* tj_out);
+
+// The side-CU helper's share of a step's rest units: the main launch of U unit-equivalents
+// takes D0 = U t / (S_m o) alone (t: one depth-kd unit, o: slot occupancy, S_m / S_h: the
+// main / side stream's workgroup slots); giving x units to the helper, which starts after
+// the next chain (tc, us), balances at x t (1 / S_h + 1 / S_m) = o (D0 - tc). No helper for
+// D0 < dmin; at most half the rest units.
+int64_t helper_units(int kd, int na, int nr, int nt, int wnext, int nb, int cus, int side_cus,
+                     double tc, double dmin);
+
+// Caps a helper share hu (the tail [nr - hu, nr) of the enumeration) so that it holds no lead
+// tile (tile rows and columns < wn + lead: the inputs of the chain two steps ahead, which only
+// the main launch writes through and counts). In the supertile order every unit of triangle
+// rows < lead precedes the first unit of supertile row ceil(lead / Q). Returns 0 if the
+// enumeration mirror still finds a lead tile in the tail.
+int64_t helper_clamp(int64_t hu, int nr, int T, int wn, int lead, int Q);
+
+}  // namespace lfm

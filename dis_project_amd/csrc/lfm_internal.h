@@ -10,6 +10,7 @@
 
 #include "../../include/lfm.h"
 #include "../../include/lfm_diag.h"
+#include "lfm_host.h"
 
 namespace lfm {
 
@@ -32,18 +33,6 @@ enum KClass {
 };
 
 extern const char* const kClassName[K_NCLASS];
-
-// Structure of x detected on the host: rows come in blocks of T consecutive rows
-// that share one uniform time vector t[tau] = t0 + tau*dt, one gene index per
-// block and flag 1 — the layout dataset_3d (src/dataset.py:358-399) produces.
-struct GridLayout {
-  bool ok = false;
-  int T = 0;          // timepoints per block
-  int nblk = 0;       // number of blocks (= n / T)
-  double t0 = 0, dt = 0;
-  std::vector<double> times;   // [T]  the actual time values of block 0
-  std::vector<int> block_gene; // [nblk] clamped gene index per block
-};
 
 struct ProfEvent {
   int cls;
@@ -143,25 +132,8 @@ void prof_end(lfm_ctx* ctx, int cls, hipEvent_t a, double flops, double bytes,
 int ensure_events(lfm_ctx* ctx, size_t count);
 int prof_flush(lfm_ctx* ctx);
 
-GridLayout detect_grid(const double* x, int64_t n, int64_t G);
 int chain_coresident(lfm_ctx* ctx, hipStream_t st, int G, bool* good);
 int gene_clamp_host(double g, int64_t G);
-
-// device-side gene index semantics: trunc toward zero, negative wraps, clamp
-__host__ __device__ inline int gene_index(double g, int G) {
-  double tg = trunc(g);
-  if (tg < 0) tg += (double)G;
-  if (!(tg >= 0)) tg = 0;              // also catches NaN
-  if (tg > (double)(G - 1)) tg = (double)(G - 1);
-  return (int)tg;
-}
-__host__ __device__ inline long long flag_int(double f) {
-  double tf = trunc(f);
-  if (!(tf == tf)) return 0;
-  if (tf > 4e18) tf = 4e18;
-  if (tf < -4e18) tf = -4e18;
-  return (long long)tf;
-}
 
 // ------------------------------------------------------ launch wrappers
 // Packed parameter block on the device (doubles):
