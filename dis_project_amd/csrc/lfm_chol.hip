@@ -1359,6 +1359,10 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
     if (lead) bump_after_stores(g.e_xready);
     if (ti / 2 >= g.e_pub_lo && ti / 2 < g.e_pub_hi)
       publish_after_stores(&g.tile_step[tile_index(i0, j0, g.tile_cols)], (unsigned)g.step + 2u);
+    if (st) {
+      __syncthreads();
+      stamp_max(st + 3);  // the launch's last unit end
+    }
     return;
   }
   // tall unit (row slab rb, column block cb) of step s + 1: the slabs the early units read
@@ -2473,19 +2477,24 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       hipEvent_t* evL = ev + 1;  // evL[2 s] = ev[1 + 2 s]: launch s done (main)
       hipEvent_t* evH = ev + 2;  // evH[2 s] = ev[2 + 2 s]: helper(s) done (side)
       bool helped = false;       // the previous step had a helper launch
-      // Early units (LFM_EARLY = RE tile rows, MLL): launch s ends with the first RE (RE + 1)
-      // units of step s + 1's rest enumeration (its triangle rows < RE; RE a multiple of the
-      // supertile edge, so they are a prefix), which fill the slots launch s's last units leave
-      // idle; launch s + 1 skips them. Only between bulk steps whose early region lies above n.
+      // Early units (LFM_EARLY = RE tile rows at most, MLL): launch s ends with the first
+      // re (re + 1) units of step s + 1's rest enumeration (its triangle rows < re; re a
+      // multiple of the supertile edge, so they are a prefix), which fill the slots launch s's
+      // last units leave idle; launch s + 1 skips them. re = RE capped so the region keeps a
+      // supertile row of the triangle after it and lies above n (no padding rows), for steps
+      // s + 1 of at least LFM_EARLY_WMIN block columns.
       const int RE = mode == CHOL_MLL && !bordered ? env_int("LFM_EARLY", 0) : 0;
-      auto early_ok = [&](int s) -> bool {  // launch s runs step s + 1's early units
-        if (RE <= 0 || RE % LFM_SUPERTILE || s < 0 || s + 2 >= S) return false;
-        if (steps[s + 1].second < 4) return false;
+      const int early_wmin = env_int("LFM_EARLY_WMIN", 4);
+      auto early_rows = [&](int s) -> int {  // launch s runs step s + 1's early units
+        if (RE < LFM_SUPERTILE || s < 0 || s + 2 >= S) return 0;
+        if (steps[s + 1].second < early_wmin) return 0;
         const int64_t K1n = (steps[s + 1].first + steps[s + 1].second) * NB;
         const int Tn = (int)((rows_end(K1n) - K1n) / ST), wnn = steps[s + 2].second;
-        return Tn - wnn >= RE + LFM_SUPERTILE && K1n + (int64_t)(wnn + RE + 1) * NB <= n;
+        int re = std::min(RE, Tn - wnn - LFM_SUPERTILE);
+        re = std::min<int64_t>(re, (n - K1n) / NB - wnn - 1);
+        re = re / LFM_SUPERTILE * LFM_SUPERTILE;
+        return re > 0 ? re : 0;
       };
-      const int64_t E = (int64_t)RE * (RE + 1);
       // algorithmic flops (profiling) of rest units [b0, b1) of a step's update: 2 kd per
       // updated lower element of their tiles, rows past n (identity padding) excluded
       auto units_alg = [&](int64_t s0u, int T, int wn, int kd, int64_t b0, int64_t b1) {
@@ -2516,14 +2525,15 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         g.tile_cols = (int)tile_cols;
         g.step = s;
         const int64_t total = g.nr;                     // the step's rest enumeration
-        const int64_t head = early_ok(s - 1) ? E : 0;   // done by launch s - 1's early units
-        const bool early = early_ok(s);
+        const int re_prev = early_rows(s - 1), re = early_rows(s);
+        const int64_t head = (int64_t)re_prev * (re_prev + 1);  // launch s - 1's early units
+        const bool early = re > 0;
         int protect = g.xready ? g.lead : 0;            // triangle rows the helper must not take
         if (early) {
           // step s + 1's early region (its triangle rows < RE) in this step's tile rows
           StepArgs gn{};
           update_args(gn, s + 1);
-          g.ne = (int)E;
+          g.ne = re * (re + 1);
           g.e_s0 = gn.s0;
           g.e_T = gn.T;
           g.e_wn = gn.wn;
@@ -2531,15 +2541,15 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
             g.e_xready = xready + s + 3;
             g.e_lead = steps[s + 3].second;
           }
-          if (early_ok(s + 1)) {  // step s + 2's early region within these units
+          if (const int re2 = early_rows(s + 1)) {  // step s + 2's early region in these units
             g.e_pub_lo = gn.wn + steps[s + 3].second;
-            g.e_pub_hi = g.e_pub_lo + RE;
+            g.e_pub_hi = g.e_pub_lo + re2;
           }
           g.pub_lo = g.wn + gn.wn;
-          g.pub_hi = g.pub_lo + RE;
+          g.pub_hi = g.pub_lo + re;
           g.xrow = xrow + (size_t)(s + 1) * slabs;
-          g.xrow_slabs = 2 * (gn.wn + RE);
-          protect = std::max(protect, gn.wn + RE);
+          g.xrow_slabs = 2 * (gn.wn + re);
+          protect = std::max(protect, gn.wn + re);
           ctx->last_early += g.ne;
         }
         // Side-CU helper (LFM_HELPER): while the factor chain has slack (long launches), the
