@@ -369,16 +369,20 @@ def test_early_units_bit_identical_and_flops_conserved(c2_dev, monkeypatch):
         assert f == pytest.approx(f0, rel=1e-12)
 
 
-@pytest.mark.parametrize("G,T,re_rows,w4", [(16, 256, "6", "1024"), (16, 256, "12", "2048"),
-                                            (10, 200, "6", "512"), (24, 256, "18", "1536")])
+@pytest.mark.parametrize("G,T,re_rows,w4,w2", [(16, 256, "6", "1024", "512"),
+                                               (16, 256, "12", "2048", "1024"),
+                                               (20, 200, "6", "512", "256"),
+                                               (24, 256, "18", "1536", "768"),
+                                               (24, 256, "12", "4096", "3072")])
 @pytest.mark.parametrize("helper", ["off", "forced"])
 @pytest.mark.parametrize("wmin", ["4", "1"])
-def test_early_units_small_bulk_plans(monkeypatch, G, T, re_rows, w4, helper, wmin):
-    """Early units on plans with bulk steps at N = 4096 / 2000 (unaligned, padded) / 6144
-    (LFM_W4_MIN lowered so the wide super-panels start early), alone and with the side-CU
-    helper forced onto every step (its tail then clamped against the early region), for bulk
-    steps only and for every step width (LFM_EARLY_WMIN=1): the MLL bit-identical to
-    LFM_EARLY=0 and within 1e-9 of the oracle."""
+def test_early_units_small_bulk_plans(monkeypatch, G, T, re_rows, w4, w2, helper, wmin):
+    """Early units on plans with bulk steps at N = 4096 / 4000 (unaligned, padded) / 6144
+    (LFM_W4_MIN / LFM_W2_MIN lowered so the wide super-panels start early), alone and with the
+    side-CU helper forced onto every step (its tail then clamped against the early region), for
+    bulk steps only and for every step width (LFM_EARLY_WMIN=1: the last plan then has early
+    units in its w = 2 and w = 1 steps): the MLL bit-identical to LFM_EARLY=0 and within 1e-9
+    of the oracle."""
     from dis_project_amd import _lib, configs
     from oracle import lfm_oracle as O
 
@@ -387,6 +391,7 @@ def test_early_units_small_bulk_plans(monkeypatch, G, T, re_rows, w4, helper, wm
     y = np.ascontiguousarray(work.data.y.reshape(-1))
     ctx = _lib.get_context(0)
     monkeypatch.setenv("LFM_W4_MIN", w4)
+    monkeypatch.setenv("LFM_W2_MIN", w2)
     monkeypatch.setenv("LFM_EARLY_WMIN", wmin)
     if helper == "forced":
         monkeypatch.setenv("LFM_HELPER_MIN", "0")
