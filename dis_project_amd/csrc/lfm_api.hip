@@ -38,13 +38,20 @@ int set_err(lfm_ctx* ctx, int code, const std::string& msg) {
   return code;
 }
 
-int status_code(lfm_ctx* ctx, double st) {
+int status_code(lfm_ctx* ctx, double st, double why) {
   const long long v = (long long)st;
   if (v == INT_MAX) return LFM_OK;
-  if (v == STATUS_TIMEOUT)
+  if (v == STATUS_TIMEOUT) {
+    static const char* const kind[] = {"unrecorded", "tall unit on the chain's factor",
+                                       "tall unit on its ahead units", "early unit on its C tile",
+                                       "early unit on its X rows", "chain input wait",
+                                       "chain grid barrier", "fused panel wait"};
+    const int k = why >= 0 && why < 8 ? (int)why : 0;
     return set_err(ctx, LFM_E_TIMEOUT,
-                   "device-side wait timed out (a cross-stream hand-off of the factorisation "
-                   "stalled): the result is invalid, not a property of the input");
+                   std::string("device-side wait timed out (a cross-stream hand-off of the "
+                               "factorisation stalled; first: ") + kind[k] +
+                       "): the result is invalid, not a property of the input");
+  }
   return set_err(ctx, LFM_E_NOT_PD,
                  "Cholesky failed: non-positive pivot at index " + std::to_string(v));
 }
@@ -323,11 +330,11 @@ int mll_blocked(lfm_ctx* ctx, const Staged& st, const double* d_x, const double*
                         fuse ? &gen : nullptr);
   if (r) return r;
   double* hres = ctx->hpin + (ctx->hpin_bytes / 8 - 8);
-  hipMemcpyAsync(hres, ctx->result, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+  hipMemcpyAsync(hres, ctx->result, 5 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
   r = finish(ctx);
   if (r) return r;
   *out = hres[0];
-  r = status_code(ctx, hres[3]);
+  r = status_code(ctx, hres[3], hres[4]);
   if (r) *out = std::nan("");
   return r;
 }
@@ -873,13 +880,13 @@ int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
   r = ensure_pinned(ctx, (ng + 16) * sizeof(double));
   if (r) return r;
   double* hres = ctx->hpin;
-  hipMemcpyAsync(hres, ctx->result, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+  hipMemcpyAsync(hres, ctx->result, 5 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
   hipMemcpyAsync(hres + 8, d_out, ng * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
   r = finish(ctx);
   if (r) return r;
   *value = hres[0];
   std::memcpy(grad, hres + 8, ng * sizeof(double));
-  r = status_code(ctx, hres[3]);
+  r = status_code(ctx, hres[3], hres[4]);
   if (r) {
     *value = std::nan("");
     for (size_t i = 0; i < ng; ++i) grad[i] = std::nan("");
@@ -926,12 +933,12 @@ int lfm_posterior_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
   r = ensure_pinned(ctx, 64 * sizeof(double));
   if (r) return r;
   double* hres = ctx->hpin;
-  hipMemcpyAsync(hres, ctx->result, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+  hipMemcpyAsync(hres, ctx->result, 5 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
   hipMemcpyAsync(mean, d_mean, m * 8, hipMemcpyDeviceToHost, ctx->stream);
   hipMemcpyAsync(cov, d_cov, (size_t)m * m * 8, hipMemcpyDeviceToHost, ctx->stream);
   r = finish(ctx);
   if (r) return r;
-  r = status_code(ctx, hres[3]);
+  r = status_code(ctx, hres[3], hres[4]);
   if (r) {
     const double nan = std::nan("");
     for (int64_t i = 0; i < m; ++i) mean[i] = nan;
@@ -1088,11 +1095,11 @@ int lfm_log_prob_f64(lfm_ctx* ctx, const double* loc, const double* scale, int64
   r = chol_factor_solve(ctx, ctx->A, Mp, n, Mp, 0, ctx->result);
   if (r) return r;
   double* hres = ctx->hpin + (ctx->hpin_bytes / 8 - 8);
-  hipMemcpyAsync(hres, ctx->result, 4 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+  hipMemcpyAsync(hres, ctx->result, 5 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
   r = finish(ctx);
   if (r) return r;
   *out = hres[0];
-  r = status_code(ctx, hres[3]);
+  r = status_code(ctx, hres[3], hres[4]);
   if (r) *out = std::nan("");
   return r;
 }

@@ -52,6 +52,13 @@ static constexpr int KB = 16;        // SYRK K-step staged through LDS
 static constexpr int LDP = LFM_LDS_PAD;
 static constexpr int STATUS_NONE = INT_MAX;
 constexpr int PANEL_TIMEOUT = STATUS_TIMEOUT;  // status: a bounded device-side wait ran out
+// Which wait ran out first (status[1], reported in LFM_E_TIMEOUT's message): 1 tall unit on the
+// chain, 2 tall unit on its ahead units, 3 early unit on its C tile, 4 early unit on X rows,
+// 5 chain input wait, 6 chain grid barrier, 7 fused panel wait.
+__device__ __forceinline__ void timeout_at(int* status, int why) {
+  atomicMin(status, PANEL_TIMEOUT);
+  atomicCAS(status + 1, 0, why);
+}
 
 __device__ __forceinline__ double4v mfma16(double a, double b, double4v c) {
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -1339,17 +1346,16 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
       if (threadIdx.x == 0) {
         bool good = spin_until<false>(&g.tile_step[tile_index(i0, j0, g.tile_cols)],
                                       (unsigned)g.step + 1u, g.spin);
+        if (!good) timeout_at(g.status, 3);
         const unsigned tw = (unsigned)g.tw;
         good = good && spin_until<false>(&g.xrow[ti], tw, g.spin);
         good = good && spin_until<false>(&g.xrow[2 * tj], tw, g.spin);
         good = good && spin_until<false>(&g.xrow[2 * tj + 1], tw, g.spin);
+        if (!good) timeout_at(g.status, 4);
         ok = good;
       }
       __syncthreads();
-      if (!ok) {
-        if (threadIdx.x == 0) atomicMin(g.status, PANEL_TIMEOUT);
-        return;
-      }
+      if (!ok) return;
     }
     const Panel pe{g.X, (int64_t)g.tw * NB, g.tr0};
     const bool lead = syrk_unit<true, 64, false, LFM_STEP_KS, false, true>(
@@ -1387,18 +1393,20 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
     // relaxed polling and device-coherent operand loads below instead of an acquire fence:
     // an agent-scope acquire invalidates this XCD's L2 under the running bulk units
     if (threadIdx.x == 0) {
+      int why = 0;
       bool good = !g.chain_done || spin_until<false>(g.chain_done, 1u, g.spin);
+      if (!good) why = 1;
       // rows past step s's update (bordered: the border rows that entered the window with
       // super-panel s + 1, zero in every earlier panel column) have no ahead unit to wait for
-      if (good && g.a_done && (i0 - g.s0) / ST < g.T)
+      if (good && g.a_done && (i0 - g.s0) / ST < g.T) {
         good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], 2u * g.wn, g.spin);
+        if (!good) why = 2;
+      }
+      if (!good) timeout_at(g.status, why);
       ok = good;
     }
     __syncthreads();
-    if (!ok) {
-      if (threadIdx.x == 0) atomicMin(g.status, PANEL_TIMEOUT);
-      return;
-    }
+    if (!ok) return;
     if (st) stamp_max(st + 2);
   }
   const int W = g.tw * NB;
@@ -1520,7 +1528,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
     if (b == 1) return;
     if (!wait_counter(&sync[1], 2u * epoch, spin)) {
       if (tid == 0) {
-        atomicMin(status, PANEL_TIMEOUT);
+        timeout_at(status, 7);
         __hip_atomic_store(&sync[0], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
       return;
@@ -1539,7 +1547,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) sA[wr + ir * 4 + lk][wc + jr * 16 + li] = -acc[ir][jr];
   if (!wait_counter(&sync[0], epoch, spin)) {
-    if (tid == 0) atomicMin(status, PANEL_TIMEOUT);
+    if (tid == 0) timeout_at(status, 7);
     return;
   }
   trsm_rows(sA, A, lda, i0, kb, dinv);
@@ -1599,7 +1607,7 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, int* s
       if (++it >= limit ||
           __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == PANEL_TIMEOUT) {
         good = false;
-        atomicMin(status, PANEL_TIMEOUT);
+        timeout_at(status, 6);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -1627,7 +1635,7 @@ __device__ __forceinline__ bool grid_sync_light(unsigned* bar, unsigned target, 
       if (++it >= limit ||
           __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == PANEL_TIMEOUT) {
         good = false;
-        atomicMin(status, PANEL_TIMEOUT);
+        timeout_at(status, 6);
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -1750,15 +1758,15 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
   // the block's inputs come from the main stream's launch in flight: wait for its count
   if (g.xready) {
     __shared__ int okx;
-    if (tid == 0) okx = spin_until<false>(g.xready, g.xtarget, g.spin);
+    if (tid == 0) {
+      okx = spin_until<false>(g.xready, g.xtarget, g.spin);
+      if (!okx) timeout_at(g.status, 5);
+    }
     __syncthreads();
     // one agent-scope acquire so the inputs below come through plain, cached loads (LIGHT:
     // device-coherent loads instead)
     if (!LIGHT) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    if (!okx) {
-      if (tid == 0) atomicMin(g.status, PANEL_TIMEOUT);
-      return;
-    }
+    if (!okx) return;
   }
   stamp(14);
   if (g.kd > 0) {
@@ -2000,10 +2008,14 @@ __global__ __launch_bounds__(1024) void finalize_kernel(const double* __restrict
     out[1] = logdet;
     out[2] = Q;
     out[3] = (double)status[0];
+    out[4] = (double)status[1];
   }
 }
 
-__global__ void status_init_kernel(int* st) { st[0] = STATUS_NONE; }
+__global__ void status_init_kernel(int* st) {
+  st[0] = STATUS_NONE;
+  st[1] = 0;  // which wait timed out first (timeout_at)
+}
 
 
 namespace {

@@ -112,7 +112,7 @@ namespace lfm {
 // wait ran out (it wins the atomicMin over any pivot index).
 constexpr int STATUS_TIMEOUT = -2;
 // LFM_OK, LFM_E_NOT_PD (pivot index in the message) or LFM_E_TIMEOUT for a status word.
-int status_code(lfm_ctx* ctx, double st);
+int status_code(lfm_ctx* ctx, double st, double why = 0.0);
 
 // The next factorisation on ctx runs schedule 3 (the CU-partitioned pair exists, and the
 // call holds the device's schedule-3 tenancy: lfm_api.hip S3Tenancy).
