@@ -1020,7 +1020,7 @@ __device__ __forceinline__ void unit_tile(int T, int tj_lo, int tj_hi, int64_t b
                                           int* ti_out, int* tj_out) {
   constexpr int SUB = ST / TR;  // row tiles per 128 rows
   int ti, tj;  // ti in TR-row units
-  if (LFM_BAND_ROWS && tj_hi - tj_lo <= 8 && ti0 >= tj_hi) {
+  if (LFM_BAND_ROWS && tj_hi - tj_lo <= kBandMaxCols && ti0 >= tj_hi) {
     // rectangular band (every row below the band's columns): row by row, so consecutive units
     // share a row panel and the band's few column panels stay in L2
     const int nb = tj_hi - tj_lo;
@@ -1028,7 +1028,7 @@ __device__ __forceinline__ void unit_tile(int T, int tj_lo, int tj_hi, int64_t b
     const int rem = (int)(b - r * nb * SUB);
     tj = tj_lo + rem / SUB;
     ti = SUB * (ti0 + (int)r) + rem % SUB;
-  } else if (tj_hi - tj_lo <= 8) {
+  } else if (tj_hi - tj_lo <= kBandMaxCols) {
     // band: tile columns [tj_lo, tj_hi), tile rows max(tj, ti0) .. T - 1
     tj = tj_lo;
     while (b >= (int64_t)SUB * max(0, T - max(tj, ti0))) {
@@ -2540,7 +2540,9 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         const int re_prev = early_rows(s - 1), re = early_rows(s);
         const int64_t head = (int64_t)re_prev * (re_prev + 1);  // launch s - 1's early units
         const bool early = re > 0;
-        int protect = g.xready ? g.lead : 0;            // triangle rows the helper must not take
+        // triangle rows the helper must not take: chain(s + 2)'s lead tiles, the head (done by
+        // launch s - 1) and the next step's early region (below)
+        int protect = std::max(g.xready ? g.lead : 0, re_prev);
         if (early) {
           // step s + 1's early region (its triangle rows < RE) in this step's tile rows
           StepArgs gn{};

@@ -111,7 +111,10 @@ int64_t helper_units(int kd, int na, int nr, int nt, int wnext, int nb, int cus,
 }
 
 int64_t helper_clamp(int64_t hu, int nr, int T, int wn, int lead, int Q) {
-  if (hu <= 0) return 0;
+  // a rest region of at most 8 tile columns is enumerated on the device as a band, column by
+  // column (lfm_chol.hip unit_tile), not as this triangle: no helper there (its tail would be
+  // the last columns, lead tiles included)
+  if (hu <= 0 || T - wn <= kBandMaxCols) return 0;
   Q = std::max(Q, 1);
   const int64_t r0e = std::min<int64_t>((int64_t)(lead + Q - 1) / Q * Q, (int64_t)T - wn);
   hu = std::min<int64_t>(hu, (int64_t)nr - r0e * (r0e + 1));  // 2 slabs per triangle tile

@@ -58,6 +58,10 @@ std::vector<std::pair<int64_t, int>> plan_steps(int64_t nblk, int64_t Mp, int nb
                                                 bool s3, int wbulk, int64_t w4min,
                                                 int64_t w2min);
 
+// Rest regions of at most this many tile columns are enumerated as bands (column by column),
+// wider ones as the supertiled triangle below (lfm_chol.hip unit_tile).
+constexpr int kBandMaxCols = 8;
+
 // Host mirror of the step kernel's rest-triangle enumeration (64-row slabs x 128-column tiles,
 // Q x Q supertiles; lfm_chol.hip syrk_unit): unit b -> (64-row slab ti, 128-column tile tj)
 // relative to the trailing matrix, tile columns [tj_lo, T).
@@ -75,7 +79,8 @@ int64_t helper_units(int kd, int na, int nr, int nt, int wnext, int nb, int cus,
 // tile (tile rows and columns < wn + lead: the inputs of the chain two steps ahead, which only
 // the main launch writes through and counts). In the supertile order every unit of triangle
 // rows < lead precedes the first unit of supertile row ceil(lead / Q). Returns 0 if the
-// enumeration mirror still finds a lead tile in the tail.
+// enumeration mirror still finds a lead tile in the tail, and for band-enumerated regions
+// (T - wn <= kBandMaxCols).
 int64_t helper_clamp(int64_t hu, int nr, int T, int wn, int lead, int Q);
 
 }  // namespace lfm

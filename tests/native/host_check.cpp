@@ -71,7 +71,7 @@ static void check_helper_clamp() {
     const int Q = (int)(rng() % 2) ? 6 : 1 + (int)(rng() % 4);
     const int T = 2 + (int)(rng() % 130);
     const int wn = 1 + (int)(rng() % 5);
-    if (wn >= T) continue;
+    if (T - wn <= kBandMaxCols) continue;  // band enumeration: no helper (checked below)
     const int lead = 1 + (int)(rng() % 5);
     const int nr = (T - wn) * (T - wn + 1);
     const int64_t want = (int64_t)(rng() % (nr + 1));
@@ -86,6 +86,12 @@ static void check_helper_clamp() {
     capped += hu < want;
     ++cases;
   }
+  // band-enumerated rest regions (<= 8 tile columns) never get a helper
+  for (int T = 2; T <= 40; ++T)
+    for (int wn = 1; wn < T && wn <= 5; ++wn)
+      if (T - wn <= kBandMaxCols)
+        CHECK(helper_clamp((T - wn) * (T - wn + 1) / 2, (T - wn) * (T - wn + 1), T, wn, 1, 6) == 0,
+              "band region T=%d wn=%d got a helper", T, wn);
   CHECK(helper_units(640, 100, 5000, 200, 5, 128, 256, 32, 700, 1200) >= 0, "helper_units");
   CHECK(helper_units(640, 100, 5000, 200, 5, 128, 256, 32, 700, 1200) <= 2500, "helper half");
   CHECK(helper_units(640, 0, 10, 0, 5, 128, 256, 32, 700, 1200) == 0, "no helper for short");
