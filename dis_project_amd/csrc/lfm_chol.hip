@@ -53,8 +53,8 @@ static constexpr int LDP = LFM_LDS_PAD;
 static constexpr int STATUS_NONE = INT_MAX;
 constexpr int PANEL_TIMEOUT = STATUS_TIMEOUT;  // status: a bounded device-side wait ran out
 // Which wait ran out first (status[1], reported in LFM_E_TIMEOUT's message): 1 tall unit on the
-// chain, 2 tall unit on its ahead units, 3 early unit on its C tile, 4 early unit on X rows,
-// 5 chain input wait, 6 chain grid barrier, 7 fused panel wait.
+// chain, 2 tall unit on its ahead units, 5 chain input wait, 6 chain grid barrier, 7 fused panel
+// wait (3 and 4 are unused).
 __device__ __forceinline__ void timeout_at(int* status, int why) {
   atomicMin(status, PANEL_TIMEOUT);
   atomicCAS(status + 1, 0, why);
@@ -909,7 +909,7 @@ __device__ __forceinline__ double ldc(const double* p) {
 // GEN: C is not read but generated from the gram tables (GramGen, a tile inside one gene pair
 // of an aligned grid layout): the tile's Toeplitz windows and row / column tables staged in
 // sP first, then gram_grid_aligned_kernel's arithmetic per element (bit-identical Sigma).
-template <bool CIO, int TR, int KS, bool LDCOH, bool CLOAD, bool GEN = false, bool CCOH = false>
+template <bool CIO, int TR, int KS, bool LDCOH, bool CLOAD, bool GEN = false>
 __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, Panel P, int kd,
                                           int64_t i0, int64_t j0, bool diag, bool coh,
                                           double (*__restrict__ sP)[KS + LDP],
@@ -985,7 +985,7 @@ __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, P
     for (int ir = 0; ir < IRN; ++ir)
 #pragma unroll
       for (int jr = 0; jr < 4; ++jr)
-        acc[ir][jr] = (CIO && CLOAD) ? -ldc<LDCOH || CCOH>(&Cb[ir * ld4 + jr * 16]) : 0.0;
+        acc[ir][jr] = (CIO && CLOAD) ? -ldc<LDCOH>(&Cb[ir * ld4 + jr * 16]) : 0.0;
   }
   gemm_accumulate<TR, false, LDCOH, KS>(P.p + (i0 - P.r0) * P.ld, P.ld, P.p + (j0 - P.r0) * P.ld,
                                         P.ld, kd, acc, sP);
@@ -1080,18 +1080,14 @@ __device__ __forceinline__ void unit_tile(int T, int tj_lo, int tj_hi, int64_t b
 // Returns whether the unit's tile lies in the leading coh_lim x coh_lim tiles of the trailing
 // matrix (stores then write through to memory: device-coherent, for an in-flight reader).
 // LDCOH: C and panel loads device-coherent too (a reader of data written in the same launch).
-// CCOH: the C tile is loaded device-coherently (written through by another unit of the same
-// launch); tiles with 128-row tile index in [pub_lo, pub_hi) (the next step's early units
-// read them in this launch) are stored write-through like the lead tiles.
-template <bool CIO, int TR, bool COH = false, int KS = KB, bool LDCOH = false, bool CCOH = false>
+template <bool CIO, int TR, bool COH = false, int KS = KB, bool LDCOH = false>
 __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, int64_t s, Panel P,
                                           int kd, int T, int tj_lo, int tj_hi, int64_t b, int ti0,
                                           double (*__restrict__ sP)[KS + LDP], int coh_lim = 0,
                                           int64_t pad_after = INT64_MAX,
                                           int64_t pad_end = INT64_MAX,
                                           int64_t zero_from = INT64_MAX,
-                                          const GramGen* gen = nullptr, int pub_lo = 0,
-                                          int pub_hi = 0) {
+                                          const GramGen* gen = nullptr) {
   constexpr int SUB = ST / TR;  // row tiles per 128 rows
   int ti, tj;  // ti in TR-row units
   unit_tile<TR>(T, tj_lo, tj_hi, b, ti0, &ti, &tj);
@@ -1099,11 +1095,10 @@ __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, i
   const int64_t i0 = s + (int64_t)ti * TR, j0 = s + (int64_t)tj * ST;
   const bool diag = i0 < j0 + ST;  // the tile reaches the diagonal: keep col <= row only
   const bool in_lead = (i0 - s) / ST < coh_lim && (j0 - s) / ST < coh_lim;
-  const bool in_pub = ti / SUB >= pub_lo && ti / SUB < pub_hi;
   // rows in (pad_after, pad_end) are identity padding of the augmented matrix (their panel
   // entries are zero): nothing reads their update
   if (i0 > pad_after && i0 < pad_end && !in_lead) return false;
-  const bool coh = COH || in_lead || in_pub;
+  const bool coh = COH || in_lead;
   // rows >= zero_from are zeros no update has written yet (the bordered matrix's border rows
   // entering the window; never initialised in memory): a tile body that does not load C. (A
   // per-element load-or-zero choice makes hipcc branch around every load and wait on each, +7 %
@@ -1113,7 +1108,7 @@ __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, i
   else if (gen && i0 + TR <= gen->n)
     syrk_tile<CIO, TR, KS, LDCOH, false, true>(A, lda, P, kd, i0, j0, diag, coh, sP, gen);
   else
-    syrk_tile<CIO, TR, KS, LDCOH, true, false, CCOH>(A, lda, P, kd, i0, j0, diag, coh, sP);
+    syrk_tile<CIO, TR, KS, LDCOH, true>(A, lda, P, kd, i0, j0, diag, coh, sP);
   return in_lead;
 }
 
@@ -1201,40 +1196,8 @@ struct StepArgs {
   int64_t copy_from;
   GramGen gen;       // gen.tab != NULL: the first step's update units generate Sigma (fused gram)
   int64_t rest_off;  // rest units of this launch are [rest_off, rest_off + nr) of the step's
-                     // enumeration (the side-CU helper launch takes the tail of it, the
-                     // previous launch's early units its head)
-  // Early units: the first ne units of step s + 1's rest enumeration, run at the end of this
-  // launch (after the tall units) so they fill the slots this launch's last units leave idle.
-  // Each waits for its C tile's step-s update (tile_step >= step + 1: the rest units of tile
-  // rows [pub_lo, pub_hi) store write-through and publish) and for the rows of X_{s+1} it reads
-  // (xrow[slab] == tw: the tall units of the first xrow_slabs slabs, dispatched first, store
-  // write-through and count). Every wait is on an earlier unit of this launch (dispatched
-  // before it on its XCD) or on the side stream's chain, as for the tall units.
-  int ne;
-  int64_t e_s0;      // step s + 1: trailing matrix start K1_{s+1} (= tr0)
-  int e_T, e_wn;     // its 128-tiles and next width; depth tw * 128, panel X (rows from tr0)
-  unsigned* e_xready;  // chain(s + 3)'s inputs among the early units (NULL: none)
-  int e_lead;
-  int e_pub_lo, e_pub_hi;  // early units publish these tile rows for step s + 2's early units
-  int pub_lo, pub_hi;      // this step's rest units publish these (step s + 1's early region)
-  unsigned* tile_step;     // [Mp / 64][tile_cols]: 1 + the last step that updated the tile
-  int tile_cols;
-  unsigned* xrow;          // [slabs of X_{s+1}] completed column blocks (tall units)
-  int xrow_slabs;
-  int step;                // s
+                     // enumeration (the side-CU helper launch takes the tail of it)
 };
-
-// Absolute index of the (64-row slab, 128-column tile) holding element (i0, j0).
-__device__ __forceinline__ int64_t tile_index(int64_t i0, int64_t j0, int cols) {
-  return (i0 / 64) * cols + j0 / ST;
-}
-
-// Stores of this workgroup completed (write-through), then one device-scope store of v.
-__device__ __forceinline__ void publish_after_stores(unsigned* p, unsigned v) {
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Diagnostics: atomic max of the 100 MHz clock (or of its bitwise NOT: the earliest start)
 __device__ __forceinline__ void stamp_max(unsigned long long* p, bool negate = false) {
@@ -1257,12 +1220,11 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
   double (*sP)[KB + LDP] = reinterpret_cast<double (*)[KB + LDP]>(sPbuf);
   double (*sPu)[LFM_STEP_KS + LDP] = reinterpret_cast<double (*)[LFM_STEP_KS + LDP]>(sPbuf);
   const int64_t b = blockIdx.x;
-  // roles in blockIdx order: ahead (1), rest (2), tall (3), early (4), each padded to a
-  // multiple of 8
-  const int cnt[4] = {g.na, g.nr, g.nt, g.ne};
+  // roles in blockIdx order: ahead (1), rest (2), tall (3), each padded to a multiple of 8
+  const int cnt[3] = {g.na, g.nr, g.nt};
   int seg = 0;
   int64_t base = 0;
-  while (seg < 3 && b >= base + (cnt[seg] + 7) / 8 * 8) {
+  while (seg < 2 && b >= base + (cnt[seg] + 7) / 8 * 8) {
     base += (cnt[seg] + 7) / 8 * 8;
     ++seg;
   }
@@ -1307,22 +1269,12 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
       c0 = __builtin_amdgcn_s_memtime();
       r0 = __builtin_amdgcn_s_memrealtime();
     }
-    const int64_t ub = u + g.rest_off;
     const bool lead = syrk_unit<true, 64, false, LFM_STEP_KS>(g.A, g.lda, g.s0, g.px, g.kd, g.T,
-                                                              g.wn, g.T, ub, 0, sPu,
+                                                              g.wn, g.T, u + g.rest_off, 0, sPu,
                                                               g.xready ? g.wn + g.lead : 0, g.n,
                                                               g.pad_end, g.zero_from,
-                                                              g.gen.tab ? &g.gen : nullptr,
-                                                              g.pub_lo, g.pub_hi);
+                                                              g.gen.tab ? &g.gen : nullptr);
     if (lead) bump_after_stores(g.xready);
-    if (g.pub_hi > g.pub_lo) {
-      int ti, tj;
-      unit_tile<64>(g.T, g.wn, g.T, ub, 0, &ti, &tj);
-      if (ti / 2 >= g.pub_lo && ti / 2 < g.pub_hi)
-        publish_after_stores(&g.tile_step[tile_index(g.s0 + (int64_t)ti * 64,
-                                                     g.s0 + (int64_t)tj * ST, g.tile_cols)],
-                             (unsigned)g.step + 1u);
-    }
     if (st) {
       __syncthreads();
       stamp_max(st + 1);
@@ -1336,56 +1288,11 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
     }
     return;
   }
-  if (role == 4) {
-    // early unit u of step s + 1 (see StepArgs)
-    int ti, tj;
-    unit_tile<64>(g.e_T, g.e_wn, g.e_T, u, 0, &ti, &tj);
-    const int64_t i0 = g.e_s0 + (int64_t)ti * 64, j0 = g.e_s0 + (int64_t)tj * ST;
-    {
-      __shared__ int ok;
-      if (threadIdx.x == 0) {
-        bool good = spin_until<false>(&g.tile_step[tile_index(i0, j0, g.tile_cols)],
-                                      (unsigned)g.step + 1u, g.spin);
-        if (!good) timeout_at(g.status, 3);
-        const unsigned tw = (unsigned)g.tw;
-        good = good && spin_until<false>(&g.xrow[ti], tw, g.spin);
-        good = good && spin_until<false>(&g.xrow[2 * tj], tw, g.spin);
-        good = good && spin_until<false>(&g.xrow[2 * tj + 1], tw, g.spin);
-        if (!good) timeout_at(g.status, 4);
-        ok = good;
-      }
-      __syncthreads();
-      if (!ok) return;
-    }
-    const Panel pe{g.X, (int64_t)g.tw * NB, g.tr0};
-    const bool lead = syrk_unit<true, 64, false, LFM_STEP_KS, false, true>(
-        g.A, g.lda, g.e_s0, pe, g.tw * NB, g.e_T, g.e_wn, g.e_T, u, 0, sPu,
-        g.e_xready ? g.e_wn + g.e_lead : 0, g.n, g.pad_end, INT64_MAX, nullptr, g.e_pub_lo,
-        g.e_pub_hi);
-    if (lead) bump_after_stores(g.e_xready);
-    if (ti / 2 >= g.e_pub_lo && ti / 2 < g.e_pub_hi)
-      publish_after_stores(&g.tile_step[tile_index(i0, j0, g.tile_cols)], (unsigned)g.step + 2u);
-    if (st) {
-      __syncthreads();
-      stamp_max(st + 3);  // the launch's last unit end
-    }
-    return;
-  }
-  // tall unit (row slab rb, column block cb) of step s + 1: the slabs the early units read
-  // first (write-through, counted), then deepest column blocks first (longest units), so the
-  // launch ends on short ones
-  const int64_t nrb = g.nt / g.tw, xs = g.xrow_slabs;
-  int cb;
-  int64_t rb;
-  if (u < xs * g.tw) {
-    cb = g.tw - 1 - (int)(u / xs);
-    rb = u % xs;
-  } else {
-    const int64_t v = u - xs * g.tw;
-    cb = g.tw - 1 - (int)(v / (nrb - xs));
-    rb = xs + v % (nrb - xs);
-  }
-  const bool xcoh = rb < xs;
+  // tall unit (row slab rb, column block cb) of step s + 1
+  // deepest column blocks first (longest units), so the launch ends on short ones
+  const int64_t nrb = g.nt / g.tw;
+  const int cb = g.tw - 1 - (int)(u / nrb);
+  const int64_t rb = u % nrb;
   const int64_t i0 = g.tr0 + rb * 64;
   if (i0 > g.n && i0 < g.pad_end) return;  // identity padding rows: their X is never read
   {
@@ -1437,25 +1344,13 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
   gemm_accumulate<64, true, true>(g.A + i0 * g.lda + g.tk0, g.lda, g.Bd + cb * NB, W,
                                   NB * (cb + 1), acc, sP);
   double* Xb = g.X + (i0 - g.tr0 + wr + lk) * W + cb * NB + wc + li;
-  if (xcoh) {
-    // read by this launch's early units: write-through, then counted per slab
 #pragma unroll
-    for (int ir = 0; ir < 8; ++ir)
+  for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
-      for (int jr = 0; jr < 4; ++jr) {
-        st1<true>(&Xb[(ir * 4) * W + jr * 16], acc[ir][jr]);
-        if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + cb * NB + wc + jr * 16 + li] = acc[ir][jr];
-      }
-    bump_after_stores(&g.xrow[rb]);
-  } else {
-#pragma unroll
-    for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-      for (int jr = 0; jr < 4; ++jr) {
-        Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
-        if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + cb * NB + wc + jr * 16 + li] = acc[ir][jr];
-      }
-  }
+    for (int jr = 0; jr < 4; ++jr) {
+      Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
+      if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + cb * NB + wc + jr * 16 + li] = acc[ir][jr];
+    }
   if (st) {
     __syncthreads();
     stamp_max(st + 3);
@@ -2210,7 +2105,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   // posterior keeps schedule 1
   const bool s3 = s3_on(ctx) && mode != CHOL_SCHUR;
   ctx->last_sched = s3 ? 3 : 1;
-  ctx->last_early = 0;
   // the bordered matrix's bottom rows [I, 0]: in memory for schedule 1; schedule 3 never reads
   // them before its window reaches them (StepArgs zero_from / copy_from)
   if (bordered && !s3) {
@@ -2291,10 +2185,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     if (!r)
       r = ensure(ctx, (void**)&ctx->linv_full, &ctx->linv_full_bytes, (size_t)NB * NB * sizeof(double));
     if (!r) r = ensure(ctx, (void**)&ctx->xd, &ctx->xd_bytes, (size_t)Wmax * Wmax * sizeof(double));
-    // early units' hand-offs: the last step that updated each (64-row slab, 128-column tile),
-    // and per step the completed column blocks of each 64-row slab of X_s
-    const int64_t slabs = Mp / 64 + 1, tile_cols = (int)Tmax;
-    const size_t nflags = (size_t)S * (3 + Tmax) + (size_t)slabs * tile_cols + (size_t)S * slabs;
+    const size_t nflags = (size_t)S * (3 + Tmax);
     if (!r) r = ensure(ctx, (void**)&ctx->flags, &ctx->flags_bytes, nflags * sizeof(unsigned));
     if (r) return r;
     unsigned* chain_done = ctx->flags;     // [S]
@@ -2304,8 +2195,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     auto xbuf = [&](int s) { return ctx->xbuf + (size_t)(s & 1) * Mp * Wmax; };
     unsigned* bars = a_done + (size_t)S * Tmax;  // [S] grid barrier counters of chain(s)
     unsigned* xready = bars + S;                  // [S] inputs of chain(s) landed (s >= 1)
-    unsigned* tile_step = xready + S;             // [slabs][tile_cols]
-    unsigned* xrow = tile_step + (size_t)slabs * tile_cols;  // [S][slabs]
     auto wkbuf = [&](int s) { return ctx->wk + (size_t)(s & 1) * 2 * Wmax * Wmax; };
     // launch j = s - 2 (step j's update) writes the inputs of chain(s), s >= 2: the block's
     // tiles (leading rest units, w_s (w_s + 1) slabs) and its rows of the columns of super-
@@ -2359,7 +2248,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       return (int)((rows_end(K1) - K1) / 64 * steps[s].second);
     };
     // alg_adjust: algorithmic flops of the step's update done elsewhere (the side-CU helper's
-    // tail, the previous launch's early units) less those of the next step's early units here
+    // tail, its own kernel class)
     auto launch_step = [&](StepArgs& g, double alg_adjust = 0.0) {
       g.n = n;  // padding rows past n are skipped
       g.pad_end = pad_end;
@@ -2367,7 +2256,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       if (!g.copy_from) g.copy_from = INT64_MAX;
       g.spin = ctx->spin_limit;
       const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 + (int64_t)(g.nr + 7) / 8 * 8 +
-                           (int64_t)(g.nt + 7) / 8 * 8 + (int64_t)(g.ne + 7) / 8 * 8;
+                           (int64_t)(g.nt + 7) / 8 * 8;
       if (grid == 0) return;
       // issued: every 64 x 128 unit in full (padding rows included), tall units as GEMMs with
       // the triangular inverse; algorithmic: the update of the unpadded augmented trailing
@@ -2375,8 +2264,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       // the next diagonal block (the chain's), and the triangular solve of the rows below
       // the next super-panel (rows .. n) against its W' x W' factor
       const double issued = ((double)g.na + g.nr) * 64 * ST * 2.0 * g.kd +
-                            (double)g.nt * 64 * ST * NB * (g.tw + 1) +
-                            (double)g.ne * 64 * ST * 2.0 * g.tw * NB;
+                            (double)g.nt * 64 * ST * NB * (g.tw + 1);
       double alg = 0.0;
       if (g.na + g.nr > 0) {
         // bordered: the whole Mp-row window is algorithmic (Cholesky + inverse = Mp^3)
@@ -2489,24 +2377,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       hipEvent_t* evL = ev + 1;  // evL[2 s] = ev[1 + 2 s]: launch s done (main)
       hipEvent_t* evH = ev + 2;  // evH[2 s] = ev[2 + 2 s]: helper(s) done (side)
       bool helped = false;       // the previous step had a helper launch
-      // Early units (LFM_EARLY = RE tile rows at most, MLL): launch s ends with the first
-      // re (re + 1) units of step s + 1's rest enumeration (its triangle rows < re; re a
-      // multiple of the supertile edge, so they are a prefix), which fill the slots launch s's
-      // last units leave idle; launch s + 1 skips them. re = RE capped so the region keeps a
-      // supertile row of the triangle after it and lies above n (no padding rows), for steps
-      // s + 1 of at least LFM_EARLY_WMIN block columns.
-      const int RE = mode == CHOL_MLL && !bordered ? env_int("LFM_EARLY", 0) : 0;
-      const int early_wmin = env_int("LFM_EARLY_WMIN", 4);
-      auto early_rows = [&](int s) -> int {  // launch s runs step s + 1's early units
-        if (RE < LFM_SUPERTILE || s < 0 || s + 2 >= S) return 0;
-        if (steps[s + 1].second < early_wmin) return 0;
-        const int64_t K1n = (steps[s + 1].first + steps[s + 1].second) * NB;
-        const int Tn = (int)((rows_end(K1n) - K1n) / ST), wnn = steps[s + 2].second;
-        int re = std::min(RE, Tn - wnn - LFM_SUPERTILE);
-        re = std::min<int64_t>(re, (n - K1n) / NB - wnn - 1);
-        re = re / LFM_SUPERTILE * LFM_SUPERTILE;
-        return re > 0 ? re : 0;
-      };
       // algorithmic flops (profiling) of rest units [b0, b1) of a step's update: 2 kd per
       // updated lower element of their tiles, rows past n (identity padding) excluded
       auto units_alg = [&](int64_t s0u, int T, int wn, int kd, int64_t b0, int64_t b1) {
@@ -2520,7 +2390,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         }
         return a * 2.0 * kd;
       };
-      ctx->last_early = 0;
       for (int s = 0; s + 1 < S; ++s) {
         chain(s + 1);
         StepArgs g{};
@@ -2533,73 +2402,31 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
           g.xready = xready + s + 2;
           g.lead = steps[s + 2].second;
         }
-        g.tile_step = tile_step;
-        g.tile_cols = (int)tile_cols;
-        g.step = s;
-        const int64_t total = g.nr;                     // the step's rest enumeration
-        const int re_prev = early_rows(s - 1), re = early_rows(s);
-        const int64_t head = (int64_t)re_prev * (re_prev + 1);  // launch s - 1's early units
-        const bool early = re > 0;
-        // triangle rows the helper must not take: chain(s + 2)'s lead tiles, the head (done by
-        // launch s - 1) and the next step's early region (below)
-        int protect = std::max(g.xready ? g.lead : 0, re_prev);
-        if (early) {
-          // step s + 1's early region (its triangle rows < RE) in this step's tile rows
-          StepArgs gn{};
-          update_args(gn, s + 1);
-          g.ne = re * (re + 1);
-          g.e_s0 = gn.s0;
-          g.e_T = gn.T;
-          g.e_wn = gn.wn;
-          if (s + 3 < S) {
-            g.e_xready = xready + s + 3;
-            g.e_lead = steps[s + 3].second;
-          }
-          if (const int re2 = early_rows(s + 1)) {  // step s + 2's early region in these units
-            g.e_pub_lo = gn.wn + steps[s + 3].second;
-            g.e_pub_hi = g.e_pub_lo + re2;
-          }
-          g.pub_lo = g.wn + gn.wn;
-          g.pub_hi = g.pub_lo + re;
-          g.xrow = xrow + (size_t)(s + 1) * slabs;
-          g.xrow_slabs = 2 * (gn.wn + re);
-          protect = std::max(protect, gn.wn + re);
-          ctx->last_early += g.ne;
-        }
         // Side-CU helper (LFM_HELPER): while the factor chain has slack (long launches), the
         // side stream runs the tail of this step's rest units after chain(s + 1), sized so it
         // ends with the main launch; launch s + 1 waits for it, chain(s + 2) follows it. Its
         // units store without write-through and bump no counter, so they never include a lead
-        // tile of chain(s + 2) or a tile the next step's early units read.
-        StepArgs gs = g;  // the helper's sizing sees the units this launch runs
-        gs.nr = (int)(total - head + g.ne);
+        // tile of chain(s + 2).
+        const int64_t total = g.nr;  // the step's rest enumeration
         const int64_t hu = s >= 1 && s + 2 < S
-                               ? helper_clamp(helper_share(gs, steps[s + 1].second), (int)total,
-                                              g.T, g.wn, protect, LFM_SUPERTILE)
+                               ? helper_clamp(helper_share(g, steps[s + 1].second), (int)total,
+                                              g.T, g.wn, g.xready ? g.lead : 0, LFM_SUPERTILE)
                                : 0;
-        g.rest_off = head;
-        g.nr = (int)(total - head - hu);
-        double adj = 0.0;  // profiling: see launch_step
-        double alg_h = 0.0;
-        if (ctx->prof) {
-          if (hu > 0) alg_h = units_alg(g.s0, g.T, g.wn, g.kd, total - hu, total);
-          if (head > 0) adj += units_alg(g.s0, g.T, g.wn, g.kd, 0, head);
-          if (g.ne > 0) adj -= units_alg(g.e_s0, g.e_T, g.e_wn, g.tw * NB, 0, g.ne);
-        }
+        g.nr = (int)(total - hu);
+        const double alg_h =
+            ctx->prof && hu > 0 ? units_alg(g.s0, g.T, g.wn, g.kd, total - hu, total) : 0.0;
         if (helped) hipStreamWaitEvent(main, evH[2 * (s - 1)], 0);
-        launch_step(g, adj + alg_h);
+        launch_step(g, alg_h);
         hipEventRecord(evL[2 * s], main);
         helped = hu > 0;
         if (hu > 0) {
           StepArgs h = g;
           h.na = 0;
           h.nt = 0;
-          h.ne = 0;
           h.rest_off = total - hu;
           h.nr = (int)hu;
           h.stamps = nullptr;
           h.xready = nullptr;  // tail units: never the lead tiles
-          h.pub_lo = h.pub_hi = 0;
           // X_s and step s's C input: launch s - 1 complete
           hipStreamWaitEvent(side, evL[2 * (s - 1)], 0);
           hipEvent_t pe;

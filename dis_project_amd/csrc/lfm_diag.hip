@@ -364,12 +364,6 @@ int lfm_debug_last_schedule(const lfm_ctx* ctx, int* out) {
   return LFM_OK;
 }
 
-int lfm_debug_early_units(const lfm_ctx* ctx, int64_t* out) {
-  if (!ctx || !out) return LFM_E_ARG;
-  *out = ctx->last_early;
-  return LFM_OK;
-}
-
 int lfm_debug_lock_path(const lfm_ctx* ctx, char* buf, int len) {
   if (!ctx || !buf || len < 1) return LFM_E_ARG;
   const std::string p = tenancy_lock_path(ctx->device);

@@ -76,7 +76,6 @@ struct lfm_ctx {
   bool s3_yield = false;                         // this call runs schedule 1: another process
                                                  // holds the device's schedule-3 tenancy
   int last_sched = 0;                            // schedule the last factorisation ran (diag)
-  int64_t last_early = 0;                        // early units it ran ahead of their step (diag)
   bool s3_events = false;                        // schedule 3 ordered by events (LFM_S3_EVENTS)
   unsigned spin_limit = 1u << 26;                // device-side wait bound (LFM_DEBUG_SPIN_LIMIT)
   bool grad_direct = false;                      // gradient: per-pair path only (LFM_GRAD_DIRECT)

@@ -34,10 +34,6 @@ int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max)
  * context runs schedule 1 for a call while another process holds the device's tenancy lock. */
 int lfm_debug_last_schedule(const lfm_ctx* ctx, int* out);
 
-/* Early units of the context's last schedule-3 factorisation: trailing-update units of step
- * s + 1 run at the end of launch s (LFM_EARLY). */
-int lfm_debug_early_units(const lfm_ctx* ctx, int64_t* out);
-
 /* The advisory lock file of the context's device (schedule-3 tenancy across processes). */
 int lfm_debug_lock_path(const lfm_ctx* ctx, char* buf, int len);
 

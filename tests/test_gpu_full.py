@@ -330,81 +330,3 @@ def test_side_cu_helper_forced_on_every_step(monkeypatch, G, T):
     assert out["0"][1] == 0 and out["1"][1] > 0  # the forced run used helper launches
     assert np.isfinite(out["1"][0]) and out["1"][0] == out["0"][0]
 
-
-def _early_units(ctx):
-    from dis_project_amd import _lib
-
-    out = _lib.ctypes.c_int64(0)
-    ctx.check(ctx.diag.lfm_debug_early_units(ctx.handle, _lib.ctypes.byref(out)))
-    return out.value
-
-
-def test_early_units_bit_identical_and_flops_conserved(c2_dev, monkeypatch):
-    """Early units (LFM_EARLY: launch s ends with the first RE (RE + 1) units of step s + 1's
-    trailing update, waiting on device counters for their C tile and their rows of X_{s+1})
-    change where units run, not what they compute: the N = 16384 MLL is bit-identical with
-    them off, and the algorithmic flops booked to the step launches (plus the side-CU helper)
-    are conserved."""
-    from dis_project_amd import _lib
-
-    ctx, work, dx, dy = c2_dev
-    res = {}
-    for re_rows in ("30", "12", "0"):
-        monkeypatch.setenv("LFM_EARLY", re_rows)  # read per call
-        v = np.empty(1)
-        ctx.profile_reset()
-        ctx.profile(True)
-        ctx.check(ctx.lib.lfm_mll_f64_dev(ctx.handle, dx, dy, work.n, work.model.hyp().ref, 0,
-                                          _lib.dptr(v)))
-        ctx.profile(False)
-        st = ctx.profile_read()
-        res[re_rows] = (float(v[0]), st.get("syrk", {}).get("flops", 0.0) +
-                        st.get("syrk_side", {}).get("flops", 0.0), _early_units(ctx))
-    m0, f0, e0 = res["0"]
-    assert e0 == 0 and np.isfinite(m0)
-    for re_rows in ("30", "12"):
-        m, f, e = res[re_rows]
-        assert e > 0, re_rows
-        assert m == m0, (re_rows, m, m0)
-        assert f == pytest.approx(f0, rel=1e-12)
-
-
-@pytest.mark.parametrize("G,T,re_rows,w4,w2", [(16, 256, "6", "1024", "512"),
-                                               (16, 256, "12", "2048", "1024"),
-                                               (20, 200, "6", "512", "256"),
-                                               (24, 256, "18", "1536", "768"),
-                                               (24, 256, "12", "4096", "3072")])
-@pytest.mark.parametrize("helper", ["off", "forced"])
-@pytest.mark.parametrize("wmin", ["4", "1"])
-def test_early_units_small_bulk_plans(monkeypatch, G, T, re_rows, w4, w2, helper, wmin):
-    """Early units on plans with bulk steps at N = 4096 / 4000 (unaligned, padded) / 6144
-    (LFM_W4_MIN / LFM_W2_MIN lowered so the wide super-panels start early), alone and with the
-    side-CU helper forced onto every step (its tail then clamped against the early region), for
-    bulk steps only and for every step width (LFM_EARLY_WMIN=1: the last plan then has early
-    units in its w = 2 and w = 1 steps): the MLL bit-identical to LFM_EARLY=0 and within 1e-9
-    of the oracle."""
-    from dis_project_amd import _lib, configs
-    from oracle import lfm_oracle as O
-
-    work = configs.grid_workload("early", G, T, seed_params=5, seed_y=6)
-    x = np.ascontiguousarray(work.data.X)
-    y = np.ascontiguousarray(work.data.y.reshape(-1))
-    ctx = _lib.get_context(0)
-    monkeypatch.setenv("LFM_W4_MIN", w4)
-    monkeypatch.setenv("LFM_W2_MIN", w2)
-    monkeypatch.setenv("LFM_EARLY_WMIN", wmin)
-    if helper == "forced":
-        monkeypatch.setenv("LFM_HELPER_MIN", "0")
-        monkeypatch.setenv("LFM_HELPER_TC", "0")
-    out = {}
-    for re_val in (re_rows, "0"):
-        monkeypatch.setenv("LFM_EARLY", re_val)
-        v = np.empty(1)
-        ctx.check(ctx.lib.lfm_mll_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
-                                      work.model.hyp().ref, 0, _lib.dptr(v)))
-        out[re_val] = (float(v[0]), _early_units(ctx))
-    assert out["0"][1] == 0 and out[re_rows][1] > 0
-    assert np.isfinite(out["0"][0]) and out[re_rows][0] == out["0"][0]
-    m = work.model
-    ref = O.mll(x, y, m.true_d, m.true_s, m.true_b, m.l, m.obs_stddev, m.jitter)
-    assert abs(out["0"][0] - ref) <= MLL_RTOL * abs(ref)
