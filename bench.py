@@ -535,11 +535,12 @@ def main(argv=None):
                 try:
                     rec = json.load(open(tf))
                     per_eval = rec.get("hbm_bytes_per_eval")
+                    pmc_lpe = rec.get("launches", 0) / max(1, rec.get("evals", 1))
                     traffic = per_eval / (syrk["launches"] / prof_steps) if per_eval else None
                     tsrc = ("PMC (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction) bytes "
                             "per evaluation from profiles/syrk_traffic.json, measured on the "
                             "event-ordered schedule 3 (LFM_S3_EVENTS=1, no side-CU helper: "
-                            f"{rec.get('launches_per_eval', 'n/a')} step launches per eval) - "
+                            f"{pmc_lpe:.0f} step launches per eval) - "
                             "device-side cross-stream waits cannot run under the counters' "
                             "serialised dispatch - divided by this run's "
                             f"{syrk['launches'] // prof_steps} launches per evaluation")
@@ -581,14 +582,26 @@ def main(argv=None):
             # fused (the schedule-3 default on this layout): the gram kernel writes only the
             # first block column and the next super-panel's diagonal block; the first trailing
             # update generates every other Sigma tile from the tables
-            line["gram"] = {
-                "fused": gram["bytes"] < 0.5 * 8.0 * n * (n + 1) / 2 * prof_steps,
-                "kernel": "gram_region_kernel (first block column + next diagonal block; "
-                          "the rest of Sigma is generated inside the first trailing update)",
-                "bytes_per_eval": gram["bytes"] / prof_steps,
-                "ms_per_eval": gram["total_ms"] / prof_steps,
-                "unfused_bytes": 8.0 * n * (n + 1) / 2,
-            }
+            fused = gram["bytes"] < 0.5 * 8.0 * n * (n + 1) / 2 * prof_steps
+            if fused:
+                # no HBM roofline to claim: the fill is no longer a kernel of its own
+                line["gram"] = {
+                    "fused": True,
+                    "kernel": "gram_region_kernel (first block column + next diagonal block; "
+                              "the rest of Sigma is generated inside the first trailing update)",
+                    "bytes_per_eval": gram["bytes"] / prof_steps,
+                    "ms_per_eval": gram["total_ms"] / prof_steps,
+                    "unfused_bytes": 8.0 * n * (n + 1) / 2,
+                }
+            else:  # LFM_GRAM_FUSE=0: the fp64 lower fill as its own kernel
+                gbs = gram["bytes"] / (gram["total_ms"] * 1e-3) / 1e9
+                line["gram_roofline"] = {
+                    "kernel": "gram_grid_aligned_kernel (fp64 lower-triangle fill)",
+                    "bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": gbs / HBM_PEAK_GBS,
+                    "bytes_per_launch": gram["bytes"] / gram["launches"],
+                    "avg_launch_ms": gram["total_ms"] / gram["launches"],
+                }
     if prof and rank == 0 and c4:
         gram = stats.get("gram_grid", {})
         tab = stats.get("tables", {})
