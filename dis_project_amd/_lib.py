@@ -144,6 +144,8 @@ PRODUCT_SIGNATURES = [
 DIAG_SIGNATURES = [
     ("lfm_debug_stamps", c_int, [_c_ctx, c_int, POINTER(ctypes.c_ulonglong), c_int]),
     ("lfm_debug_last_schedule", c_int, [_c_ctx, POINTER(c_int)]),
+    ("lfm_debug_trace", c_int, [_c_ctx, ctypes.c_int64, POINTER(ctypes.c_ulonglong),
+                                ctypes.c_int64, POINTER(ctypes.c_int64)]),
     ("lfm_debug_lock_path", c_int, [_c_ctx, ctypes.c_char_p, c_int]),
     ("lfm_probe_rsq", c_int, [_c_ctx, c_void_p, c_int64, c_void_p]),
     ("lfm_probe_mfma_f64_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr]),

@@ -858,6 +858,78 @@ __device__ __forceinline__ void gemm_accumulate(const double* __restrict__ pi, i
   }
 }
 
+// gemm_accumulate on v_mfma_f64_16x16x4_f64: the same staging and the same products, acc as
+// TR / 32 x 4 blocks of 16 x 16 (acc[rb][jr][r] = C[wr + 16 rb + 4 r + (lane >> 4)][wc + 16 jr
+// + (lane & 15)] — element for element the map of gemm_accumulate's acc[4 rb + r][jr]). Per
+// 4-deep k step a wave issues 2 TR / 64 A and 4 B fragment reads and 2 TR / 16 MFMAs of 2048
+// flops (against 12 reads and 32 MFMAs of 512 flops on the 4x4x4 blocks).
+template <int TR, bool BT = false, bool COH = false, int KS = KB>
+__device__ __forceinline__ void gemm_accumulate16(const double* __restrict__ pi, int64_t ldi,
+                                                  const double* __restrict__ pj, int64_t ldj,
+                                                  int kd, double4v (&acc)[TR / 32][4],
+                                                  double (*__restrict__ sP)[KS + LDP]) {
+  constexpr int RB = TR / 32;
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // opaque: lane offsets are recomputed, not held live
+  const int lane = tid & 63, w = tid >> 6;
+  const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
+  const int li = lane & 15, lk = lane >> 4;
+  static_assert(KS % 16 == 0 && KS <= 64, "stage depth");
+  constexpr int CH = KS / 2, RP = 256 / CH;
+  constexpr int NUI = TR / RP, NUJ = ST / RP, NU = NUI + NUJ;
+  const int srow = tid / CH, sch = tid % CH;
+  const double* gi = pi + srow * ldi + 2 * sch;
+  const double* gj = BT ? pj + (tid >> 6) * ldj + 2 * (tid & 63) : pj + srow * ldj + 2 * sch;
+  const int li32 = (int)(RP * ldi);
+  const int lj32 = BT ? (int)(4 * ldj) : (int)(RP * ldj);
+  double2 pre[NU];
+  auto gload = [&](int k0) {
+    int l32 = li32, m32 = lj32;
+    asm volatile("" : "+v"(l32), "+v"(m32));
+#pragma unroll
+    for (int u = 0; u < NUI; ++u) pre[u] = ld2<COH>(gi + u * l32 + k0);
+    const double* gjk = BT ? gj + (int64_t)k0 * ldj : gj + k0;
+#pragma unroll
+    for (int u = 0; u < NUJ; ++u) pre[NUI + u] = ld2<COH>(gjk + u * m32);
+  };
+  gload(0);
+  for (int k0 = 0; k0 < kd; k0 += KS) {
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NUI; ++u) {
+      double* d = &sP[srow + RP * u][2 * sch];
+      d[0] = pre[u].x;
+      d[1] = pre[u].y;
+    }
+#pragma unroll
+    for (int u = 0; u < NUJ; ++u) {
+      if (BT) {
+        const int kr = (tid >> 6) + 4 * u, jc = 2 * (tid & 63);
+        sP[TR + jc][kr] = pre[NUI + u].x;
+        sP[TR + jc + 1][kr] = pre[NUI + u].y;
+      } else {
+        double* d = &sP[TR + srow + RP * u][2 * sch];
+        d[0] = pre[NUI + u].x;
+        d[1] = pre[NUI + u].y;
+      }
+    }
+    __syncthreads();
+    if (k0 + KS < kd) gload(k0 + KS);
+#pragma unroll LFM_KK_UNROLL
+    for (int kk = 0; kk < KS; kk += 4) {
+      double bb[4], a[RB];
+#pragma unroll
+      for (int jr = 0; jr < 4; ++jr) bb[jr] = sP[TR + wc + jr * 16 + li][kk + lk];
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) a[rb] = sP[wr + rb * 16 + li][kk + lk];
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+        for (int jr = 0; jr < 4; ++jr) acc[rb][jr] = mfma16(a[rb], bb[jr], acc[rb][jr]);
+    }
+  }
+}
+
 // Source of a trailing update's panel rows: matrix row r (k = 0 at the panel's first column)
 // starts at p + (r - r0) * ld. The factor's own block column: {A + kb, lda, 0}; a separate
 // panel buffer holding rows r0 .. : {X, ldx, r0}.
@@ -892,6 +964,10 @@ struct Panel {
 #ifndef LFM_STEP_KS
 #define LFM_STEP_KS 16
 #endif
+// trailing-update tile body on v_mfma_f64_16x16x4_f64 (1) or the 4x4x4_4b blocks (0)
+#ifndef LFM_MFMA16
+#define LFM_MFMA16 1
+#endif
 // C tile loads of the trailing update: device-coherent, or plain / nontemporal (LFM_C_NT bit 0;
 // bit 1: nontemporal C stores)
 #ifndef LFM_C_NT
@@ -921,7 +997,13 @@ __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, P
   double* Cb = A + (i0 + wr + lk) * lda + j0 + wc + li;  // C[wr + lk][wc + li]
   const int ld4 = (int)(4 * lda);  // row-group stride (elements); 60 * ld4 < 2^31 for lda < 2^23
 
+#if LFM_MFMA16
+  double4v acc4[IRN / 4][4];
+#define ACC(ir, jr) acc4[(ir) >> 2][jr][(ir) & 3]
+#else
   double acc[IRN][4];
+#define ACC(ir, jr) acc[ir][jr]
+#endif
   if constexpr (GEN) {
     constexpr int WIN = ST + TR - 1;
     static_assert(4 * WIN + 3 * TR + 3 * ST <= (TR + ST) * (KS + LDP), "gram windows in sP");
@@ -976,7 +1058,7 @@ __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, P
         v = fma(-(sEk[cl] * sEj[rl]), sQk[cl] + sQj[rl], v);
         v = Cjk * v;
         if (i0 + rl == j0 + cl) v = (v + gen->da1) + gen->da2;
-        acc[ir][jr] = -v;
+        ACC(ir, jr) = -v;
         if (jr == 3) __builtin_amdgcn_sched_barrier(0);  // one row group's reads at a time
       }
     __syncthreads();  // the windows are read: sP is the K stages' again
@@ -985,10 +1067,15 @@ __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, P
     for (int ir = 0; ir < IRN; ++ir)
 #pragma unroll
       for (int jr = 0; jr < 4; ++jr)
-        acc[ir][jr] = (CIO && CLOAD) ? -ldc<LDCOH>(&Cb[ir * ld4 + jr * 16]) : 0.0;
+        ACC(ir, jr) = (CIO && CLOAD) ? -ldc<LDCOH>(&Cb[ir * ld4 + jr * 16]) : 0.0;
   }
+#if LFM_MFMA16
+  gemm_accumulate16<TR, false, LDCOH, KS>(P.p + (i0 - P.r0) * P.ld, P.ld,
+                                          P.p + (j0 - P.r0) * P.ld, P.ld, kd, acc4, sP);
+#else
   gemm_accumulate<TR, false, LDCOH, KS>(P.p + (i0 - P.r0) * P.ld, P.ld, P.p + (j0 - P.r0) * P.ld,
                                         P.ld, kd, acc, sP);
+#endif
 
   int ld4s = ld4;
   asm volatile("" : "+v"(ld4s));  // recompute store addresses instead of keeping 64 pointers live
@@ -1000,15 +1087,16 @@ __device__ __forceinline__ void syrk_tile(double* __restrict__ A, int64_t lda, P
       if (CIO && (!diag || col <= row)) {
         // coh: device-coherent (write-through) stores, read by another XCD in flight
         if (coh)
-          __hip_atomic_store(&Cb[ir * ld4s + jr * 16], -acc[ir][jr], __ATOMIC_RELAXED,
+          __hip_atomic_store(&Cb[ir * ld4s + jr * 16], -ACC(ir, jr), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
         else if (LFM_C_NT & 2)
-          __builtin_nontemporal_store(-acc[ir][jr], &Cb[ir * ld4s + jr * 16]);
+          __builtin_nontemporal_store(-ACC(ir, jr), &Cb[ir * ld4s + jr * 16]);
         else
-          Cb[ir * ld4s + jr * 16] = -acc[ir][jr];
+          Cb[ir * ld4s + jr * 16] = -ACC(ir, jr);
       }
-      if (!CIO && acc[ir][jr] == 1.2345e300) Cb[0] = 0.0;  // keep the MFMAs live
+      if (!CIO && ACC(ir, jr) == 1.2345e300) Cb[0] = 0.0;  // keep the MFMAs live
     }
+#undef ACC
 }
 
 // Unit b of a band / triangle enumeration -> (TR-row slab ti, 128-column tile tj), relative
@@ -1197,6 +1285,8 @@ struct StepArgs {
   GramGen gen;       // gen.tab != NULL: the first step's update units generate Sigma (fused gram)
   int64_t rest_off;  // rest units of this launch are [rest_off, rest_off + nr) of the step's
                      // enumeration (the side-CU helper launch takes the tail of it)
+  unsigned long long* trace;  // diagnostics (NULL: off): 4 words per workgroup (lfm_debug_trace)
+  unsigned long long trace_tag;  // launch tag, bits 40+ of each record's last word
 };
 
 // Diagnostics: atomic max of the 100 MHz clock (or of its bitwise NOT: the earliest start)
@@ -1336,6 +1426,16 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
   }
   const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64;
   const int li = lane & 15, lk = lane >> 4;
+#if LFM_MFMA16
+  double4v acc4[2][4];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int jr = 0; jr < 4; ++jr) acc4[rb][jr] = (double4v){0.0, 0.0, 0.0, 0.0};
+  gemm_accumulate16<64, true, true>(g.A + i0 * g.lda + g.tk0, g.lda, g.Bd + cb * NB, W,
+                                    NB * (cb + 1), acc4, sP);
+#define ACC(ir, jr) acc4[(ir) >> 2][jr][(ir) & 3]
+#else
   double acc[8][4];
 #pragma unroll
   for (int ir = 0; ir < 8; ++ir)
@@ -1343,18 +1443,48 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
     for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = 0.0;
   gemm_accumulate<64, true, true>(g.A + i0 * g.lda + g.tk0, g.lda, g.Bd + cb * NB, W,
                                   NB * (cb + 1), acc, sP);
+#define ACC(ir, jr) acc[ir][jr]
+#endif
   double* Xb = g.X + (i0 - g.tr0 + wr + lk) * W + cb * NB + wc + li;
 #pragma unroll
   for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) {
-      Xb[(ir * 4) * W + jr * 16] = acc[ir][jr];
-      if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + cb * NB + wc + jr * 16 + li] = acc[ir][jr];
+      Xb[(ir * 4) * W + jr * 16] = ACC(ir, jr);
+      if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + cb * NB + wc + jr * 16 + li] = ACC(ir, jr);
     }
+#undef ACC
   if (st) {
     __syncthreads();
     stamp_max(st + 3);
     add_dur(6);
+  }
+}
+
+// Diagnostics (lfm_debug_trace): per workgroup {entry, exit} (s_memrealtime), the hardware
+// id (HW_ID | XCC_ID << 32) and the launch tag | role << 32 | unit (role 0: padding)
+__device__ __forceinline__ void step_traced(const StepArgs& g) {
+  __shared__ unsigned long long t0;  // in LDS: nothing held in registers across the body
+  if (threadIdx.x == 0) t0 = __builtin_amdgcn_s_memrealtime();
+  step_body(g);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int64_t b = blockIdx.x;
+    const int64_t pa = (g.na + 7) / 8 * 8, pr = (g.nr + 7) / 8 * 8;
+    const int seg = b < pa ? 0 : b < pa + pr ? 1 : 2;
+    const int64_t base = seg == 0 ? 0 : seg == 1 ? pa : pa + pr;
+    int64_t lo, hi;
+    xcd_range(seg == 0 ? g.na : seg == 1 ? g.nr : g.nt, (int)(b % 8), &lo, &hi);
+    const int64_t u = lo + (b - base) / 8;
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    unsigned long long* r = g.trace + 4 * b;
+    r[0] = t0;
+    r[1] = __builtin_amdgcn_s_memrealtime();
+    r[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+    r[3] = (g.trace_tag << 40) | ((unsigned long long)(u < hi ? seg + 1 : 0) << 32) |
+           (unsigned long long)(u < hi ? u : 0);
   }
 }
 
@@ -1363,6 +1493,12 @@ __global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) { step_body(g)
 // The side-CU helper's launches (rest units only): the same body under its own name, so
 // traces and counters keep the main-stream step launches apart
 __global__ __launch_bounds__(256, 4) void helper_update_kernel(StepArgs g) { step_body(g); }
+// Both with the unit trace (lfm_debug_trace on): separate symbols, so the product kernels'
+// code is the untraced body
+__global__ __launch_bounds__(256, 4) void step_kernel_traced(StepArgs g) { step_traced(g); }
+__global__ __launch_bounds__(256, 4) void helper_update_kernel_traced(StepArgs g) {
+  step_traced(g);
+}
 
 // ---------------------------------------------------------- fused panel
 // One block column of the look-ahead chain in one launch (w = 1 steps):
@@ -2073,6 +2209,17 @@ bool chol_fuses_gram(const lfm_ctx* ctx, int mode, const GridLayout& lay, int64_
          s3_on(ctx) && mode != CHOL_SCHUR;
 }
 
+// Diagnostics: the next region of the unit trace (lfm_debug_trace) for a launch of `grid`
+// workgroups, tagged with the launch count (bit 23: a side-CU helper launch); none while the
+// trace is off or full
+static void trace_launch(lfm_ctx* ctx, StepArgs& g, int64_t grid, bool helper) {
+  g.trace = nullptr;
+  if (!ctx->dbg_trace || ctx->dbg_trace_cur + grid > ctx->dbg_trace_cap) return;
+  g.trace = ctx->dbg_trace + 4 * ctx->dbg_trace_cur;
+  g.trace_tag = (unsigned long long)(ctx->dbg_trace_launch++ & 0x7fffff) | (helper ? 1ull << 23 : 0);
+  ctx->dbg_trace_cur += grid;
+}
+
 int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t Mp, int negative,
                       double* d_out, int mode, const GramGen* gen) {
   static bool attr = false;
@@ -2278,9 +2425,11 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         alg += (double)std::max<int64_t>(0, rows) * W2 * W2;
       }
       alg -= alg_adjust;
+      trace_launch(ctx, g, grid, false);
       hipEvent_t pe;
       prof_begin(ctx, K_SYRK, &pe, main);
-      hipLaunchKernelGGL(step_kernel, dim3((unsigned)grid), dim3(256), 0, main, g);
+      hipLaunchKernelGGL(g.trace ? step_kernel_traced : step_kernel, dim3((unsigned)grid),
+                         dim3(256), 0, main, g);
       prof_end(ctx, K_SYRK, pe, alg, 0, main, issued);
     };
     auto tall_args = [&](StepArgs& g, int s) {  // tall part of the step launch: step s's rows
@@ -2427,12 +2576,13 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
           h.nr = (int)hu;
           h.stamps = nullptr;
           h.xready = nullptr;  // tail units: never the lead tiles
+          trace_launch(ctx, h, (hu + 7) / 8 * 8, true);
           // X_s and step s's C input: launch s - 1 complete
           hipStreamWaitEvent(side, evL[2 * (s - 1)], 0);
           hipEvent_t pe;
           prof_begin(ctx, K_SIDE_SYRK, &pe, side);
-          hipLaunchKernelGGL(helper_update_kernel, dim3((unsigned)((hu + 7) / 8 * 8)), dim3(256),
-                             0, side, h);
+          hipLaunchKernelGGL(h.trace ? helper_update_kernel_traced : helper_update_kernel,
+                             dim3((unsigned)((hu + 7) / 8 * 8)), dim3(256), 0, side, h);
           prof_end(ctx, K_SIDE_SYRK, pe, alg_h, 0, side, (double)hu * 64 * ST * 2.0 * g.kd);
           hipEventRecord(evH[2 * s], side);
         }

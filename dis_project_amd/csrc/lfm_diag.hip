@@ -358,6 +358,41 @@ int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max)
   return hip_fail(ctx, e, "debug stamps");
 }
 
+// cap > 0 turns on the step-kernel unit trace for the next `cap` workgroups (4 words each:
+// entry / exit s_memrealtime, HW_ID | XCC_ID << 32, launch tag << 40 | role << 32 | unit);
+// cap = 0 copies out min(written, max) records, reports how many were written and turns it off.
+int lfm_debug_trace(lfm_ctx* ctx, int64_t cap, unsigned long long* out, int64_t max,
+                    int64_t* written) {
+  if (!ctx || cap < 0) return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  if (cap > 0) {
+    if (ctx->dbg_trace) hipFree(ctx->dbg_trace);
+    ctx->dbg_trace = nullptr;
+    hipError_t e = hipMalloc((void**)&ctx->dbg_trace, (size_t)cap * 32);
+    if (e == hipSuccess) e = hipMemsetAsync(ctx->dbg_trace, 0, (size_t)cap * 32, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+      hipFree(ctx->dbg_trace);
+      ctx->dbg_trace = nullptr;
+      return hip_fail(ctx, e, "debug trace");
+    }
+    ctx->dbg_trace_cap = cap;
+    ctx->dbg_trace_cur = 0;
+    ctx->dbg_trace_launch = 0;
+    return LFM_OK;
+  }
+  if (written) *written = ctx->dbg_trace_cur;
+  if (!ctx->dbg_trace) return LFM_OK;
+  hipError_t e = hipDeviceSynchronize();
+  const int64_t nrec = std::min<int64_t>(ctx->dbg_trace_cur, std::max<int64_t>(max, 0));
+  if (e == hipSuccess && out && nrec > 0)
+    e = hipMemcpy(out, ctx->dbg_trace, (size_t)nrec * 32, hipMemcpyDeviceToHost);
+  hipFree(ctx->dbg_trace);
+  ctx->dbg_trace = nullptr;
+  ctx->dbg_trace_cap = ctx->dbg_trace_cur = 0;
+  return hip_fail(ctx, e, "debug trace");
+}
+
 int lfm_debug_last_schedule(const lfm_ctx* ctx, int* out) {
   if (!ctx || !out) return LFM_E_ARG;
   *out = ctx->last_sched;

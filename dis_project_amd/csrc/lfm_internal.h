@@ -86,6 +86,9 @@ struct lfm_ctx {
 
   unsigned long long* dbg_stamps = nullptr;     // lfm_debug_stamps: chain phases 256 x 16, then
                                                 // step launches 256 x 8
+  unsigned long long* dbg_trace = nullptr;      // lfm_debug_trace: 4 words per step-kernel unit
+  int64_t dbg_trace_cap = 0, dbg_trace_cur = 0;  // records allocated / written
+  unsigned dbg_trace_launch = 0;                 // launches traced so far
 
   // pinned host staging
   double* hpin = nullptr; size_t hpin_bytes = 0;

@@ -30,6 +30,14 @@ extern "C" {
  * values out and disarms. */
 int lfm_debug_stamps(lfm_ctx* ctx, int enable, unsigned long long* out, int max);
 
+/* Per-workgroup trace of the schedule-3 step and helper launches. cap > 0 arms it for the next
+ * cap workgroups (later launches untraced); cap = 0 copies min(written, max) records of four
+ * words out — entry and exit s_memrealtime (100 MHz), HW_ID | XCC_ID << 32, and launch tag
+ * << 40 | role << 32 | unit (tag: launch count, bit 23 set on helper launches; role 1 ahead,
+ * 2 rest, 3 tall, 0 padding) — stores the count written in *written and disarms. */
+int lfm_debug_trace(lfm_ctx* ctx, int64_t cap, unsigned long long* out, int64_t max,
+                    int64_t* written);
+
 /* The schedule (1 or 3) the context's last factorisation ran; 0 before the first. A schedule-3
  * context runs schedule 1 for a call while another process holds the device's tenancy lock. */
 int lfm_debug_last_schedule(const lfm_ctx* ctx, int* out);
