@@ -863,25 +863,27 @@ __device__ __forceinline__ void gemm_accumulate(const double* __restrict__ pi, i
 // + (lane & 15)] — element for element the map of gemm_accumulate's acc[4 rb + r][jr]). Per
 // 4-deep k step a wave issues 2 TR / 64 A and 4 B fragment reads and 2 TR / 16 MFMAs of 2048
 // flops (against 12 reads and 32 MFMAs of 512 flops on the 4x4x4 blocks).
-template <int TR, bool BT = false, bool COH = false, int KS = KB>
+template <int TR, bool BT = false, bool COH = false, int KS = KB, int CW = ST>
 __device__ __forceinline__ void gemm_accumulate16(const double* __restrict__ pi, int64_t ldi,
                                                   const double* __restrict__ pj, int64_t ldj,
-                                                  int kd, double4v (&acc)[TR / 32][4],
+                                                  int kd, double4v (&acc)[TR / 32][CW / 32],
                                                   double (*__restrict__ sP)[KS + LDP]) {
-  constexpr int RB = TR / 32;
+  constexpr int RB = TR / 32, JB = CW / 32;  // 16 x 16 blocks per wave: RB rows, JB columns
+  constexpr int CPR = CW / 2;                 // K-major j panel: double2 chunks per k row
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));  // opaque: lane offsets are recomputed, not held live
   const int lane = tid & 63, w = tid >> 6;
-  const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * 64;
+  const int wr = (w >> 1) * (TR / 2), wc = (w & 1) * (CW / 2);
   const int li = lane & 15, lk = lane >> 4;
   static_assert(KS % 16 == 0 && KS <= 64, "stage depth");
   constexpr int CH = KS / 2, RP = 256 / CH;
-  constexpr int NUI = TR / RP, NUJ = ST / RP, NU = NUI + NUJ;
+  constexpr int NUI = TR / RP, NUJ = CW / RP, NU = NUI + NUJ;
+  static_assert(BT ? KS * CPR == 256 * NUJ : true, "K-major staging");
   const int srow = tid / CH, sch = tid % CH;
   const double* gi = pi + srow * ldi + 2 * sch;
-  const double* gj = BT ? pj + (tid >> 6) * ldj + 2 * (tid & 63) : pj + srow * ldj + 2 * sch;
+  const double* gj = BT ? pj + (tid / CPR) * ldj + 2 * (tid % CPR) : pj + srow * ldj + 2 * sch;
   const int li32 = (int)(RP * ldi);
-  const int lj32 = BT ? (int)(4 * ldj) : (int)(RP * ldj);
+  const int lj32 = BT ? (int)((256 / CPR) * ldj) : (int)(RP * ldj);
   double2 pre[NU];
   auto gload = [&](int k0) {
     int l32 = li32, m32 = lj32;
@@ -904,7 +906,7 @@ __device__ __forceinline__ void gemm_accumulate16(const double* __restrict__ pi,
 #pragma unroll
     for (int u = 0; u < NUJ; ++u) {
       if (BT) {
-        const int kr = (tid >> 6) + 4 * u, jc = 2 * (tid & 63);
+        const int kr = tid / CPR + (256 / CPR) * u, jc = 2 * (tid % CPR);
         sP[TR + jc][kr] = pre[NUI + u].x;
         sP[TR + jc + 1][kr] = pre[NUI + u].y;
       } else {
@@ -917,15 +919,15 @@ __device__ __forceinline__ void gemm_accumulate16(const double* __restrict__ pi,
     if (k0 + KS < kd) gload(k0 + KS);
 #pragma unroll LFM_KK_UNROLL
     for (int kk = 0; kk < KS; kk += 4) {
-      double bb[4], a[RB];
+      double bb[JB], a[RB];
 #pragma unroll
-      for (int jr = 0; jr < 4; ++jr) bb[jr] = sP[TR + wc + jr * 16 + li][kk + lk];
+      for (int jr = 0; jr < JB; ++jr) bb[jr] = sP[TR + wc + jr * 16 + li][kk + lk];
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb) a[rb] = sP[wr + rb * 16 + li][kk + lk];
 #pragma unroll
       for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
-        for (int jr = 0; jr < 4; ++jr) acc[rb][jr] = mfma16(a[rb], bb[jr], acc[rb][jr]);
+        for (int jr = 0; jr < JB; ++jr) acc[rb][jr] = mfma16(a[rb], bb[jr], acc[rb][jr]);
     }
   }
 }
@@ -967,6 +969,14 @@ struct Panel {
 // trailing-update tile body on v_mfma_f64_16x16x4_f64 (1) or the 4x4x4_4b blocks (0)
 #ifndef LFM_MFMA16
 #define LFM_MFMA16 1
+#endif
+// tall units (X_{s+1} = A21 Bd) in 64 x (128 / LFM_TALL_SPLIT) pieces
+#ifndef LFM_TALL_SPLIT
+#define LFM_TALL_SPLIT 2
+#endif
+// tall units dealt round-robin to the XCDs (1) or in contiguous ranges like the other roles (0)
+#ifndef LFM_TALL_RR
+#define LFM_TALL_RR 1
 #endif
 // C tile loads of the trailing update: device-coherent, or plain / nontemporal (LFM_C_NT bit 0;
 // bit 1: nontemporal C stores)
@@ -1297,6 +1307,24 @@ __device__ __forceinline__ void stamp_max(unsigned long long* p, bool negate = f
   }
 }
 
+// Unit of workgroup b (offset within its role's segment) of a step launch: *u, and *end (u >=
+// *end: padding). Ahead and rest units are dealt to the XCDs in contiguous ranges (panel
+// sharing in each XCD's L2); the tall units round-robin, so every XCD gets the same mix of
+// depths, deepest first (contiguous ranges gave one XCD all the deepest column block and made
+// it the launch's last by a whole unit: profiles/r03_unit_trace_*).
+__device__ __forceinline__ void tall_or_xcd_range(int seg, int64_t cnt, int64_t b, int64_t* u,
+                                                  int64_t* end) {
+  if (seg == 2 && LFM_TALL_RR) {
+    *u = b;
+    *end = cnt;
+    return;
+  }
+  int64_t lo, hi;
+  xcd_range(cnt, (int)(b % 8), &lo, &hi);
+  *u = lo + b / 8;
+  *end = hi;
+}
+
 __device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
   __builtin_amdgcn_s_waitcnt(0);  // this thread's write-through stores have completed
   __syncthreads();
@@ -1319,8 +1347,8 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
     ++seg;
   }
   int64_t lo, hi;
-  xcd_range(cnt[seg], (int)(b % 8), &lo, &hi);
-  const int64_t u = lo + (b - base) / 8;
+  tall_or_xcd_range(seg, cnt[seg], b - base, &lo, &hi);
+  const int64_t u = lo;
   if (u >= hi) return;
   const int role = seg + 1;
   unsigned long long* const st = g.stamps;
@@ -1378,11 +1406,15 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
     }
     return;
   }
-  // tall unit (row slab rb, column block cb) of step s + 1
-  // deepest column blocks first (longest units), so the launch ends on short ones
-  const int64_t nrb = g.nt / g.tw;
-  const int cb = g.tw - 1 - (int)(u / nrb);
-  const int64_t rb = u % nrb;
+  // tall unit (row slab rb, column block cb, its part hf of LFM_TALL_SPLIT) of step s + 1:
+  // deepest column blocks first (longest units), so the launch ends on short ones; the split
+  // halves a unit's width so the launch's last round drains in shorter pieces
+  constexpr int TCW = NB / LFM_TALL_SPLIT;  // output columns per tall unit
+  const int64_t nrb = g.nt / (g.tw * LFM_TALL_SPLIT);
+  const int cb = g.tw - 1 - (int)(u / (nrb * LFM_TALL_SPLIT));
+  const int64_t rq = u % (nrb * LFM_TALL_SPLIT);
+  const int64_t rb = rq / LFM_TALL_SPLIT;
+  const int c0 = cb * NB + (int)(rq % LFM_TALL_SPLIT) * TCW;  // first output column in X_{s+1}
   const int64_t i0 = g.tr0 + rb * 64;
   if (i0 > g.n && i0 < g.pad_end) return;  // identity padding rows: their X is never read
   {
@@ -1410,11 +1442,11 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (i0 >= g.copy_from) {
     // border rows: X = e_{row - copy_from} Bd, the row of Bd (written through by the chain)
-    const double* src = g.Bd + (i0 - g.copy_from) * W + cb * NB;
-    double* dst = g.X + (i0 - g.tr0) * W + cb * NB;
+    const double* src = g.Bd + (i0 - g.copy_from) * W + c0;
+    double* dst = g.X + (i0 - g.tr0) * W + c0;
 #pragma unroll 4
-    for (int u = 0; u < 64 * NB / 2 / 256; ++u) {
-      const int idx = tid + 256 * u, r = idx / (NB / 2), c2 = 2 * (idx % (NB / 2));
+    for (int u = 0; u < 64 * TCW / 2 / 256; ++u) {
+      const int idx = tid + 256 * u, r = idx / (TCW / 2), c2 = 2 * (idx % (TCW / 2));
       *reinterpret_cast<double2*>(&dst[r * W + c2]) = ld2<true>(&src[(int64_t)r * W + c2]);
     }
     if (st) {
@@ -1424,18 +1456,20 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
     }
     return;
   }
-  const int wr = (wv >> 1) * 32, wc = (wv & 1) * 64;
+  const int wr = (wv >> 1) * 32, wc = (wv & 1) * (TCW / 2);
   const int li = lane & 15, lk = lane >> 4;
+  constexpr int JR = TCW / 32;  // 16-column blocks per wave
 #if LFM_MFMA16
-  double4v acc4[2][4];
+  double4v acc4[2][JR];
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-    for (int jr = 0; jr < 4; ++jr) acc4[rb][jr] = (double4v){0.0, 0.0, 0.0, 0.0};
-  gemm_accumulate16<64, true, true>(g.A + i0 * g.lda + g.tk0, g.lda, g.Bd + cb * NB, W,
-                                    NB * (cb + 1), acc4, sP);
+    for (int jr = 0; jr < JR; ++jr) acc4[rb][jr] = (double4v){0.0, 0.0, 0.0, 0.0};
+  gemm_accumulate16<64, true, true, KB, TCW>(g.A + i0 * g.lda + g.tk0, g.lda, g.Bd + c0, W,
+                                             NB * (cb + 1), acc4, sP);
 #define ACC(ir, jr) acc4[(ir) >> 2][jr][(ir) & 3]
 #else
+  static_assert(TCW == NB, "the 4x4x4 tile body has no split tall units");
   double acc[8][4];
 #pragma unroll
   for (int ir = 0; ir < 8; ++ir)
@@ -1445,13 +1479,13 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
                                   NB * (cb + 1), acc, sP);
 #define ACC(ir, jr) acc[ir][jr]
 #endif
-  double* Xb = g.X + (i0 - g.tr0 + wr + lk) * W + cb * NB + wc + li;
+  double* Xb = g.X + (i0 - g.tr0 + wr + lk) * W + c0 + wc + li;
 #pragma unroll
   for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
-    for (int jr = 0; jr < 4; ++jr) {
+    for (int jr = 0; jr < JR; ++jr) {
       Xb[(ir * 4) * W + jr * 16] = ACC(ir, jr);
-      if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + cb * NB + wc + jr * 16 + li] = ACC(ir, jr);
+      if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + c0 + wc + jr * 16 + li] = ACC(ir, jr);
     }
 #undef ACC
   if (st) {
@@ -1474,8 +1508,8 @@ __device__ __forceinline__ void step_traced(const StepArgs& g) {
     const int seg = b < pa ? 0 : b < pa + pr ? 1 : 2;
     const int64_t base = seg == 0 ? 0 : seg == 1 ? pa : pa + pr;
     int64_t lo, hi;
-    xcd_range(seg == 0 ? g.na : seg == 1 ? g.nr : g.nt, (int)(b % 8), &lo, &hi);
-    const int64_t u = lo + (b - base) / 8;
+    tall_or_xcd_range(seg, seg == 0 ? g.na : seg == 1 ? g.nr : g.nt, b - base, &lo, &hi);
+    const int64_t u = lo;
     unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -2180,7 +2214,7 @@ int probe_update_launch(lfm_ctx* ctx, hipStream_t st, int T, int kd, int cio, in
       g.tw = 1;
       g.tr0 = 512 + ST;
       g.tk0 = 0;
-      g.nt = 2 * (T - 1);
+      g.nt = 2 * (T - 1) * LFM_TALL_SPLIT;
       g.Bd = ctx->A;
       g.X = xs + xb / 8;
       g.zvec = xs;
@@ -2392,7 +2426,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     // tall units of step s: rows [K1_s, Mp) x w_s column blocks
     auto tall_units = [&](int s) {
       const int64_t K1 = (steps[s].first + steps[s].second) * NB;
-      return (int)((rows_end(K1) - K1) / 64 * steps[s].second);
+      return (int)((rows_end(K1) - K1) / 64 * steps[s].second * LFM_TALL_SPLIT);
     };
     // alg_adjust: algorithmic flops of the step's update done elsewhere (the side-CU helper's
     // tail, its own kernel class)
@@ -2411,7 +2445,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       // the next diagonal block (the chain's), and the triangular solve of the rows below
       // the next super-panel (rows .. n) against its W' x W' factor
       const double issued = ((double)g.na + g.nr) * 64 * ST * 2.0 * g.kd +
-                            (double)g.nt * 64 * ST * NB * (g.tw + 1);
+                            (double)g.nt * 64 * (ST / LFM_TALL_SPLIT) * NB * (g.tw + 1);
       double alg = 0.0;
       if (g.na + g.nr > 0) {
         // bordered: the whole Mp-row window is algorithmic (Cholesky + inverse = Mp^3)
@@ -2476,8 +2510,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     const double helper_min = env_int("LFM_HELPER_MIN", 1200);  // smallest D0 helped, us
     auto helper_share = [&](const StepArgs& g, int wnext) -> int64_t {
       if (!helper_on) return 0;
-      return helper_units(g.kd, g.na, g.nr, g.nt, wnext, NB, ctx->cus, ctx->side_cus, helper_tc,
-                          helper_min);
+      return helper_units(g.kd, g.na, g.nr, g.nt / LFM_TALL_SPLIT, wnext, NB, ctx->cus,
+                          ctx->side_cus, helper_tc, helper_min);
     };
     // side: chain(0) after the gram; every later chain(s) follows chain(s - 1) in stream order
     // and waits on the device for its inputs (xready[s]) from the main launch in flight

@@ -22,6 +22,7 @@ from dis_project_amd import _lib, configs  # noqa: E402
 
 NB = 128
 SLOTS = 4 * 224  # resident step-kernel workgroups: 4 per main-stream CU (32 side CUs)
+TALL_SPLIT = 2  # tall units per 64-row x 128-column block of X (lfm_chol.hip LFM_TALL_SPLIT)
 
 
 def plan(n, bordered=False):
@@ -121,7 +122,7 @@ def main():
         K1n = K1 + wn * NB
         rows_t = (Mp if not grad else 2 * Mp) - K1n
         nt_all = rows_t // 64 * wn
-        nt = nt_all if grad else ((n + 1 - K1n + 63) // 64) * wn
+        nt = (nt_all if grad else ((n + 1 - K1n + 63) // 64) * wn) * TALL_SPLIT
         tall_us = float(sp[s][6]) * 0.01 / nt if nt > 0 else 0.0
         ahead_us = float(sp[s][7]) * 0.01 / na if na > 0 else 0.0
         # slot occupancy over the launch: summed unit time / (slots x launch span)
