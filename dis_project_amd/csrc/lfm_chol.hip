@@ -974,6 +974,10 @@ struct Panel {
 #ifndef LFM_TALL_SPLIT
 #define LFM_TALL_SPLIT 2
 #endif
+// the chain's 32 x 32 products (gemm32) on v_mfma_f64_16x16x4_f64 (1) or 4x4x4_4b (0)
+#ifndef LFM_G32_M16
+#define LFM_G32_M16 1
+#endif
 // tall units dealt round-robin to the XCDs (1) or in contiguous ranges like the other roles (0)
 #ifndef LFM_TALL_RR
 #define LFM_TALL_RR 1
@@ -1186,7 +1190,6 @@ __device__ __forceinline__ bool syrk_unit(double* __restrict__ A, int64_t lda, i
                                           int64_t pad_end = INT64_MAX,
                                           int64_t zero_from = INT64_MAX,
                                           const GramGen* gen = nullptr) {
-  constexpr int SUB = ST / TR;  // row tiles per 128 rows
   int ti, tj;  // ti in TR-row units
   unit_tile<TR>(T, tj_lo, tj_hi, b, ti0, &ti, &tj);
 
@@ -1735,12 +1738,20 @@ __device__ __forceinline__ void gemm32(const double* __restrict__ pi, int64_t ld
   int tid = threadIdx.x;
   asm volatile("" : "+v"(tid));  // opaque: index math is redone per call, not hoisted and held
   const int lane = tid & 63, w = tid >> 6;
-  const int li = lane & 15, lk = lane >> 4, l3 = lane & 3;
+  const int li = lane & 15, lk = lane >> 4;
   double* sA = smem;             // [32][G32K]: P rows
   double* sB = smem + 32 * G32K;  // [32][G32K]: Q columns (j-major)
+#if LFM_G32_M16
+  double4v acc4[2][2];  // 16 x 16 blocks: acc4[rb][jr][r] = element (16 rb + 4 r + lk, 16 jr + li)
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) acc4[rb][0] = acc4[rb][1] = (double4v){0.0, 0.0, 0.0, 0.0};
+#define ACC(ir, jr) acc4[(ir) >> 2][jr][(ir) & 3]
+#else
   double acc[8][2];
 #pragma unroll
   for (int ir = 0; ir < 8; ++ir) acc[ir][0] = acc[ir][1] = 0.0;
+#define ACC(ir, jr) acc[ir][jr]
+#endif
   double2 pre[16];
   auto gload = [&](int k0) {
 #pragma unroll
@@ -1775,14 +1786,22 @@ __device__ __forceinline__ void gemm32(const double* __restrict__ pi, int64_t ld
 #pragma unroll
     for (int kk = 32 * w; kk < 32 * w + 32; kk += 4) {
       const double b0 = sB[li * G32K + kk + lk], b1 = sB[(16 + li) * G32K + kk + lk];
+#if LFM_G32_M16
+      const double a0 = sA[li * G32K + kk + lk], a1 = sA[(16 + li) * G32K + kk + lk];
+      acc4[0][0] = mfma16(a0, b0, acc4[0][0]);
+      acc4[0][1] = mfma16(a0, b1, acc4[0][1]);
+      acc4[1][0] = mfma16(a1, b0, acc4[1][0]);
+      acc4[1][1] = mfma16(a1, b1, acc4[1][1]);
+#else
       double a[8];
 #pragma unroll
-      for (int ir = 0; ir < 8; ++ir) a[ir] = sA[(ir * 4 + l3) * G32K + kk + lk];
+      for (int ir = 0; ir < 8; ++ir) a[ir] = sA[(ir * 4 + (lane & 3)) * G32K + kk + lk];
 #pragma unroll
       for (int ir = 0; ir < 8; ++ir) {
         acc[ir][0] = mfma4(a[ir], b0, acc[ir][0]);
         acc[ir][1] = mfma4(a[ir], b1, acc[ir][1]);
       }
+#endif
     }
   }
   __syncthreads();  // operand reads done: the partials alias them
@@ -1790,7 +1809,8 @@ __device__ __forceinline__ void gemm32(const double* __restrict__ pi, int64_t ld
 #pragma unroll
   for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
-    for (int jr = 0; jr < 2; ++jr) red[(w * 32 + ir * 4 + lk) * 33 + jr * 16 + li] = acc[ir][jr];
+    for (int jr = 0; jr < 2; ++jr) red[(w * 32 + ir * 4 + lk) * 33 + jr * 16 + li] = ACC(ir, jr);
+#undef ACC
   __syncthreads();
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
