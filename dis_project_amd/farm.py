@@ -187,10 +187,12 @@ class Farm:
                                                           [datasets[i] for i in idx]))
 
 
-# Measured C3 throughput on one MI355X at N = 16384, evaluations / s with c
-# schedule-1 evaluations in flight, and one schedule-3 evaluation at a time
-_S1_RATE = {1: 29.1, 2: 35.8, 3: 37.3, 4: 37.0}
-_S3_RATE = 34.6
+# Measured C3 throughput on one MI355X at N = 16384 (scripts/concurrency_probe.py,
+# profiles/r03_concurrency.json), evaluations / s with c schedule-1 evaluations in flight, and
+# one schedule-3 evaluation at a time. Round 3's faster schedule-3 kernels put one schedule-3
+# evaluation at a time ahead of every concurrent count.
+_S1_RATE = {1: 28.6, 2: 33.8, 3: 35.3, 4: 33.7}
+_S3_RATE = 36.6
 
 
 def predicted_seconds(k: int, workers: int) -> float:
@@ -207,8 +209,9 @@ def predicted_seconds(k: int, workers: int) -> float:
 
 def choose_workers(k: int, max_workers: int = 4) -> int:
     """Evaluations in flight for a rank that owns k restarts of one large dataset: the count
-    with the shortest predicted wall time (ties: fewer contexts). 32 -> 3, 16 / 8 / 4 -> 4 (so
-    the 8-GPU split's 4 restarts per rank run as one round of 4, not 3 then 1)."""
+    with the shortest predicted wall time (ties: fewer contexts). With the round-3 rates every
+    share (32, 16, 8, 4 restarts) runs one schedule-3 evaluation at a time, so no rank runs an
+    uneven remainder round (the round-2 rates chose 3 for 32 and 4 for the 8-GPU split's 4)."""
     best = 1
     for w in range(2, max(1, min(max_workers, k)) + 1):
         if predicted_seconds(k, w) < predicted_seconds(k, best) - 1e-9:
