@@ -342,6 +342,10 @@ def main(argv=None):
     a = parse(argv)
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         return self_launch(a, argv)
+    if os.environ.get("LFM_BENCH_WATCHDOG"):
+        # diagnostics: dump every thread's Python stack (and exit) if the run outlives this
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["LFM_BENCH_WATCHDOG"]), exit=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -361,12 +365,30 @@ def main(argv=None):
     lib, h = ctx.lib, ctx.handle
 
     # farm communicator (replicas-only exchange of per-rank results)
+    exchange = a.gather
     if world > 1 and a.gather == "gloo":
         gather = farm.TorchGather(world)
     elif world > 1:
         obj = [farm.RcclGather.unique_id(ctx) if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        gather = farm.RcclGather(ctx, world, rank, obj[0])
+        err = None
+        try:
+            # non-blocking communicator, every wait bounded (LFM_RCCL_TIMEOUT_S)
+            gather = farm.RcclGather(ctx, world, rank, obj[0])
+        except Exception as e:  # noqa: BLE001 — every rank must learn of any rank's failure
+            err = e
+        ok = torch.tensor([0 if err is not None else 1], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if not int(ok.item()):
+            # one rank's communicator failed: all ranks exchange over gloo instead, and the
+            # line says so (the evaluations themselves are unaffected)
+            if err is None:
+                gather.close()
+            print(f"rank {rank}: RCCL communicator unavailable "
+                  f"({err if err is not None else 'failed on another rank'}); "
+                  "results exchanged over gloo", file=sys.stderr, flush=True)
+            gather = farm.TorchGather(world)
+            exchange = "gloo-fallback"
     else:
         gather = lambda send: np.asarray(send, np.float64).copy()  # noqa: E731
     fm = farm.Farm(world, rank, gather)
@@ -454,7 +476,8 @@ def main(argv=None):
             lat.append((time.perf_counter() - t1) * 1e6)
         lt = torch.tensor([float(np.median(lat[5:]))], dtype=torch.float64)
         dist.all_reduce(lt, op=dist.ReduceOp.MAX)
-        collective = {"op": "ncclAllGather (RCCL)" if a.gather == "rccl" else "gloo all_gather",
+        collective = {"op": {"rccl": "ncclAllGather (RCCL)", "gloo": "gloo all_gather",
+                             "gloo-fallback": "gloo all_gather (RCCL init failed)"}[exchange],
                       "bytes_per_rank": 8 * slots,
                       "latency_us_median": float(lt.item())}
     # the timed region's results: all finite, every step the same values (same inputs)
@@ -502,8 +525,10 @@ def main(argv=None):
                    "genes": a.genes if a.workload != "c5" else 4,
                    "timepoints": a.timepoints if a.workload != "c5" else 7,
                    "problems_per_step": per_step, "parallelism": f"replicas{world}",
-                   "exchange": ("RCCL all-gather of NaN-padded per-rank result slots"
-                                if a.gather == "rccl" else "gloo all-gather (rehearsal)")
+                   "exchange": {"rccl": "RCCL all-gather of NaN-padded per-rank result slots",
+                                "gloo": "gloo all-gather (rehearsal)",
+                                "gloo-fallback": "gloo all-gather of the same slots (the RCCL "
+                                                 "communicator failed to initialise)"}[exchange]
                                if world > 1 else "none"},
         "result_first": float(res[0][0]),
     }

@@ -10,12 +10,15 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cerrno>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 
 #include "lfm_internal.h"
 
@@ -212,38 +215,64 @@ struct DeviceGuard {
 };
 
 // ------------------------------------------------------ schedule-3 tenancy
-// Schedule 3 is single tenant per GPU: its factor chain needs all of its workgroups resident on
-// the reserved CUs, and two chains on the same CUs starve each other at their grid barriers
-// until the bounded waits fire (LFM_E_TIMEOUT). A schedule-3 factorisation therefore holds
-//   * a per-device mutex of this process for the whole call (enqueue to the final
-//     synchronise): threads of one process take turns — each evaluation runs the same
-//     schedule-3 arithmetic, so its result is bit-identical to running alone;
-//   * an advisory flock on /tmp/lfm_gpu_<PCI bus id>.lock (TMPDIR if set), tried without
-//     blocking: if another process holds it, this call runs schedule 1 instead (look-ahead on
-//     every CU, no device-side waits between streams; equal to the schedule-3 value to
-//     rounding, tests/test_gpu_farm_tenancy.py), so neither process stalls.
-// The key is the PCI bus id, not the device ordinal, which depends on each process's
-// HIP_VISIBLE_DEVICES.
+// Schedule 3 is single tenant per GPU: its factor chain needs every one of its workgroups
+// resident on the reserved CUs (one per CU, nearly all of the CU's LDS). Any other work on the
+// GPU can starve it: two chains on the same CUs stall each other at their grid barriers, and a
+// stream of smaller workgroups from another context (a schedule-1 factorisation, a gram fill)
+// keeps refilling the LDS a waiting chain workgroup needs, while the resident ones spin until
+// the bounded waits fire (LFM_E_TIMEOUT, minutes later: seen with two ranks of bench.py on one
+// card at N = 16384). So the library holds a per-device readers-writer lock over its GPU work:
+//   * exclusive: a schedule-3 factorisation (MLL, gradient, log_prob), from enqueue to the final
+//     synchronise;
+//   * shared: every other call that fills the GPU (schedule-1 factorisations, the posterior,
+//     gram and cross-covariance fills). Shared holders run concurrently.
+// In-process: a std::shared_mutex per device. Across processes: flock on
+// $TMPDIR/lfm_gpu_<PCI bus id>.lock (LOCK_EX / LOCK_SH, the process's shared hold counted over
+// its threads) behind a turnstile file (.turn, taken LOCK_EX for a moment by readers and held
+// by a waiting writer), so a stream of readers cannot starve a schedule-3 call. Waits block:
+// a call that finds the device busy runs when it is free, with its own schedule's arithmetic
+// (the result is the same as running alone). The key is the PCI bus id, not the device ordinal,
+// which depends on each process's HIP_VISIBLE_DEVICES. No lock is held while a call waits on
+// anything but the GPU, so the order cannot deadlock; a nested request on a thread that already
+// holds the device's lock is a no-op (a shared holder asking for exclusive runs schedule 1).
 constexpr int kMaxDevices = 64;
-std::mutex g_dev_mutex[kMaxDevices];
-std::mutex g_fd_mutex;
-int g_lock_fd[kMaxDevices] = {};        // 0: not opened yet; -1: unavailable
-std::string g_lock_path[kMaxDevices];
+struct DevLock {
+  std::shared_mutex rw;   // in-process readers-writer lock
+  std::mutex turn_mu;     // serialises this process's threads at the turnstile
+  std::mutex fd_mu;       // guards readers / the flock state of `fd`
+  int readers = 0;        // this process's shared holders (flock LOCK_SH held while > 0)
+  int fd = 0, turn = 0;   // 0: not opened yet; -1: unavailable
+  std::string path;
+};
+DevLock g_dev[kMaxDevices];
+std::mutex g_open_mu;
+thread_local int t_depth[kMaxDevices] = {};
+thread_local bool t_excl[kMaxDevices] = {};
 
-int device_lock_fd(int dev) {
-  std::lock_guard<std::mutex> lk(g_fd_mutex);
-  if (g_lock_fd[dev] != 0) return g_lock_fd[dev];
+void device_lock_open(int dev) {
+  std::lock_guard<std::mutex> lk(g_open_mu);
+  DevLock& d = g_dev[dev];
+  if (d.fd != 0) return;
   char bus[64] = {0};
-  int fd = -1;
+  int fd = -1, turn = -1;
   if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) == hipSuccess) {
     for (char* c = bus; *c; ++c)
       if (*c == ':' || *c == '.') *c = '_';
     const char* tmp = std::getenv("TMPDIR");
-    g_lock_path[dev] = std::string(tmp && *tmp ? tmp : "/tmp") + "/lfm_gpu_" + bus + ".lock";
-    fd = ::open(g_lock_path[dev].c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+    d.path = std::string(tmp && *tmp ? tmp : "/tmp") + "/lfm_gpu_" + bus + ".lock";
+    fd = ::open(d.path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+    const std::string tp = d.path.substr(0, d.path.size() - 5) + ".turn";
+    turn = ::open(tp.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
   }
-  g_lock_fd[dev] = fd >= 0 ? fd : -1;
-  return g_lock_fd[dev];
+  d.turn = turn >= 0 ? turn : -1;
+  d.fd = fd >= 0 && turn >= 0 ? fd : -1;
+  if (fd >= 0 && turn < 0) ::close(fd);
+}
+
+// flock, restarted when a signal interrupts the wait
+void flock_retry(int fd, int op) {
+  while (::flock(fd, op) != 0 && errno == EINTR) {
+  }
 }
 
 }  // namespace
@@ -251,39 +280,84 @@ int device_lock_fd(int dev) {
 namespace lfm {
 std::string tenancy_lock_path(int dev) {
   if (dev < 0 || dev >= kMaxDevices) return std::string();
-  device_lock_fd(dev);
-  std::lock_guard<std::mutex> lk(g_fd_mutex);
-  return g_lock_path[dev];
+  device_lock_open(dev);
+  std::lock_guard<std::mutex> lk(g_open_mu);
+  return g_dev[dev].path;
 }
 }  // namespace lfm
 
 namespace {
 
-class S3Tenancy {
+class DeviceTenancy {
  public:
-  explicit S3Tenancy(lfm_ctx* ctx) : ctx_(ctx) {
+  // s3: the call would run schedule 3 (exclusive); else shared
+  DeviceTenancy(lfm_ctx* ctx, bool s3) : ctx_(ctx) {
     ctx->s3_yield = false;
-    if (!s3_on(ctx) || ctx->device < 0 || ctx->device >= kMaxDevices) return;
-    mu_ = &g_dev_mutex[ctx->device];
-    mu_->lock();
-    fd_ = device_lock_fd(ctx->device);
-    if (fd_ >= 0 && ::flock(fd_, LOCK_EX | LOCK_NB) != 0) {
-      ctx->s3_yield = true;  // another process's schedule-3 evaluation: run schedule 1
-      fd_ = -1;
+    const int dev = ctx->device;
+    if (dev < 0 || dev >= kMaxDevices) return;
+    if (t_depth[dev] > 0) {
+      // nested on this thread: the held lock covers the call; a shared holder cannot upgrade
+      if (s3 && !t_excl[dev]) ctx->s3_yield = true;
+      ++t_depth[dev];
+      dev_ = dev;
+      nested_ = true;
+      return;
+    }
+    device_lock_open(dev);
+    DevLock& d = g_dev[dev];
+    dev_ = dev;
+    excl_ = s3;
+    if (excl_) {
+      d.rw.lock();
+      if (d.fd > 0) {
+        std::lock_guard<std::mutex> tl(d.turn_mu);
+        flock_retry(d.turn, LOCK_EX);  // readers arriving from now on wait at the turnstile
+        flock_retry(d.fd, LOCK_EX);    // the readers already in drain
+        flock_retry(d.turn, LOCK_UN);
+      }
+    } else {
+      d.rw.lock_shared();
+      if (d.fd > 0) {
+        {
+          std::lock_guard<std::mutex> tl(d.turn_mu);
+          flock_retry(d.turn, LOCK_EX);  // behind any writer waiting in another process
+          flock_retry(d.turn, LOCK_UN);
+        }
+        std::lock_guard<std::mutex> fl(d.fd_mu);
+        if (d.readers++ == 0) flock_retry(d.fd, LOCK_SH);
+      }
+    }
+    t_depth[dev] = 1;
+    t_excl[dev] = excl_;
+  }
+  ~DeviceTenancy() {
+    ctx_->s3_yield = false;
+    if (dev_ < 0) return;
+    if (nested_) {
+      --t_depth[dev_];
+      return;
+    }
+    DevLock& d = g_dev[dev_];
+    t_depth[dev_] = 0;
+    t_excl[dev_] = false;
+    if (excl_) {
+      if (d.fd > 0) flock_retry(d.fd, LOCK_UN);
+      d.rw.unlock();
+    } else {
+      if (d.fd > 0) {
+        std::lock_guard<std::mutex> fl(d.fd_mu);
+        if (--d.readers == 0) flock_retry(d.fd, LOCK_UN);
+      }
+      d.rw.unlock_shared();
     }
   }
-  ~S3Tenancy() {
-    if (fd_ >= 0) ::flock(fd_, LOCK_UN);
-    if (mu_) mu_->unlock();
-    ctx_->s3_yield = false;
-  }
-  S3Tenancy(const S3Tenancy&) = delete;
-  S3Tenancy& operator=(const S3Tenancy&) = delete;
+  DeviceTenancy(const DeviceTenancy&) = delete;
+  DeviceTenancy& operator=(const DeviceTenancy&) = delete;
 
  private:
   lfm_ctx* ctx_;
-  std::mutex* mu_ = nullptr;
-  int fd_ = -1;
+  int dev_ = -1;
+  bool excl_ = false, nested_ = false;
 };
 
 int finish(lfm_ctx* ctx) {
@@ -305,7 +379,7 @@ int mll_blocked(lfm_ctx* ctx, const Staged& st, const double* d_x, const double*
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)Mp * Mp * sizeof(double));
   if (r) return r;
   const double noise = hyp->obs_stddev * hyp->obs_stddev;  // objectives.py:66
-  S3Tenancy tenancy(ctx);  // held to the final synchronise (finish)
+  DeviceTenancy tenancy(ctx, s3_on(ctx));  // held to the final synchronise (finish)
   GramGen gen;
   const bool fuse = chol_fuses_gram(ctx, CHOL_MLL, st.lay, n);
   if (st.lay.ok) {
@@ -457,6 +531,7 @@ static int gram_host(lfm_ctx* ctx, const double* x, int64_t n, const lfm_hyp* hy
   if (!out || ldo < n) return set_err(ctx, LFM_E_ARG, "out is NULL or ldo < n");
   if (uplo != LFM_UPLO_FULL && uplo != LFM_UPLO_LOWER) return set_err(ctx, LFM_E_ARG, "bad uplo");
   DeviceGuard g(ctx->device);
+  DeviceTenancy tenancy(ctx, false);
   r = ensure(ctx, (void**)&ctx->xin, &ctx->xin_bytes, (size_t)n * 3 * 8);
   if (r) return r;
   r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)n * n * sizeof(OutT));
@@ -480,6 +555,7 @@ static int gram_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* h
   if (!d_out || ldo < n) return set_err(ctx, LFM_E_ARG, "out is NULL or ldo < n");
   if (uplo != LFM_UPLO_FULL && uplo != LFM_UPLO_LOWER) return set_err(ctx, LFM_E_ARG, "bad uplo");
   DeviceGuard g(ctx->device);
+  DeviceTenancy tenancy(ctx, false);
   std::vector<double> xh((size_t)n * 3);
   hipError_t e = hipMemcpyAsync(xh.data(), d_x, n * 3 * 8, hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
@@ -752,6 +828,7 @@ int lfm_cross_covariance_f64(lfm_ctx* ctx, const double* x, int64_t n, const dou
   if (r) return r;
   if (!out || ldo < m) return set_err(ctx, LFM_E_ARG, "out is NULL or ldo < m");
   DeviceGuard g(ctx->device);
+  DeviceTenancy tenancy(ctx, false);
   Staged st;
   r = stage_hyp(ctx, hyp, nullptr, 0, false, &st);
   if (r) return r;
@@ -849,7 +926,7 @@ int lfm_mll_grad_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
   r = ensure(ctx, (void**)&ctx->gacc, &ctx->gacc_bytes, (size_t)(5 * G + 3) * sizeof(double));
   if (r) return r;
   const double noise = hyp->obs_stddev * hyp->obs_stddev;  // objectives.py:66
-  S3Tenancy tenancy(ctx);  // held to the final synchronise (finish)
+  DeviceTenancy tenancy(ctx, s3_on(ctx));  // held to the final synchronise (finish)
   GramGen gen;
   const bool fuse = chol_fuses_gram(ctx, CHOL_INVERSE, st.lay, n);
   if (st.lay.ok) {
@@ -910,6 +987,7 @@ int lfm_posterior_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n,
   if (r) return r;
   if ((n + m) > (int64_t)1 << 17) return set_err(ctx, LFM_E_ARG, "n + m too large");
   DeviceGuard g(ctx->device);
+  DeviceTenancy tenancy(ctx, false);  // schedule 1 (Schur complement), shared
   Staged st;
   r = stage_hyp(ctx, hyp, nullptr, 0, false, &st);
   if (r) return r;
@@ -1091,7 +1169,7 @@ int lfm_log_prob_f64(lfm_ctx* ctx, const double* loc, const double* scale, int64
   HypDev h{nullptr, nullptr, nullptr, 1, 1.0};
   r = launch_augment(ctx, h, nullptr, ctx->xin + n, ctx->xin, n, ctx->A, Mp, Mp);
   if (r) return r;
-  S3Tenancy tenancy(ctx);  // held to the final synchronise (finish)
+  DeviceTenancy tenancy(ctx, s3_on(ctx));  // held to the final synchronise (finish)
   r = chol_factor_solve(ctx, ctx->A, Mp, n, Mp, 0, ctx->result);
   if (r) return r;
   double* hres = ctx->hpin + (ctx->hpin_bytes / 8 - 8);
@@ -1190,6 +1268,10 @@ struct Rccl {
                             hipStream_t) = nullptr;
   ncclResult_t (*commDestroy)(ncclComm_t) = nullptr;
   const char* (*errStr)(ncclResult_t) = nullptr;
+  // optional (non-blocking communicator, bounded waits): absent -> blocking init
+  ncclResult_t (*commInitRankConfig)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;
+  ncclResult_t (*commGetAsyncError)(ncclComm_t, ncclResult_t*) = nullptr;
+  ncclResult_t (*commAbort)(ncclComm_t) = nullptr;
 };
 Rccl g_rccl;
 
@@ -1203,6 +1285,10 @@ int rccl_load(lfm_ctx* ctx) {
   g_rccl.allGather = (decltype(g_rccl.allGather))dlsym(h, "ncclAllGather");
   g_rccl.commDestroy = (decltype(g_rccl.commDestroy))dlsym(h, "ncclCommDestroy");
   g_rccl.errStr = (decltype(g_rccl.errStr))dlsym(h, "ncclGetErrorString");
+  g_rccl.commInitRankConfig =
+      (decltype(g_rccl.commInitRankConfig))dlsym(h, "ncclCommInitRankConfig");
+  g_rccl.commGetAsyncError = (decltype(g_rccl.commGetAsyncError))dlsym(h, "ncclCommGetAsyncError");
+  g_rccl.commAbort = (decltype(g_rccl.commAbort))dlsym(h, "ncclCommAbort");
   if (!g_rccl.getUniqueId || !g_rccl.commInitRank || !g_rccl.allGather || !g_rccl.commDestroy)
     return set_err(ctx, LFM_E_RCCL, "librccl lacks a required symbol");
   g_rccl.h = h;
@@ -1213,6 +1299,34 @@ int rccl_fail(lfm_ctx* ctx, ncclResult_t r, const char* what) {
   if (r == ncclSuccess) return LFM_OK;
   return set_err(ctx, LFM_E_RCCL,
                  std::string(what) + ": " + (g_rccl.errStr ? g_rccl.errStr(r) : "rccl error"));
+}
+
+// Bound on every wait of a non-blocking communicator (seconds, LFM_RCCL_TIMEOUT_S, default
+// 300): a peer rank that died or never joined ends the call with LFM_E_RCCL instead of a hang.
+double rccl_timeout_s() {
+  const char* v = std::getenv("LFM_RCCL_TIMEOUT_S");
+  const double t = v ? std::atof(v) : 300.0;
+  return t > 0.0 ? t : 300.0;
+}
+
+double mono_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+// Poll a non-blocking communicator until its pending operation leaves ncclInProgress.
+int rccl_poll(lfm_ctx* ctx, ncclComm_t comm, const char* what) {
+  const double end = mono_s() + rccl_timeout_s();
+  for (;;) {
+    ncclResult_t st = ncclInProgress;
+    const ncclResult_t q = g_rccl.commGetAsyncError(comm, &st);
+    if (q != ncclSuccess) return rccl_fail(ctx, q, what);
+    if (st != ncclInProgress) return rccl_fail(ctx, st, what);
+    if (mono_s() > end)
+      return set_err(ctx, LFM_E_RCCL, std::string(what) + ": timed out (a peer rank did not join)");
+    usleep(200);
+  }
 }
 }  // namespace
 
@@ -1237,9 +1351,31 @@ int lfm_farm_init(lfm_ctx* ctx, const unsigned char id[128], int nranks, int ran
   ncclUniqueId u;
   std::memcpy(u.internal, id, 128);
   ncclComm_t comm = nullptr;
-  r = rccl_fail(ctx, g_rccl.commInitRank(&comm, nranks, u, rank), "ncclCommInitRank");
-  if (r) return r;
+  bool nb = false;
+  if (g_rccl.commInitRankConfig && g_rccl.commGetAsyncError && g_rccl.commAbort) {
+    // non-blocking communicator: the init (and every later call) is polled against a deadline
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    const ncclResult_t q = g_rccl.commInitRankConfig(&comm, nranks, u, rank, &cfg);
+    if (q == ncclSuccess || q == ncclInProgress) {
+      r = rccl_poll(ctx, comm, "ncclCommInitRankConfig");
+      if (r) {
+        g_rccl.commAbort(comm);
+        return r;
+      }
+      nb = true;
+    } else if (q != ncclInvalidArgument) {
+      return rccl_fail(ctx, q, "ncclCommInitRankConfig");
+    } else {
+      comm = nullptr;  // a library that rejects this config layout: blocking init below
+    }
+  }
+  if (!nb) {
+    r = rccl_fail(ctx, g_rccl.commInitRank(&comm, nranks, u, rank), "ncclCommInitRank");
+    if (r) return r;
+  }
   ctx->comm = comm;
+  ctx->comm_nb = nb;
   ctx->nranks = nranks;
   ctx->rank = rank;
   return LFM_OK;
@@ -1255,12 +1391,28 @@ int lfm_farm_allgather_f64(lfm_ctx* ctx, const double* send, int64_t count, doub
   double* dsend = ctx->farm_buf;
   double* drecv = ctx->farm_buf + count;
   hipMemcpyAsync(dsend, send, count * 8, hipMemcpyHostToDevice, ctx->stream);
-  r = rccl_fail(ctx,
-                g_rccl.allGather(dsend, drecv, (size_t)count, ncclFloat64, (ncclComm_t)ctx->comm,
-                                 ctx->stream),
-                "ncclAllGather");
+  const ncclResult_t q = g_rccl.allGather(dsend, drecv, (size_t)count, ncclFloat64,
+                                         (ncclComm_t)ctx->comm, ctx->stream);
+  if (ctx->comm_nb && q == ncclInProgress) {
+    r = rccl_poll(ctx, (ncclComm_t)ctx->comm, "ncclAllGather");
+  } else {
+    r = rccl_fail(ctx, q, "ncclAllGather");
+  }
   if (r) return r;
   hipMemcpyAsync(recv, drecv, (size_t)count * ctx->nranks * 8, hipMemcpyDeviceToHost, ctx->stream);
+  if (ctx->comm_nb) {
+    // bounded completion: a collective whose peers never arrive would block the stream forever
+    const double end = mono_s() + rccl_timeout_s();
+    hipError_t e;
+    while ((e = hipStreamQuery(ctx->stream)) == hipErrorNotReady) {
+      if (mono_s() > end) {
+        g_rccl.commAbort((ncclComm_t)ctx->comm);
+        ctx->comm = nullptr;
+        return set_err(ctx, LFM_E_RCCL, "ncclAllGather: timed out (a peer rank did not arrive)");
+      }
+      usleep(50);
+    }
+  }
   return finish(ctx);
 }
 

@@ -2326,7 +2326,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   const int wbulk = s3 ? (bordered ? LFM_WBORD : LFM_WBULK) : 4;
   const int64_t w2min = env_int("LFM_W2_MIN", s3 ? 5120 : 4096);
   const std::vector<std::pair<int64_t, int>> steps =
-      plan_steps(nblk, Mp, NB, bordered, s3, wbulk, w4min, w2min);
+      plan_steps(nblk, Mp, NB, bordered, s3, wbulk, w4min, w2min, (int)env_int("LFM_W0", 1));
   const int S = (int)steps.size();
   r = ensure_events(ctx, 2 * (size_t)S + 3);
   if (r) return r;

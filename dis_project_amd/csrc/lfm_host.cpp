@@ -45,7 +45,7 @@ GridLayout detect_grid(const double* x, int64_t n, int64_t G) {
 
 std::vector<std::pair<int64_t, int>> plan_steps(int64_t nblk, int64_t Mp, int nb, bool bordered,
                                                 bool s3, int wbulk, int64_t w4min,
-                                                int64_t w2min) {
+                                                int64_t w2min, int w0) {
   std::vector<std::pair<int64_t, int>> steps;
   for (int64_t k = 0; k < nblk;) {
     const int64_t m = bordered ? Mp + nb : Mp - k * nb;
@@ -55,7 +55,7 @@ std::vector<std::pair<int64_t, int>> plan_steps(int64_t nblk, int64_t Mp, int nb
     if (m >= w4min && k + wk <= nblk) w = wk;
     else if (m >= w4min && k + 4 <= nblk) w = 4;
     else if (m >= w2min && k + 2 <= nblk) w = 2;
-    if (k == 0 && s3) w = 1;
+    if (k == 0 && s3) w = (w0 == 2 && nblk >= 2) ? 2 : 1;
     steps.emplace_back(k, w);
     k += w;
   }

@@ -52,11 +52,11 @@ GridLayout detect_grid(const double* x, int64_t n, int64_t G);
 // Super-panel plan of a blocked factorisation over nblk block columns of width nb: (first
 // block column, width in block columns) per step. Width wbulk (the first bulk step 4) while
 // the trailing matrix has >= w4min rows, 4 if wbulk does not fit, 2 down to w2min rows, else
-// 1; schedule 3 starts with a one-column super-panel. Bordered (the gradient's inverse): the
-// trailing window is a constant Mp + nb rows.
+// 1; schedule 3 starts with a super-panel of w0 (1 or 2) columns. Bordered (the gradient's
+// inverse): the trailing window is a constant Mp + nb rows.
 std::vector<std::pair<int64_t, int>> plan_steps(int64_t nblk, int64_t Mp, int nb, bool bordered,
                                                 bool s3, int wbulk, int64_t w4min,
-                                                int64_t w2min);
+                                                int64_t w2min, int w0 = 1);
 
 // Rest regions of at most this many tile columns are enumerated as bands (column by column),
 // wider ones as the supertiled triangle below (lfm_chol.hip unit_tile).

@@ -73,8 +73,8 @@ struct lfm_ctx {
   unsigned panel_epoch = 0;                      // fused panel launches so far
   int side_cus = 0;                              // CUs reserved for the side stream (LFM_SIDE_CUS)
   int sched = 3;                                 // look-ahead schedule 1 or 3 (LFM_SCHED)
-  bool s3_yield = false;                         // this call runs schedule 1: another process
-                                                 // holds the device's schedule-3 tenancy
+  bool s3_yield = false;                         // this call runs schedule 1: nested in a
+                                                 // shared hold of the device's tenancy lock
   int last_sched = 0;                            // schedule the last factorisation ran (diag)
   bool s3_events = false;                        // schedule 3 ordered by events (LFM_S3_EVENTS)
   unsigned spin_limit = 1u << 26;                // device-side wait bound (LFM_DEBUG_SPIN_LIMIT)
@@ -102,6 +102,7 @@ struct lfm_ctx {
 
   // farm (RCCL)
   void* comm = nullptr;
+  bool comm_nb = false;  // communicator created non-blocking (calls polled, bounded)
   int nranks = 0, rank = -1;
   double* farm_buf = nullptr; size_t farm_bytes = 0;
 };

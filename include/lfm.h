@@ -99,15 +99,18 @@ int lfm_ctx_create(int device, lfm_ctx** out);
 void lfm_ctx_destroy(lfm_ctx* ctx);
 const char* lfm_last_error(const lfm_ctx* ctx);
 int lfm_ctx_synchronize(lfm_ctx* ctx);
-/* Block size of the blocked Cholesky (64 or 128); 0 restores the default. */
+/* Block size of the blocked Cholesky: 128 (the only size built; 0 restores it). */
 int lfm_ctx_set_block(lfm_ctx* ctx, int nb);
 /* Factorisation schedule of this context's MLL / gradient:
  *   3  CU-partitioned stream pair: the factor chain on LFM_SIDE_CUS reserved CUs, the bulk on
- *      the rest. Lowest latency of ONE evaluation; single tenant: two schedule-3 contexts
- *      running at once on one GPU starve each other's co-resident chains (device-side wait
- *      bound -> LFM_E_TIMEOUT).
+ *      the rest. Lowest latency of ONE evaluation. Single tenant: the chain needs all of its
+ *      workgroups resident, so a schedule-3 factorisation holds the device's lock exclusively
+ *      (threads and processes: a per-device readers-writer lock plus flock on
+ *      $TMPDIR/lfm_gpu_<PCI bus id>.lock); other GPU work of the library holds it shared.
+ *      Concurrent callers wait their turn; results do not depend on it.
  *   1  look-ahead on every CU. Several schedule-1 contexts driven from separate host threads
- *      share one GPU: the throughput mode of a restart farm (farm.ConcurrentEvaluator).
+ *      share one GPU (shared holders): the throughput mode of a restart farm
+ *      (farm.ConcurrentEvaluator).
  *   0  the process default (LFM_SCHED, else 3).
  * Schedule 3 on a context without a CU partition -> LFM_E_ARG. Replaces no reference call:
  * the reference's XLA executable has no schedule (src/objectives.py:43-46 is the whole MLL). */

@@ -1,8 +1,11 @@
 """Schedule 3 is single tenant per GPU (include/lfm.h lfm_ctx_set_schedule; lfm_api.hip
-S3Tenancy): two schedule-3 factor chains on the same reserved CUs would starve each other at
-their grid barriers. The library serialises the schedule-3 factorisations of one process on a
-per-device mutex (bit-identical results), and a process that finds another process holding the
-device's advisory lock runs that call on schedule 1 instead of stalling.
+DeviceTenancy): its factor chain needs every workgroup resident on the reserved CUs, so two
+chains, or any other work refilling those CUs, starve it at its grid barriers. The library
+holds a per-device readers-writer lock over its GPU work — exclusive for a schedule-3
+factorisation, shared for everything else that fills the GPU — in-process (a shared mutex) and
+across processes (flock on $TMPDIR/lfm_gpu_<bus id>.lock behind a turnstile file). A call that
+finds the device busy waits, then runs its own schedule (results bit-identical to running
+alone).
 
 The reference's call site is single threaded (src/trainer.py:126 value_and_grad inside one
 XLA scan); these are the concurrent uses the Python shim allows on top of it."""
@@ -87,10 +90,22 @@ def test_two_threads_default_contexts_take_turns():
             assert abs(v - ref) <= MLL_RTOL * abs(ref)
 
 
-def test_other_process_holding_the_lock_gives_schedule_1():
-    """While another open file description holds the device's advisory lock (what a second
-    process's schedule-3 evaluation does), a schedule-3 context runs the call on schedule 1 —
-    equal to the oracle at 1e-9 — and returns to schedule 3 once the lock is free."""
+def _hold(path, op, seconds, started):
+    """Another open file description (what another process has) holding the lock for a while."""
+    with open(path, "a+") as f:
+        fcntl.flock(f.fileno(), op)
+        started.set()
+        threading.Event().wait(seconds)
+        fcntl.flock(f.fileno(), fcntl.LOCK_UN)
+
+
+@pytest.mark.parametrize("op", ["LOCK_EX", "LOCK_SH"])
+def test_other_process_holding_the_lock_delays_schedule_3(op):
+    """While another process holds the device lock (exclusive: its schedule-3 evaluation;
+    shared: its schedule-1 / gram work), a schedule-3 call waits for it instead of running
+    beside it, then runs schedule 3 with the same bits as before."""
+    import time
+
     from dis_project_amd import _lib
 
     w, ref = _problem(seed=43)
@@ -108,17 +123,52 @@ def test_other_process_holding_the_lock_gives_schedule_1():
 
         v3 = mll()
         assert _last_schedule(ctx) == 3
+        assert abs(v3 - ref) <= MLL_RTOL * abs(ref)
         path = _lock_path(ctx)
         assert path.endswith(".lock") and "lfm_gpu_" in path
-        with open(path, "a+") as f:
-            fcntl.flock(f.fileno(), fcntl.LOCK_EX)
-            v1 = mll()
-            assert _last_schedule(ctx) == 1
-            assert ctx.schedule == 3  # the context's own setting is unchanged
-            fcntl.flock(f.fileno(), fcntl.LOCK_UN)
-        assert abs(v1 - ref) <= MLL_RTOL * abs(ref)
-        assert abs(v1 - v3) <= 1e-11 * abs(v3)
-        assert mll() == v3 and _last_schedule(ctx) == 3
+        started = threading.Event()
+        holder = threading.Thread(target=_hold, args=(path, getattr(fcntl, op), 1.5, started))
+        holder.start()
+        assert started.wait(30)
+        t0 = time.perf_counter()
+        v = mll()
+        waited = time.perf_counter() - t0
+        holder.join(timeout=60)
+        assert waited >= 1.0, waited  # it waited for the holder (1.5 s) instead of running
+        assert _last_schedule(ctx) == 3
+        assert v == v3
+    finally:
+        ctx.close()
+
+
+def test_waiting_writer_holds_back_new_readers():
+    """Turnstile: while another process's schedule-3 call waits for the shared holders to drain
+    (it holds the .turn file), a new shared call (a gram fill) waits behind it instead of
+    joining the readers, so a stream of readers cannot starve a schedule-3 call."""
+    import time
+
+    from dis_project_amd import _lib
+
+    w, _ = _problem(G=4, T=256, seed=45)
+    ctx = _lib.Context(0)
+    try:
+        path = _lock_path(ctx)
+        turn = path[: -len(".lock")] + ".turn"
+        started = threading.Event()
+        holder = threading.Thread(target=_hold, args=(turn, fcntl.LOCK_EX, 1.5, started))
+        holder.start()
+        assert started.wait(30)
+        n = w.data.X.shape[0]
+        x = np.ascontiguousarray(w.data.X)
+        k = np.empty((n, n))
+        hp = w.model.hyp()
+        t0 = time.perf_counter()
+        ctx.check(ctx.lib.lfm_gram_f64(ctx.handle, _lib.dptr(x), n, hp.ref, 0.0, 0,
+                                       _lib.dptr(k), n))
+        waited = time.perf_counter() - t0
+        holder.join(timeout=60)
+        assert waited >= 1.0, waited
+        assert np.all(np.isfinite(k))
     finally:
         ctx.close()
 
@@ -136,9 +186,8 @@ print(repr(vals))
 
 
 def test_two_processes_share_the_gpu_without_stalling():
-    """A second process evaluating on the same GPU at the same time as this one: both finish
-    (whichever holds the lock runs schedule 3, the other schedule 1 for that call), every value
-    within 1e-9 of the oracle."""
+    """A second process evaluating on the same GPU at the same time as this one: the two take
+    turns on the device lock and both finish, every value within 1e-9 of the oracle."""
     import dis_project_amd as lfm
 
     w, ref = _problem(seed=47)
