@@ -21,9 +21,36 @@ for w, esz, fn in ((configs.c2(), 8, lib.lfm_gram_f64_dev), (configs.c4(), 4, li
     ctx.check(lib.lfm_memcpy_h2d(h, dx, x.ctypes.data, x.nbytes))
     ctx.check(lib.lfm_dev_alloc(h, n * n * esz, _lib.ctypes.byref(dk)))
     cases.append((w.name, n, esz, fn, dx, dk, w.model.hyp()))
+# bit-identity of every variant against the first: sampled rows of each fill (lower part)
+ref_rows = {}
+for vi, v in enumerate(variants):
+    for k in {kk for vv in variants for kk in vv}:
+        os.environ.pop(k, None)
+    os.environ.update(v)
+    for name, n, esz, fn, dx, dk, hp in cases:
+        ctx.check(lib.lfm_memset_dev(h, dk, 0, n * n * esz))
+        ctx.check(fn(h, dx, n, hp.ref, 0.0, _lib.LFM_UPLO_LOWER, dk, n))
+        rows = list(range(0, n, n // 61)) + [n - 1]
+        buf = np.empty(n, dtype=np.float64 if esz == 8 else np.float32)
+        got = []
+        for r in rows:
+            ctx.check(lib.lfm_memcpy_d2h(h, buf.ctypes.data, _lib.c_void_p(dk.value + r * n * esz),
+                                         (r + 1) * esz))
+            got.append(buf[: r + 1].copy())
+        if vi == 0:
+            ref_rows[name] = got
+        else:
+            same = all(np.array_equal(a.view(np.uint8), b.view(np.uint8))
+                       for a, b in zip(got, ref_rows[name]))
+            print(f"{sys.argv[1 + vi]:18s} {name:28s} sampled rows bit-identical to variant 0: {same}",
+                  flush=True)
+for k in {kk for vv in variants for kk in vv}:
+    os.environ.pop(k, None)
 res = {}
 for rnd in range(4):
     for vi, v in enumerate(variants):
+        for k in {kk for vv in variants for kk in vv}:
+            os.environ.pop(k, None)
         os.environ.update(v)
         for name, n, esz, fn, dx, dk, hp in cases:
             ctx.check(fn(h, dx, n, hp.ref, 0.0, _lib.LFM_UPLO_LOWER, dk, n))
