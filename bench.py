@@ -337,6 +337,43 @@ def c4_setup(ctx, a):
     return work, step, rows, close
 
 
+def make_gather(ctx, world, rank, mode, rccl=None):
+    """The farm's result exchange for this rank: (gather, kind). kind "rccl": the library's
+    RCCL all-gather (non-blocking communicator, every wait bounded by LFM_RCCL_TIMEOUT_S);
+    "gloo": the rehearsal's torch.distributed all-gather; "gloo-fallback": any rank's RCCL
+    communicator failed to initialise, so every rank (they agree over the gloo control plane)
+    exchanges over gloo instead. rccl(ctx, world, rank, uid) builds the communicator (tests pass
+    a stand-in); the unique id comes from rank 0."""
+    if world <= 1:
+        return (lambda send: np.asarray(send, np.float64).copy()), "none"
+    if mode == "gloo":
+        return farm.TorchGather(world), "gloo"
+    if rccl is None:
+        rccl = farm.RcclGather
+    uid = None
+    if rank == 0:
+        uid = farm.RcclGather.unique_id(ctx) if rccl is farm.RcclGather else b"\0" * 128
+    obj = [uid]
+    dist.broadcast_object_list(obj, src=0)
+    err, gather = None, None
+    try:
+        gather = rccl(ctx, world, rank, obj[0])
+    except Exception as e:  # noqa: BLE001 — every rank must learn of any rank's failure
+        err = e
+    ok = torch.tensor([0 if err is not None else 1], dtype=torch.int32)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()):
+        return gather, "rccl"
+    # one rank's communicator failed: every rank exchanges over gloo instead, and the line says
+    # so (the evaluations themselves are unaffected)
+    if gather is not None:
+        gather.close()
+    print(f"rank {rank}: RCCL communicator unavailable "
+          f"({err if err is not None else 'failed on another rank'}); "
+          "results exchanged over gloo", file=sys.stderr, flush=True)
+    return farm.TorchGather(world), "gloo-fallback"
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else list(argv)
     a = parse(argv)
@@ -365,32 +402,7 @@ def main(argv=None):
     lib, h = ctx.lib, ctx.handle
 
     # farm communicator (replicas-only exchange of per-rank results)
-    exchange = a.gather
-    if world > 1 and a.gather == "gloo":
-        gather = farm.TorchGather(world)
-    elif world > 1:
-        obj = [farm.RcclGather.unique_id(ctx) if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        err = None
-        try:
-            # non-blocking communicator, every wait bounded (LFM_RCCL_TIMEOUT_S)
-            gather = farm.RcclGather(ctx, world, rank, obj[0])
-        except Exception as e:  # noqa: BLE001 — every rank must learn of any rank's failure
-            err = e
-        ok = torch.tensor([0 if err is not None else 1], dtype=torch.int32)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if not int(ok.item()):
-            # one rank's communicator failed: all ranks exchange over gloo instead, and the
-            # line says so (the evaluations themselves are unaffected)
-            if err is None:
-                gather.close()
-            print(f"rank {rank}: RCCL communicator unavailable "
-                  f"({err if err is not None else 'failed on another rank'}); "
-                  "results exchanged over gloo", file=sys.stderr, flush=True)
-            gather = farm.TorchGather(world)
-            exchange = "gloo-fallback"
-    else:
-        gather = lambda send: np.asarray(send, np.float64).copy()  # noqa: E731
+    gather, exchange = make_gather(ctx, world, rank, a.gather)
     fm = farm.Farm(world, rank, gather)
 
     workers = None

@@ -97,3 +97,61 @@ def test_rank_processes_do_not_relaunch(monkeypatch):
     monkeypatch.setenv("RANK", "0")
     with pytest.raises(SystemExit, match="WORLD_SIZE=3"):
         bench.main(["--gpus", "2"])
+
+
+def _gather_rank(rank, world, port, fail_rank, q):
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        class Stub:
+            """Stands in for farm.RcclGather (no GPU here): fails on `fail_rank`."""
+
+            closed = False
+
+            def __init__(self, ctx, world, rank, uid):
+                if rank == fail_rank:
+                    raise RuntimeError("LFM_E_RCCL: stand-in failure")
+
+            def __call__(self, send):
+                raise AssertionError("the failed communicator must not be used")
+
+            def close(self):
+                Stub.closed = True
+
+        import numpy as np
+
+        gather, kind = bench.make_gather(None, world, rank, "rccl", rccl=Stub)
+        recv = None if kind == "rccl" else gather(np.array([float(rank), float(10 + rank)]))
+        q.put((rank, kind, Stub.closed, None if recv is None else recv.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank", [0, 1, -1])
+def test_gather_falls_back_to_gloo_on_every_rank(fail_rank):
+    """bench.make_gather: when any rank's RCCL communicator fails to initialise, every rank
+    (agreeing over the gloo control plane) exchanges its slots over gloo and labels the line
+    "gloo-fallback"; a rank whose own communicator came up closes it. With no failure every
+    rank keeps the communicator ("rccl")."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = bench._free_port()
+    ps = [ctx.Process(target=_gather_rank, args=(r, 2, port, fail_rank, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, kind, closed, recv in res:
+        if fail_rank < 0:
+            assert kind == "rccl" and not closed  # the communicator is kept
+            continue
+        assert kind == "gloo-fallback"
+        assert recv == [0.0, 10.0, 1.0, 11.0]
+        assert closed == (rank != fail_rank)
