@@ -199,3 +199,52 @@ def test_two_processes_share_the_gpu_without_stalling():
     theirs = ast.literal_eval(so.strip().splitlines()[-1])  # the child's list of floats
     for v in mine + theirs:
         assert abs(v - ref) <= MLL_RTOL * abs(ref)
+
+
+CHILD_S1 = r"""
+import sys, time
+sys.path.insert(0, {root!r})
+import numpy as np
+from dis_project_amd import _lib, configs, farm
+w = configs.c2()
+ctx = _lib.Context(0)
+ctx.schedule = 1
+ev = farm.ResidentEvaluator(ctx, w.data)
+print("ready", flush=True)
+vals = list(ev([w.model] * 4))
+ev.close()
+ctx.close()
+print(repr(vals))
+"""
+
+
+def test_schedule_1_process_beside_schedule_3_at_full_size():
+    """The case that stalled before the readers-writer lock: a schedule-1 process (look-ahead on
+    every CU) evaluating the C2 problem (N = 16384) while this process runs schedule 3 on the
+    same card. The schedule-1 kernels kept refilling the LDS the schedule-3 chain's workgroups
+    need, and the chain spun until its bounded waits fired (an evaluation stuck over 90 s,
+    DESIGN.md §5). Both must now finish with the same value."""
+    import time
+
+    from dis_project_amd import _lib, configs, farm
+
+    w = configs.c2()
+    ctx = _lib.Context(0)
+    try:
+        ev = farm.ResidentEvaluator(ctx, w.data)
+        single = float(ev([w.model])[0])
+        child = subprocess.Popen([sys.executable, "-c", CHILD_S1.format(root=ROOT)],
+                                 stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        assert child.stdout.readline().strip() == "ready"  # its evaluations start now
+        t0 = time.perf_counter()
+        mine = [float(ev([w.model])[0]) for _ in range(12)]
+        so, se = child.communicate(timeout=120)
+        took = time.perf_counter() - t0
+        ev.close()
+    finally:
+        ctx.close()
+    assert child.returncode == 0, se[-2000:]
+    theirs = ast.literal_eval(so.strip().splitlines()[-1])
+    assert all(v == single for v in mine)
+    assert len(theirs) == 4 and all(abs(v - single) <= 1e-10 * abs(single) for v in theirs)
+    assert took < 60, took  # 16 evaluations of ~30-40 ms: no bounded wait ran out
