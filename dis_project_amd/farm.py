@@ -129,6 +129,45 @@ class ResidentEvaluator:
                 setattr(self, p, None)
 
 
+class BatchEvaluator:
+    """MLL evaluations of many small problems (n <= 128 each: the C5 ablations) in one batched
+    launch per call (``lfm_mll_batch_f64``: one workgroup per problem). The datasets are
+    registered once: their x / y are held as contiguous fp64 arrays and the problem table's
+    pointers are built at construction, as ResidentEvaluator registers its one large dataset.
+    Each call reads every model's current hyperparameters (``m.hyp()``). Not PD -> NaN."""
+
+    def __init__(self, ctx: _lib.Context, datasets, negative: bool = False):
+        self.ctx, self.negative = ctx, bool(negative)
+        self.keep = []
+        self.probs = (_lib.LfmProblem * len(datasets))()
+        for i, d in enumerate(datasets):
+            x = np.ascontiguousarray(d.X, dtype=np.float64).reshape(-1, 3)
+            y = np.ascontiguousarray(d.y, dtype=np.float64).reshape(-1)
+            if y.size != x.shape[0]:
+                raise ValueError("dataset x / y lengths differ")
+            self.keep.append((x, y))
+            self.probs[i].x = x.ctypes.data
+            self.probs[i].y = y.ctypes.data
+            self.probs[i].n = x.shape[0]
+        self.status = (_lib.c_int * len(datasets))()
+
+    def __call__(self, models) -> np.ndarray:
+        models = list(models)
+        if len(models) != len(self.keep):
+            raise ValueError("one model per registered dataset")
+        hps = [m.hyp() for m in models]  # keeps the hyperparameter buffers alive
+        for i, hp in enumerate(hps):
+            self.probs[i].hyp = hp.struct
+        out = np.empty(len(models))
+        rc = self.ctx.lib.lfm_mll_batch_f64(self.ctx.handle, len(models), self.probs,
+                                            int(self.negative), out.ctypes.data, self.status)
+        self.ctx.check(rc, allow_not_pd=True)
+        return out
+
+    def close(self):
+        self.keep = []
+
+
 def workload(kind: str, genes: int = 64, timepoints: int = 256, restarts: int = 32):
     """Problems of a farm workload as (models, datasets):
 
@@ -301,7 +340,8 @@ def gpu_evaluator(ctx: _lib.Context, datasets, negative: bool = False, workers: 
     dataset go through a ConcurrentEvaluator (x / y in HBM once per worker context, ``workers``
     evaluations in flight; workers = 1: one ResidentEvaluator on ``ctx``, schedule 3;
     workers = 0: ``choose_workers`` for this rank's share); small ones through one batched
-    launch (``CustomConjMLL.batch``: one workgroup per problem, n <= 128)."""
+    launch (BatchEvaluator: one workgroup per problem, n <= 128, the datasets registered once;
+    mixed sizes: ``CustomConjMLL.batch``)."""
     from .objectives import CustomConjMLL
 
     shared = len({id(d) for d in datasets}) == 1 and datasets[0].n > 128
@@ -313,5 +353,17 @@ def gpu_evaluator(ctx: _lib.Context, datasets, negative: bool = False, workers: 
         else:
             res = ResidentEvaluator(ctx, datasets[0], negative)
         return (lambda models, data: res(models)), res.close
+    if all(d.n <= 128 for d in datasets):
+        # registered once; a round passes this rank's block of the same datasets
+        cache = {}
+
+        def evaluate(models, data):
+            key = tuple(id(d) for d in data)
+            if key not in cache:
+                cache.clear()
+                cache[key] = BatchEvaluator(ctx, data, negative)
+            return cache[key](models)
+
+        return evaluate, cache.clear
     mll = CustomConjMLL(negative=negative)
     return (lambda models, data: mll.batch(models, data)), (lambda: None)

@@ -211,7 +211,7 @@ ctx = _lib.Context(0)
 ctx.schedule = 1
 ev = farm.ResidentEvaluator(ctx, w.data)
 print("ready", flush=True)
-vals = list(ev([w.model] * 4))
+vals = [float(v) for v in ev([w.model] * 4)]
 ev.close()
 ctx.close()
 print(repr(vals))
