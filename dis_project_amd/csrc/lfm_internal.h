@@ -117,8 +117,8 @@ constexpr int STATUS_TIMEOUT = -2;
 // LFM_OK, LFM_E_NOT_PD (pivot index in the message) or LFM_E_TIMEOUT for a status word.
 int status_code(lfm_ctx* ctx, double st, double why = 0.0);
 
-// The next factorisation on ctx runs schedule 3 (the CU-partitioned pair exists, and the
-// call holds the device's schedule-3 tenancy: lfm_api.hip S3Tenancy).
+// The next factorisation on ctx runs schedule 3: the CU-partitioned pair exists and the call
+// is not nested in a shared hold of the device's tenancy lock (lfm_api.hip DeviceTenancy).
 inline bool s3_on(const lfm_ctx* ctx) {
   return ctx->sched == 3 && ctx->side_cus > 0 && !ctx->s3_yield;
 }
