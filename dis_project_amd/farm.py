@@ -228,10 +228,11 @@ class Farm:
 
 # Measured C3 throughput on one MI355X at N = 16384 (scripts/concurrency_probe.py,
 # profiles/r03_concurrency.json), evaluations / s with c schedule-1 evaluations in flight, and
-# one schedule-3 evaluation at a time. Round 3's faster schedule-3 kernels put one schedule-3
-# evaluation at a time ahead of every concurrent count.
-_S1_RATE = {1: 28.6, 2: 33.8, 3: 35.3, 4: 33.7}
-_S3_RATE = 36.6
+# one schedule-3 evaluation at a time: the mean of round 3's two boxes (28.6 / 33.8 / 35.3 /
+# 33.7 and 36.6; 28.0 / 33.6 / 36.6 / 33.3 and 36.5). One schedule-3 evaluation at a time is
+# ahead of every concurrent count on average, and never runs an uneven remainder round.
+_S1_RATE = {1: 28.3, 2: 33.7, 3: 35.95, 4: 33.5}
+_S3_RATE = 36.55
 
 
 def predicted_seconds(k: int, workers: int) -> float:
