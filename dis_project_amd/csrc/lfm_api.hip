@@ -236,43 +236,26 @@ struct DeviceGuard {
 // anything but the GPU, so the order cannot deadlock; a nested request on a thread that already
 // holds the device's lock is a no-op (a shared holder asking for exclusive runs schedule 1).
 constexpr int kMaxDevices = 64;
-struct DevLock {
-  std::shared_mutex rw;   // in-process readers-writer lock
-  std::mutex turn_mu;     // serialises this process's threads at the turnstile
-  std::mutex fd_mu;       // guards readers / the flock state of `fd`
-  int readers = 0;        // this process's shared holders (flock LOCK_SH held while > 0)
-  int fd = 0, turn = 0;   // 0: not opened yet; -1: unavailable
-  std::string path;
-};
-DevLock g_dev[kMaxDevices];
+TenancyLock g_dev[kMaxDevices];  // lfm_host.cpp: the readers-writer lock itself
 std::mutex g_open_mu;
+bool g_dev_opened[kMaxDevices] = {};
 thread_local int t_depth[kMaxDevices] = {};
 thread_local bool t_excl[kMaxDevices] = {};
 
+// The device's lock files: $TMPDIR/lfm_gpu_<PCI bus id>.lock (and .turn), opened once
 void device_lock_open(int dev) {
   std::lock_guard<std::mutex> lk(g_open_mu);
-  DevLock& d = g_dev[dev];
-  if (d.fd != 0) return;
+  if (g_dev_opened[dev]) return;
+  g_dev_opened[dev] = true;
   char bus[64] = {0};
-  int fd = -1, turn = -1;
-  if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) == hipSuccess) {
-    for (char* c = bus; *c; ++c)
-      if (*c == ':' || *c == '.') *c = '_';
-    const char* tmp = std::getenv("TMPDIR");
-    d.path = std::string(tmp && *tmp ? tmp : "/tmp") + "/lfm_gpu_" + bus + ".lock";
-    fd = ::open(d.path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
-    const std::string tp = d.path.substr(0, d.path.size() - 5) + ".turn";
-    turn = ::open(tp.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) != hipSuccess) {
+    g_dev[dev].open("");  // in-process locking only
+    return;
   }
-  d.turn = turn >= 0 ? turn : -1;
-  d.fd = fd >= 0 && turn >= 0 ? fd : -1;
-  if (fd >= 0 && turn < 0) ::close(fd);
-}
-
-// flock, restarted when a signal interrupts the wait
-void flock_retry(int fd, int op) {
-  while (::flock(fd, op) != 0 && errno == EINTR) {
-  }
+  for (char* c = bus; *c; ++c)
+    if (*c == ':' || *c == '.') *c = '_';
+  const char* tmp = std::getenv("TMPDIR");
+  g_dev[dev].open(std::string(tmp && *tmp ? tmp : "/tmp") + "/lfm_gpu_" + bus + ".lock");
 }
 
 }  // namespace
@@ -281,8 +264,7 @@ namespace lfm {
 std::string tenancy_lock_path(int dev) {
   if (dev < 0 || dev >= kMaxDevices) return std::string();
   device_lock_open(dev);
-  std::lock_guard<std::mutex> lk(g_open_mu);
-  return g_dev[dev].path;
+  return g_dev[dev].path();
 }
 }  // namespace lfm
 
@@ -304,29 +286,10 @@ class DeviceTenancy {
       return;
     }
     device_lock_open(dev);
-    DevLock& d = g_dev[dev];
     dev_ = dev;
     excl_ = s3;
-    if (excl_) {
-      d.rw.lock();
-      if (d.fd > 0) {
-        std::lock_guard<std::mutex> tl(d.turn_mu);
-        flock_retry(d.turn, LOCK_EX);  // readers arriving from now on wait at the turnstile
-        flock_retry(d.fd, LOCK_EX);    // the readers already in drain
-        flock_retry(d.turn, LOCK_UN);
-      }
-    } else {
-      d.rw.lock_shared();
-      if (d.fd > 0) {
-        {
-          std::lock_guard<std::mutex> tl(d.turn_mu);
-          flock_retry(d.turn, LOCK_EX);  // behind any writer waiting in another process
-          flock_retry(d.turn, LOCK_UN);
-        }
-        std::lock_guard<std::mutex> fl(d.fd_mu);
-        if (d.readers++ == 0) flock_retry(d.fd, LOCK_SH);
-      }
-    }
+    if (excl_) g_dev[dev].lock_exclusive();
+    else g_dev[dev].lock_shared();
     t_depth[dev] = 1;
     t_excl[dev] = excl_;
   }
@@ -337,19 +300,10 @@ class DeviceTenancy {
       --t_depth[dev_];
       return;
     }
-    DevLock& d = g_dev[dev_];
     t_depth[dev_] = 0;
     t_excl[dev_] = false;
-    if (excl_) {
-      if (d.fd > 0) flock_retry(d.fd, LOCK_UN);
-      d.rw.unlock();
-    } else {
-      if (d.fd > 0) {
-        std::lock_guard<std::mutex> fl(d.fd_mu);
-        if (--d.readers == 0) flock_retry(d.fd, LOCK_UN);
-      }
-      d.rw.unlock_shared();
-    }
+    if (excl_) g_dev[dev_].unlock_exclusive();
+    else g_dev[dev_].unlock_shared();
   }
   DeviceTenancy(const DeviceTenancy&) = delete;
   DeviceTenancy& operator=(const DeviceTenancy&) = delete;

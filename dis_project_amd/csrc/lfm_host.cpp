@@ -2,7 +2,12 @@
 // into the host sanitizer check (tests/native/host_check.cpp).
 #include "lfm_host.h"
 
+#include <fcntl.h>
+#include <sys/file.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <climits>
 #include <cstring>
 
@@ -125,6 +130,78 @@ int64_t helper_clamp(int64_t hu, int nr, int T, int wn, int lead, int Q) {
     if (ti / 2 < wn + lead && tj < wn + lead) return 0;
   }
   return hu;
+}
+
+namespace {
+// flock, restarted when a signal interrupts the wait
+void flock_retry(int fd, int op) {
+  while (::flock(fd, op) != 0 && errno == EINTR) {
+  }
+}
+}  // namespace
+
+bool TenancyLock::open(const std::string& path) {
+  std::lock_guard<std::mutex> lk(open_mu_);
+  if (opened_) return ok_;
+  opened_ = true;
+  path_ = path;
+  if (path.size() < 5 || path.compare(path.size() - 5, 5, ".lock") != 0) return ok_ = false;
+  fd_ = ::open(path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  const std::string tp = path.substr(0, path.size() - 5) + ".turn";
+  turn_ = ::open(tp.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  if (fd_ < 0 || turn_ < 0) {
+    if (fd_ >= 0) ::close(fd_);
+    if (turn_ >= 0) ::close(turn_);
+    fd_ = turn_ = -1;
+    return ok_ = false;
+  }
+  return ok_ = true;
+}
+
+std::string TenancyLock::path() {
+  std::lock_guard<std::mutex> lk(open_mu_);
+  return path_;
+}
+
+void TenancyLock::lock_exclusive() {
+  rw_.lock();
+  if (fd_ >= 0) {
+    std::lock_guard<std::mutex> tl(turn_mu_);
+    flock_retry(turn_, LOCK_EX);  // readers arriving from now on wait at the turnstile
+    flock_retry(fd_, LOCK_EX);    // the readers already in drain
+    flock_retry(turn_, LOCK_UN);
+  }
+}
+
+void TenancyLock::unlock_exclusive() {
+  if (fd_ >= 0) flock_retry(fd_, LOCK_UN);
+  rw_.unlock();
+}
+
+void TenancyLock::lock_shared() {
+  rw_.lock_shared();
+  if (fd_ >= 0) {
+    {
+      std::lock_guard<std::mutex> tl(turn_mu_);
+      flock_retry(turn_, LOCK_EX);  // behind any writer waiting in another process
+      flock_retry(turn_, LOCK_UN);
+    }
+    std::lock_guard<std::mutex> fl(fd_mu_);
+    if (readers_++ == 0) flock_retry(fd_, LOCK_SH);
+  }
+}
+
+void TenancyLock::unlock_shared() {
+  if (fd_ >= 0) {
+    std::lock_guard<std::mutex> fl(fd_mu_);
+    if (--readers_ == 0) flock_retry(fd_, LOCK_UN);
+  }
+  rw_.unlock_shared();
+}
+
+TenancyLock::~TenancyLock() {
+  if (fd_ >= 0) ::close(fd_);
+  if (turn_ >= 0) ::close(turn_);
 }
 
 }  // namespace lfm

@@ -6,6 +6,9 @@
 
 #include <cmath>
 #include <cstdint>
+#include <mutex>
+#include <shared_mutex>
+#include <string>
 #include <utility>
 #include <vector>
 
@@ -82,5 +85,37 @@ int64_t helper_units(int kd, int na, int nr, int nt, int wnext, int nb, int cus,
 // enumeration mirror still finds a lead tile in the tail, and for band-enumerated regions
 // (T - wn <= kBandMaxCols).
 int64_t helper_clamp(int64_t hu, int nr, int T, int wn, int lead, int Q);
+
+// Readers-writer lock over one GPU's library work (lfm_api.hip DeviceTenancy: a schedule-3
+// factorisation exclusive, all other GPU work shared). In-process a std::shared_mutex; across
+// processes flock on `path` (LOCK_EX / LOCK_SH; the process's shared hold is counted over its
+// threads, taken by the first reader and dropped by the last) behind a turnstile file (`path`
+// with ".turn" for ".lock"): a writer holds the turnstile while it waits for the readers to
+// drain, and every reader passes through it first, so a stream of readers, of this process or
+// another, cannot starve a writer. flock is per open file description, so two TenancyLock
+// objects on one path behave like two processes. Waits block; nothing is held while waiting on
+// anything but these locks.
+class TenancyLock {
+ public:
+  // Opens (creating) the lock and turnstile files once; false: unavailable (the lock is then
+  // in-process only). Thread-safe; later calls return the first result.
+  bool open(const std::string& path);
+  void lock_exclusive();
+  void unlock_exclusive();
+  void lock_shared();
+  void unlock_shared();
+  std::string path();
+  ~TenancyLock();
+
+ private:
+  std::shared_mutex rw_;  // in-process readers-writer lock
+  std::mutex turn_mu_;    // this process's threads at the turnstile, one at a time
+  std::mutex fd_mu_;      // readers_ and the flock state of fd_
+  std::mutex open_mu_;
+  int readers_ = 0;       // this process's shared holders (LOCK_SH held while > 0)
+  int fd_ = -1, turn_ = -1;
+  bool opened_ = false, ok_ = false;
+  std::string path_;
+};
 
 }  // namespace lfm

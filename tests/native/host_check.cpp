@@ -2,12 +2,18 @@
 // C++ oracle (oracle/lfm_cpu.cpp) under AddressSanitizer + UBSan: built and run
 // by `make -C tests/native asan` (tests/test_host_asan.py). Exits non-zero on the first failed
 // check; the sanitizers abort on any memory / UB error.
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <random>
 #include <set>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "../../dis_project_amd/csrc/lfm_host.h"
@@ -204,7 +210,116 @@ static void check_oracle() {
   std::printf("oracle: mll %.10f\n", v1);
 }
 
+// The device tenancy lock (TenancyLock, lfm_api.hip DeviceTenancy). Two objects on one path
+// stand for two processes (flock is per open file description).
+static void check_tenancy() {
+  using clk = std::chrono::steady_clock;
+  auto ms_since = [](clk::time_point t) {
+    return std::chrono::duration<double, std::milli>(clk::now() - t).count();
+  };
+  char dir[] = "/tmp/lfm_tenancy_XXXXXX";
+  CHECK(mkdtemp(dir) != nullptr, "mkdtemp");
+  const std::string path = std::string(dir) + "/lfm_gpu_test.lock";
+  TenancyLock a, b;
+  CHECK(a.open(path) && b.open(path), "open");
+  CHECK(a.path() == path, "path");
+  TenancyLock bad;
+  CHECK(!bad.open(std::string(dir) + "/no_suffix"), "a path without .lock is refused");
+
+  // exclusive: mutual exclusion over threads
+  {
+    int counter = 0;
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 4; ++t)
+      ts.emplace_back([&] {
+        for (int i = 0; i < 2000; ++i) {
+          a.lock_exclusive();
+          const int v = counter;
+          counter = v + 1;
+          a.unlock_exclusive();
+        }
+      });
+    for (auto& t : ts) t.join();
+    CHECK(counter == 8000, "exclusive sections overlapped: %d", counter);
+  }
+  // shared: two readers inside at once
+  {
+    std::atomic<int> inside{0};
+    std::atomic<bool> both{false};
+    auto reader = [&] {
+      a.lock_shared();
+      ++inside;
+      const auto t0 = clk::now();
+      while (inside.load() < 2 && ms_since(t0) < 2000) std::this_thread::yield();
+      if (inside.load() == 2) both = true;
+      a.unlock_shared();
+    };
+    std::thread r1(reader), r2(reader);
+    r1.join();
+    r2.join();
+    CHECK(both.load(), "two shared holders were not admitted together");
+  }
+  // another "process" holding it exclusively: a shared request waits for the release
+  {
+    std::atomic<bool> held{false};
+    std::thread w([&] {
+      b.lock_exclusive();
+      held = true;
+      std::this_thread::sleep_for(std::chrono::milliseconds(200));
+      b.unlock_exclusive();
+    });
+    while (!held.load()) std::this_thread::yield();
+    const auto t0 = clk::now();
+    a.lock_shared();
+    const double waited = ms_since(t0);
+    a.unlock_shared();
+    w.join();
+    CHECK(waited >= 150.0, "shared request did not wait for the other writer (%.1f ms)", waited);
+  }
+  // turnstile: while a writer of another "process" waits for this process's reader, a second
+  // reader of this process queues behind the writer instead of joining the first reader
+  {
+    std::atomic<bool> r1_in{false}, w_waiting{false};
+    std::atomic<double> w_at{0.0}, r2_at{0.0};
+    const auto t0 = clk::now();
+    std::thread r1([&] {
+      a.lock_shared();
+      r1_in = true;
+      std::this_thread::sleep_for(std::chrono::milliseconds(300));
+      a.unlock_shared();
+    });
+    while (!r1_in.load()) std::this_thread::yield();
+    std::thread w([&] {
+      w_waiting = true;
+      b.lock_exclusive();
+      w_at = ms_since(t0);
+      std::this_thread::sleep_for(std::chrono::milliseconds(100));
+      b.unlock_exclusive();
+    });
+    while (!w_waiting.load()) std::this_thread::yield();
+    std::this_thread::sleep_for(std::chrono::milliseconds(80));  // the writer is queued now
+    std::thread r2([&] {
+      a.lock_shared();
+      r2_at = ms_since(t0);
+      a.unlock_shared();
+    });
+    r1.join();
+    w.join();
+    r2.join();
+    CHECK(w_at.load() >= 250.0, "writer got in before the reader left (%.1f ms)", w_at.load());
+    CHECK(r2_at.load() >= w_at.load() + 80.0,
+          "second reader overtook the waiting writer (writer %.1f, reader %.1f ms)", w_at.load(),
+          r2_at.load());
+  }
+  std::string turn = path.substr(0, path.size() - 5) + ".turn";
+  unlink(path.c_str());
+  unlink(turn.c_str());
+  rmdir(dir);
+  std::printf("tenancy lock: ok\n");
+}
+
 int main() {
+  check_tenancy();
   check_enumeration();
   check_helper_clamp();
   check_detect_grid();

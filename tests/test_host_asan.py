@@ -1,7 +1,8 @@
 """Host code under AddressSanitizer + UBSan: liblfm's host-only logic
 (dis_project_amd/csrc/lfm_host.cpp: x-layout detection, the factorisation's step plan, the
 host mirror of the trailing update's unit enumeration, the side-CU helper's sizing and lead
-clamp) and the C++ oracle (oracle/lfm_cpu.cpp), built by tests/native/Makefile and run by
+clamp, the device tenancy lock: mutual exclusion, shared admission, cross-process waits and the
+turnstile) and the C++ oracle (oracle/lfm_cpu.cpp), built by tests/native/Makefile and run by
 tests/native/host_check.cpp. CPU only."""
 
 import os
