@@ -350,6 +350,9 @@ def make_gather(ctx, world, rank, mode, rccl=None):
         return farm.TorchGather(world), "gloo"
     if rccl is None:
         rccl = farm.RcclGather
+    # a peer that never joins ends the init after this bound (then the gloo fallback), not at
+    # the library's 300 s default
+    os.environ.setdefault("LFM_RCCL_TIMEOUT_S", "120")
     uid = None
     if rank == 0:
         uid = farm.RcclGather.unique_id(ctx) if rccl is farm.RcclGather else b"\0" * 128
