@@ -138,6 +138,14 @@ void flock_retry(int fd, int op) {
   while (::flock(fd, op) != 0 && errno == EINTR) {
   }
 }
+
+// flock needs no write access: a file another user created (mode 0666 less their umask) is
+// opened read-only rather than dropping to in-process locking
+int open_lock_file(const std::string& p) {
+  int fd = ::open(p.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  if (fd < 0 && errno == EACCES) fd = ::open(p.c_str(), O_RDONLY | O_CLOEXEC);
+  return fd;
+}
 }  // namespace
 
 bool TenancyLock::open(const std::string& path) {
@@ -146,9 +154,8 @@ bool TenancyLock::open(const std::string& path) {
   opened_ = true;
   path_ = path;
   if (path.size() < 5 || path.compare(path.size() - 5, 5, ".lock") != 0) return ok_ = false;
-  fd_ = ::open(path.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
-  const std::string tp = path.substr(0, path.size() - 5) + ".turn";
-  turn_ = ::open(tp.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  fd_ = open_lock_file(path);
+  turn_ = open_lock_file(path.substr(0, path.size() - 5) + ".turn");
   if (fd_ < 0 || turn_ < 0) {
     if (fd_ >= 0) ::close(fd_);
     if (turn_ >= 0) ::close(turn_);
