@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread -m gpu \
-  tests/test_gpu_edges.py tests/test_gpu_tenancy.py > gpurun_out/s2_edges.log 2>&1
+  tests/test_gpu_edges.py > gpurun_out/s2_edges.log 2>&1
 rc=$?
 tail -5 gpurun_out/s2_edges.log
 exit $rc
