@@ -143,7 +143,9 @@ int lfm_gram_f32(lfm_ctx* ctx, const double* x, int64_t n, const lfm_hyp* hyp, d
                  int uplo, float* out, int64_t ldo);
 
 /* --------------------------------- CustomConjMLL.step (objectives.py:21-78) */
-/* out = constant * log N(y; m, K + jitter I + obs_stddev^2 I), constant = -1 if negative. */
+/* out = constant * log N(y; m, K + jitter I + obs_stddev^2 I), constant = -1 if negative.
+ * n >= 1 and n % num_genes == 0 (mean_function's broadcast, model.py:145-149), else
+ * LFM_E_ARG; the same holds for lfm_mll_batch_f64's problems and lfm_mll_grad_f64. */
 int lfm_mll_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n, const lfm_hyp* hyp,
                 int negative, double* out);
 /* nprob independent problems; out[p] per problem (NaN where not PD); status[p] optional. */
