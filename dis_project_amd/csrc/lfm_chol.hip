@@ -940,11 +940,10 @@ struct Panel {
   int64_t ld, r0;
 };
 
+// schedule 1's 64-row SYRK (syrk_kernel<., 64>): workgroups per CU in its launch bounds
 #ifndef LFM_SLAB_WGS
 #define LFM_SLAB_WGS 3
 #endif
-// Bulk trailing update (step_kernel's update units): K depth of one LDS stage and the unroll
-// of the 4-deep MFMA steps within it
 // schedule-3 MLL bulk super-panel width in block columns
 #ifndef LFM_WBULK
 #define LFM_WBULK 5
@@ -963,6 +962,8 @@ struct Panel {
 #ifndef LFM_BAND_ROWS
 #define LFM_BAND_ROWS 1
 #endif
+// Bulk trailing update (step_kernel's update units): K depth of one LDS stage (32: 130 VGPRs +
+// 64 AGPRs, 2 waves / SIMD)
 #ifndef LFM_STEP_KS
 #define LFM_STEP_KS 16
 #endif
