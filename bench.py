@@ -45,16 +45,31 @@ import subprocess
 import sys
 import time
 
-import torch  # first: liblfm then binds to the HIP runtime torch loaded (see _lib.py)
-import torch.distributed as dist
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import numpy as np  # noqa: E402
+# torch and liblfm are imported by the rank path only (_load): the launcher of `--gpus N` must
+# stay free of the HIP runtime — importing torch maps libamdhip64, and a process that has
+# initialised HIP must not start GPU processes (tests/test_bench_launcher.py checks both)
+torch = dist = _lib = configs = farm = None
 
-from dis_project_amd import _lib  # noqa: E402
-from dis_project_amd import configs, farm  # noqa: E402
+
+def _load():
+    """Import torch (first: liblfm then binds to the HIP runtime torch loaded, see _lib.py),
+    torch.distributed and the product package into this module's namespace."""
+    global torch, dist, _lib, configs, farm
+    if _lib is not None:
+        return
+    import torch as _torch
+    import torch.distributed as _dist
+
+    from dis_project_amd import _lib as _l
+    from dis_project_amd import configs as _c
+    from dis_project_amd import farm as _f
+
+    torch, dist, _lib, configs, farm = _torch, _dist, _l, _c, _f
 
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix, AMD spec (not in the local guide)
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -86,7 +101,14 @@ def parse(argv=None):
                         "(W ranks on fewer cards); the measured configuration is rccl")
     p.add_argument("--share-gpus", action="store_true",
                    help="rehearsal only: ranks share the visible GPUs (rank -> local %% count)")
+    p.add_argument("--require-rccl", dest="require_rccl", action="store_true", default=None,
+                   help="an RCCL communicator failure on any rank ends the run (non-zero exit, "
+                        "the cause on stderr) instead of exchanging over gloo; the default "
+                        "unless rehearsing (--share-gpus / --gather gloo)")
+    p.add_argument("--no-require-rccl", dest="require_rccl", action="store_false")
     a = p.parse_args(argv)
+    if a.require_rccl is None:
+        a.require_rccl = not (a.share_gpus or a.gather == "gloo")
     if a.workload is None:
         a.workload = "c2" if a.gpus == 1 else "c3"
     if a.genes is None:
@@ -103,9 +125,95 @@ def _free_port() -> int:
     return port
 
 
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+
+
+class GpuCountError(RuntimeError):
+    """The launcher could not count the GPUs without the HIP runtime."""
+
+
+def _kfd_gpus(root: str) -> list:
+    """The GPU agents of the KFD topology (sysfs), in node order — the order the ROCm runtime
+    enumerates them: a node with gpu_id != 0 whose DRM render node (/dev/dri/renderD<minor>,
+    from its properties) exists and is readable and writable by this process (a container sees
+    the render nodes of its own cards only). Returns [{"node", "unique_id"}]. Reads text files
+    only: no HIP, no /dev/kfd."""
+    try:
+        nodes = sorted((int(d) for d in os.listdir(root) if d.isdigit()))
+    except OSError as e:
+        raise GpuCountError(f"cannot read the KFD topology at {root}: {e}") from None
+    dri = os.environ.get("LFM_DRI_DIR", "/dev/dri")
+    out = []
+    for k in nodes:
+        base = os.path.join(root, str(k))
+        try:
+            with open(os.path.join(base, "gpu_id")) as f:
+                gpu_id = int(f.read().strip() or "0")
+        except (OSError, ValueError):
+            continue
+        if gpu_id == 0:  # a CPU agent
+            continue
+        props = {}
+        try:
+            with open(os.path.join(base, "properties")) as f:
+                for line in f:
+                    kv = line.split()
+                    if len(kv) == 2:
+                        props[kv[0]] = kv[1]
+        except OSError:
+            pass
+        minor = props.get("drm_render_minor")
+        if minor is not None and int(minor) > 0:
+            dev = os.path.join(dri, f"renderD{int(minor)}")
+            if not os.access(dev, os.R_OK | os.W_OK):
+                continue
+        out.append({"node": k, "unique_id": int(props.get("unique_id", "0") or 0)})
+    return out
+
+
+def _apply_visible(agents: list, spec: str | None) -> list:
+    """Narrow a device list by a *_VISIBLE_DEVICES value as the runtime does: comma-separated
+    indices into the list (or GPU-<hex unique id>), parsing stops at the first entry that names
+    no device; unset keeps the list, empty hides every device."""
+    if spec is None:
+        return agents
+    out = []
+    for tok in (t.strip() for t in spec.split(",")):
+        if not tok:
+            break
+        if tok.upper().startswith("GPU-"):
+            try:
+                uid = int(tok[4:], 16)
+            except ValueError:
+                break
+            hit = [a for a in agents if a.get("unique_id") == uid]
+            if not hit:
+                break
+            out.append(hit[0])
+            continue
+        try:
+            i = int(tok)
+        except ValueError:
+            break
+        if not 0 <= i < len(agents):
+            break
+        out.append(agents[i])
+    return out
+
+
 def visible_gpus() -> int:
-    """GPUs this process could use, counted without initialising the HIP runtime."""
-    return torch.cuda.device_count()
+    """GPUs a rank process of this launcher could use, counted WITHOUT the HIP runtime (the
+    launcher then starts the rank processes; a parent that had initialised HIP must not): the
+    KFD topology's GPU agents with an accessible render node (``LFM_KFD_TOPOLOGY`` overrides
+    the sysfs path, for tests), narrowed by ROCR_VISIBLE_DEVICES, then HIP_VISIBLE_DEVICES (or
+    CUDA_VISIBLE_DEVICES). Raises GpuCountError if the topology cannot be read — the launcher
+    then refuses rather than fall back to a count that initialises HIP."""
+    agents = _kfd_gpus(os.environ.get("LFM_KFD_TOPOLOGY", KFD_TOPOLOGY))
+    agents = _apply_visible(agents, os.environ.get("ROCR_VISIBLE_DEVICES"))
+    hip = os.environ.get("HIP_VISIBLE_DEVICES")
+    if hip is None:
+        hip = os.environ.get("CUDA_VISIBLE_DEVICES")
+    return len(_apply_visible(agents, hip))
 
 
 def self_launch(a, argv, script=None) -> int:
@@ -116,7 +224,13 @@ def self_launch(a, argv, script=None) -> int:
         print("bench.py: --gpus must be >= 1", file=sys.stderr)
         return 2
     if not (a.share_gpus or a.gather == "gloo"):
-        vis = visible_gpus()
+        try:
+            vis = visible_gpus()
+        except GpuCountError as e:
+            print(f"bench.py: {e}; refusing to start {n} rank processes (the launcher never "
+                  "initialises HIP to count GPUs; run under torch.distributed.run, or rehearse "
+                  "with --share-gpus --gather gloo)", file=sys.stderr)
+            return 3
         if vis < n:
             print(f"bench.py: --gpus {n} requested but only {vis} GPU(s) are visible "
                   "(rehearsal on fewer cards: --share-gpus --gather gloo)", file=sys.stderr)
@@ -337,13 +451,15 @@ def c4_setup(ctx, a):
     return work, step, rows, close
 
 
-def make_gather(ctx, world, rank, mode, rccl=None):
+def make_gather(ctx, world, rank, mode, rccl=None, require=False):
     """The farm's result exchange for this rank: (gather, kind). kind "rccl": the library's
     RCCL all-gather (non-blocking communicator, every wait bounded by LFM_RCCL_TIMEOUT_S);
     "gloo": the rehearsal's torch.distributed all-gather; "gloo-fallback": any rank's RCCL
     communicator failed to initialise, so every rank (they agree over the gloo control plane)
-    exchanges over gloo instead. rccl(ctx, world, rank, uid) builds the communicator (tests pass
-    a stand-in); the unique id comes from rank 0."""
+    exchanges over gloo instead — unless `require` (bench.py --require-rccl, the default outside
+    rehearsals), when every rank exits non-zero naming the cause. rccl(ctx, world, rank, uid)
+    builds the communicator (tests pass a stand-in); the unique id comes from rank 0."""
+    _load()
     if world <= 1:
         return (lambda send: np.asarray(send, np.float64).copy()), "none"
     if mode == "gloo":
@@ -367,12 +483,16 @@ def make_gather(ctx, world, rank, mode, rccl=None):
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if int(ok.item()):
         return gather, "rccl"
-    # one rank's communicator failed: every rank exchanges over gloo instead, and the line says
-    # so (the evaluations themselves are unaffected)
     if gather is not None:
         gather.close()
-    print(f"rank {rank}: RCCL communicator unavailable "
-          f"({err if err is not None else 'failed on another rank'}); "
+    cause = err if err is not None else "failed on another rank"
+    if require:
+        # the measured configuration is RCCL over xGMI: no gloo line stands in for it
+        raise SystemExit(f"rank {rank}: RCCL communicator unavailable ({cause}); "
+                         "--require-rccl (the default outside rehearsals) ends the run")
+    # one rank's communicator failed: every rank exchanges over gloo instead, and the line says
+    # so (the evaluations themselves are unaffected)
+    print(f"rank {rank}: RCCL communicator unavailable ({cause}); "
           "results exchanged over gloo", file=sys.stderr, flush=True)
     return farm.TorchGather(world), "gloo-fallback"
 
@@ -382,6 +502,7 @@ def main(argv=None):
     a = parse(argv)
     if "WORLD_SIZE" not in os.environ and a.gpus > 1:
         return self_launch(a, argv)
+    _load()
     if os.environ.get("LFM_BENCH_WATCHDOG"):
         # diagnostics: dump every thread's Python stack (and exit) if the run outlives this
         import faulthandler
@@ -405,7 +526,7 @@ def main(argv=None):
     lib, h = ctx.lib, ctx.handle
 
     # farm communicator (replicas-only exchange of per-rank results)
-    gather, exchange = make_gather(ctx, world, rank, a.gather)
+    gather, exchange = make_gather(ctx, world, rank, a.gather, require=a.require_rccl)
     fm = farm.Farm(world, rank, gather)
 
     workers = None
@@ -474,10 +595,12 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     if prof:
         stats = ctx.profile_read()
+    # per-step wall (each step ends on the host: its results are read back), median per rank
+    med_ms = float(np.median(step_ms))
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = torch.tensor([elapsed, med_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, med_ms = (float(v) for v in t.tolist())
     # the exchange step alone (collective latency reported separately): the same
     # all-gather of this workload's NaN-padded slots, outside the timed region
     collective = None
@@ -495,6 +618,27 @@ def main(argv=None):
                              "gloo-fallback": "gloo all_gather (RCCL init failed)"}[exchange],
                       "bytes_per_rank": 8 * slots,
                       "latency_us_median": float(lt.item())}
+    elif a.workload in ("c3", "c5"):
+        # one GPU: the library's exchange path alone on a 1-rank RCCL communicator (staging
+        # copies, enqueue, the bounded host wait; no xGMI transfer) — the floor the W > 1
+        # all-gather adds to per step. Best effort: a box without RCCL just omits it.
+        slots = max(per_step, 1)
+        try:
+            g1 = farm.RcclGather(ctx, 1, 0, farm.RcclGather.unique_id(ctx))
+            try:
+                lat = []
+                for i in range(120):
+                    t1 = time.perf_counter()
+                    g1(np.full(slots, np.nan))
+                    lat.append((time.perf_counter() - t1) * 1e6)
+            finally:
+                g1.close()
+            collective = {"op": "ncclAllGather (RCCL, 1 rank: the library's host path only, "
+                                "no xGMI transfer)",
+                          "bytes_per_rank": 8 * slots,
+                          "latency_us_median": float(np.median(lat[20:]))}
+        except Exception as e:  # noqa: BLE001
+            collective = {"op": "ncclAllGather (RCCL, 1 rank)", "error": str(e)}
     # the timed region's results: all finite, every step the same values (same inputs)
     res = np.array(timed)
     if not np.all(np.isfinite(res)):
@@ -502,8 +646,12 @@ def main(argv=None):
     if not np.all(res == res[0]):
         raise SystemExit("timed steps disagree (the same inputs gave different results)")
 
-    value = per_step * a.steps / elapsed
-    ms_per_step = elapsed / a.steps * 1e3
+    # value: the median step, max over ranks — one slow step (a clock dip, the
+    # first step's HIP-event records) does not move it; the mean over the K steps between the
+    # barriers is kept beside it (mean_value, mean_ms_per_step)
+    mean_ms = elapsed / a.steps * 1e3
+    value = per_step * 1e3 / med_ms
+    ms_per_step = med_ms
     chol_flops = n**3 / 3.0
     scaling = "strong" if a.workload in ("c3", "c5") else "weak"
     if a.workload == "c2":
@@ -529,7 +677,10 @@ def main(argv=None):
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": ms_per_step,
-        "median_ms_per_step": float(np.median(step_ms)),
+        "value_basis": "median step wall time (max over ranks of each rank's median)",
+        "mean_value": per_step * a.steps / elapsed,
+        "mean_ms_per_step": mean_ms,
+        "timed_region_s": elapsed,
         "higher_is_better": True,
         "scaling": scaling,
         "vs_baseline": None,

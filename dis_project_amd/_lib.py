@@ -33,7 +33,7 @@ LFM_E_OOM = 4
 LFM_E_RCCL = 5
 LFM_E_STATE = 6
 LFM_E_TIMEOUT = 7
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 LFM_UPLO_FULL = 0
 LFM_UPLO_LOWER = 1
@@ -102,6 +102,7 @@ PRODUCT_SIGNATURES = [
     ("lfm_ctx_set_block", c_int, [_c_ctx, c_int]),
     ("lfm_ctx_set_schedule", c_int, [_c_ctx, c_int]),
     ("lfm_ctx_get_schedule", c_int, [_c_ctx, POINTER(c_int)]),
+    ("lfm_ctx_fallbacks", c_int, [_c_ctx, POINTER(c_int64)]),
     ("lfm_mean_function_f64", c_int, [_c_ctx, _dptr, c_int64, POINTER(LfmHyp), _dptr]),
     ("lfm_cross_covariance_f64", c_int,
      [_c_ctx, _dptr, c_int64, _dptr, c_int64, POINTER(LfmHyp), _dptr, c_int64]),
@@ -117,6 +118,10 @@ PRODUCT_SIGNATURES = [
       _dptr]),
     ("lfm_mll_batch_f64", c_int,
      [_c_ctx, c_int64, POINTER(LfmProblem), c_int, _dptr, POINTER(c_int)]),
+    ("lfm_batch_create", c_int, [_c_ctx, c_int64, POINTER(LfmProblem), POINTER(c_void_p)]),
+    ("lfm_batch_destroy", c_int, [c_void_p]),
+    ("lfm_batch_hyp_size", c_int, [c_void_p, POINTER(c_int64)]),
+    ("lfm_batch_mll_f64", c_int, [_c_ctx, c_void_p, _dptr, c_int, _dptr, _dptr]),
     ("lfm_log_prob_f64", c_int, [_c_ctx, _dptr, _dptr, c_int64, c_int64, _dptr, _dptr]),
     ("lfm_h_f64", c_int,
      [_c_ctx, POINTER(LfmHyp), POINTER(c_int64), POINTER(c_int64), _dptr, _dptr, c_int64, _dptr]),
@@ -236,9 +241,14 @@ class HypArgs:
             self.d.size, self.d.ctypes.data, self.s.ctypes.data, self.b.ctypes.data,
             float(l), float(obs_stddev), float(jitter),
         )
+        # the struct holds plain addresses: it keeps this object (and so the arrays) alive, so
+        # a struct or a byref of it passed on alone never outlives its buffers
+        self.struct._owner = self
 
     @property
     def ref(self):
+        """byref(struct): the CArgObject keeps the struct, which keeps this object and its
+        arrays alive for as long as the reference is held (e.g. across a call)."""
         return ctypes.byref(self.struct)
 
 
@@ -293,6 +303,14 @@ class Context:
     @schedule.setter
     def schedule(self, value: int):
         self.check(self.lib.lfm_ctx_set_schedule(self.handle, int(value)))
+
+    @property
+    def fallbacks(self) -> int:
+        """Schedule-3 calls of this context re-run on schedule 1 after a device-side wait ran
+        out (include/lfm.h ``lfm_ctx_fallbacks``); their results are valid."""
+        out = c_int64(0)
+        self.check(self.lib.lfm_ctx_fallbacks(self.handle, ctypes.byref(out)))
+        return out.value
 
     # -- profiling
     def profile(self, on: bool = True, classes=None):

@@ -1240,17 +1240,36 @@ __global__ __launch_bounds__(256, TR == 64 ? LFM_SLAB_WGS : 2) void syrk_kernel(
   syrk_unit<CIO, TR>(A, lda, s, P, kd, T, tj_lo, tj_hi, b + skip, ti0, sP);
 }
 
+// Device-side waits are bounded in TIME, on the 100 MHz constant clock (s_memrealtime), not
+// in polls: `limit` ticks (ctx->wait_ticks, LFM_DEVICE_WAIT_MS; 2 s by default), so a wait
+// starved by another tenant of the GPU ends after a known time whatever the poll rate, and the
+// call re-runs on schedule 1 (lfm_api.hip). limit = 0 fails at once (the LFM_DEBUG_SPIN_LIMIT
+// test knob). A wait also ends as soon as another wait of the call has recorded a timeout
+// (`status`), so one stall drains the whole factorisation within one bound.
+__device__ __forceinline__ unsigned long long wall_ticks() { return __builtin_amdgcn_s_memrealtime(); }
+
 // Bounded relaxed / acquire spin on a device counter: true once *p >= target, false after
-// `limit` polls (the caller records PANEL_TIMEOUT). limit = 0 fails at once (the
-// LFM_DEBUG_SPIN_LIMIT test knob).
-template <bool ACQ = true>
-__device__ __forceinline__ bool spin_until(const unsigned* p, unsigned target, unsigned limit) {
-  unsigned it = 0;
-  while (__hip_atomic_load(p, ACQ ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-             target &&
-         ++it < limit)
-    __builtin_amdgcn_s_sleep(2);
-  return it < limit;
+// `limit` ticks or once *status records a timeout (the caller records PANEL_TIMEOUT).
+template <bool ACQ = true, int SLEEP = 2>
+__device__ __forceinline__ bool spin_until(const unsigned* p, unsigned target, unsigned limit,
+                                           const int* status = nullptr) {
+  auto ready = [&] {
+    return __hip_atomic_load(p, ACQ ? __ATOMIC_ACQUIRE : __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT) >= target;
+  };
+  if (ready()) return true;
+  if (limit == 0) return false;
+  const unsigned long long t0 = wall_ticks();
+  for (unsigned it = 1; !ready(); ++it) {
+    if ((it & 15) == 0) {
+      if (wall_ticks() - t0 > limit) return false;
+      if (status &&
+          __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == PANEL_TIMEOUT)
+        return false;
+    }
+    __builtin_amdgcn_s_sleep(SLEEP);
+  }
+  return true;
 }
 
 // One main-stream launch per super-panel step s (schedule 3): step s's trailing update from
@@ -1286,7 +1305,7 @@ struct StepArgs {
   // rows < wn + lead) write through to memory and bump *xready when done
   unsigned* xready;  // NULL: no chain waits on this launch
   int lead;
-  unsigned spin;     // poll bound of every device-side wait (PANEL_TIMEOUT past it)
+  unsigned spin;     // time bound of every device-side wait, ticks (PANEL_TIMEOUT past it)
   unsigned long long* stamps;  // diagnostics (NULL: off): [8] launch stamps, lfm_diag.h
   int64_t pad_end;   // rows in (n, pad_end) are skipped identity padding (INT64_MAX: every
                      // row past n; n + 1: none)
@@ -1427,12 +1446,12 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
     // an agent-scope acquire invalidates this XCD's L2 under the running bulk units
     if (threadIdx.x == 0) {
       int why = 0;
-      bool good = !g.chain_done || spin_until<false>(g.chain_done, 1u, g.spin);
+      bool good = !g.chain_done || spin_until<false>(g.chain_done, 1u, g.spin, g.status);
       if (!good) why = 1;
       // rows past step s's update (bordered: the border rows that entered the window with
       // super-panel s + 1, zero in every earlier panel column) have no ahead unit to wait for
       if (good && g.a_done && (i0 - g.s0) / ST < g.T) {
-        good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], 2u * g.wn, g.spin);
+        good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], 2u * g.wn, g.spin, g.status);
         if (!good) why = 2;
       }
       if (!good) timeout_at(g.status, why);
@@ -1553,9 +1572,10 @@ __global__ __launch_bounds__(256, 4) void helper_update_kernel_traced(StepArgs g
 constexpr size_t PANEL_LDS = (size_t)MB_DOUBLES * sizeof(double);
 static_assert(MB_DOUBLES >= 64 * (NB + 1) && MB_DOUBLES >= (64 + ST) * (KB + LDP), "LDS union");
 
-__device__ __forceinline__ bool wait_counter(unsigned* p, unsigned target, unsigned limit) {
+__device__ __forceinline__ bool wait_counter(unsigned* p, unsigned target, unsigned limit,
+                                             const int* status) {
   __shared__ int ok;
-  if (threadIdx.x == 0) ok = spin_until<true>(p, target, limit);
+  if (threadIdx.x == 0) ok = spin_until<true>(p, target, limit, status);
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   return ok;
@@ -1595,7 +1615,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(&sync[1], 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     if (b == 1) return;
-    if (!wait_counter(&sync[1], 2u * epoch, spin)) {
+    if (!wait_counter(&sync[1], 2u * epoch, spin, status)) {
       if (tid == 0) {
         timeout_at(status, 7);
         __hip_atomic_store(&sync[0], epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
@@ -1615,7 +1635,7 @@ __global__ __launch_bounds__(256) void panel_kernel(double* __restrict__ A, int6
   for (int ir = 0; ir < 8; ++ir)
 #pragma unroll
     for (int jr = 0; jr < 4; ++jr) sA[wr + ir * 4 + lk][wc + jr * 16 + li] = -acc[ir][jr];
-  if (!wait_counter(&sync[0], epoch, spin)) {
+  if (!wait_counter(&sync[0], epoch, spin, status)) {
     if (tid == 0) timeout_at(status, 7);
     return;
   }
@@ -1655,7 +1675,7 @@ struct ChainArgs {
   int64_t K0p;             // first column of super-panel s - 1
   const double* Bdp;       // Bd_{s-1}: kd x kd, ld kd
   double* xd;              // W x kd scratch
-  unsigned spin;           // poll bound of the input wait (grid barriers: spin / 4)
+  unsigned spin;           // time bound of the input wait, ticks (grid barriers: spin / 4)
 };
 
 // dynamic LDS of chain_kernel: the factor block and its inverse (packed 16x16 blocks)
@@ -1670,17 +1690,8 @@ __device__ __forceinline__ bool grid_sync(unsigned* bar, unsigned target, int* s
   if (threadIdx.x == 0) {
     __threadfence();
     __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned it = 0;
-    bool good = true;
-    while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (++it >= limit ||
-          __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == PANEL_TIMEOUT) {
-        good = false;
-        timeout_at(status, 6);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
+    const bool good = spin_until<true, 1>(bar, target, limit, status);
+    if (!good) timeout_at(status, 6);
     ok = good;
   }
   __syncthreads();
@@ -1698,17 +1709,8 @@ __device__ __forceinline__ bool grid_sync_light(unsigned* bar, unsigned target, 
   __syncthreads();
   if (threadIdx.x == 0) {
     __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned it = 0;
-    bool good = true;
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      if (++it >= limit ||
-          __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == PANEL_TIMEOUT) {
-        good = false;
-        timeout_at(status, 6);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
+    const bool good = spin_until<false, 1>(bar, target, limit, status);
+    if (!good) timeout_at(status, 6);
     ok = good;
   }
   __syncthreads();
@@ -1845,7 +1847,7 @@ __global__ __launch_bounds__(256) void chain_kernel(ChainArgs g) {
   if (g.xready) {
     __shared__ int okx;
     if (tid == 0) {
-      okx = spin_until<false>(g.xready, g.xtarget, g.spin);
+      okx = spin_until<false>(g.xready, g.xtarget, g.spin, g.status);
       if (!okx) timeout_at(g.status, 5);
     }
     __syncthreads();
@@ -2160,7 +2162,7 @@ struct Launcher {
     prof_begin(ctx, K_PANEL, &ev, st);
     hipLaunchKernelGGL(panel_kernel, dim3((unsigned)(2 + rows / 64)), dim3(256), PANEL_LDS, st, A,
                        lda, kb, pkb, pkd, n, ctx->linvT, ctx->parts, (int)k, ctx->status,
-                       ctx->psync, epoch, ctx->spin_limit);
+                       ctx->psync, epoch, ctx->wait_ticks);
     prof_end(ctx, K_PANEL, ev,
              (double)NB * NB * NB / 3.0 + (double)rows * NB * NB + 2.0 * (rows + NB) * NB * pkd,
              0, st);
@@ -2217,7 +2219,7 @@ int probe_update_launch(lfm_ctx* ctx, hipStream_t st, int T, int kd, int cio, in
     g.nr = (int)units;
     g.n = n;
     g.pad_end = INT64_MAX;
-    g.spin = ctx->spin_limit;
+    g.spin = ctx->wait_ticks;
     g.zero_from = (cio & 32) ? 0 : INT64_MAX;
     g.copy_from = INT64_MAX;
     double* xs = ctx->A + (size_t)n * n;  // [X_s | X_{s+1} | counters]
@@ -2431,7 +2433,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       c.zvec = ctx->zvec;
       c.bar = bars + s;
       c.done = chain_done + s;
-      c.spin = ctx->spin_limit;
+      c.spin = ctx->wait_ticks;
       c.stamps = ctx->dbg_stamps ? ctx->dbg_stamps + 16 * (size_t)std::min(s, 255) : nullptr;
       hipEvent_t pe;
       prof_begin(ctx, K_POTRF, &pe, side);
@@ -2456,7 +2458,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.pad_end = pad_end;
       if (!g.zero_from) g.zero_from = INT64_MAX;
       if (!g.copy_from) g.copy_from = INT64_MAX;
-      g.spin = ctx->spin_limit;
+      g.spin = ctx->wait_ticks;
       const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 + (int64_t)(g.nr + 7) / 8 * 8 +
                            (int64_t)(g.nt + 7) / 8 * 8;
       if (grid == 0) return;
@@ -2706,21 +2708,28 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
                                                         int* __restrict__ status) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const SmallProb P = probs[blockIdx.x];
-  const int n = P.n, M = n + 1, ld = n + 2;
+  const int n = P.n, M = n + 1, ld = n + 2, G = P.G;
   const int tid = threadIdx.x;
-  HypDev h{P.D, P.S, P.B, P.G, P.l};
   double* red = sm + (size_t)M * ld;  // [8] reduction scratch + [1] flag
+  // hyperparameters staged in LDS (they may live in pinned host memory: read once)
+  double* hyp = red + 16;             // D S B (3G), l, obs_stddev, jitter
+  for (int i = tid; i < 3 * G; i += 256) hyp[i] = P.dsb[i];
+  if (tid < 3) hyp[3 * G + tid] = P.sc[tid];
+  __syncthreads();
+  const HypDev h{hyp, hyp + G, hyp + 2 * G, G, hyp[3 * G]};
+  const double jitter = hyp[3 * G + 2], sd = hyp[3 * G + 1];
+  const double noise = sd * sd;  // objectives.py:66
   for (int idx = tid; idx < n * n; idx += 256) {
     const int i = idx / n, c = idx - i * n;
     if (c <= i) {
       const double* xa = P.x + 3 * i;
       const double* xb = P.x + 3 * c;
       double v = kernel_ref(h, xa[0], xa[1], xa[2], xb[0], xb[1], xb[2]);
-      if (i == c) v = (v + P.jitter) + P.noise;
+      if (i == c) v = (v + jitter) + noise;
       sm[i * ld + c] = v;
     }
   }
-  const int64_t bs = n / P.G;
+  const int64_t bs = n / G;
   for (int c = tid; c < n; c += 256) sm[n * ld + c] = P.y[c] - mean_at(h, P.x, c, bs);
   if (tid == 0) red[8] = 0.0;
   __syncthreads();
@@ -2772,9 +2781,9 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
   }
 }
 
-int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn, int negative,
-                       double* d_out, int* d_status) {
-  const size_t lds = ((size_t)(maxn + 1) * (maxn + 2) + 16) * sizeof(double);
+int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn, int maxg,
+                       int negative, double* d_out, int* d_status) {
+  const size_t lds = ((size_t)(maxn + 1) * (maxn + 2) + 16 + 3 * (size_t)maxg + 3) * sizeof(double);
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&small_mll_kernel),

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cerrno>
 #include <climits>
+#include <cstdio>
 #include <cstring>
 
 namespace lfm {
@@ -133,9 +134,11 @@ int64_t helper_clamp(int64_t hu, int nr, int T, int wn, int lead, int Q) {
 }
 
 namespace {
-// flock, restarted when a signal interrupts the wait
-void flock_retry(int fd, int op) {
-  while (::flock(fd, op) != 0 && errno == EINTR) {
+// flock, restarted when a signal interrupts the wait; 0 or the errno of the failure
+int flock_retry(int fd, int op) {
+  for (;;) {
+    if (::flock(fd, op) == 0) return 0;
+    if (errno != EINTR) return errno;
   }
 }
 
@@ -170,38 +173,68 @@ std::string TenancyLock::path() {
   return path_;
 }
 
+// The first flock failure (ENOLCK on a filesystem without locks, EBADF, ...) turns the
+// cross-process part off for good: logged once with the cause, so a later schedule-3 stall
+// beside another process can be traced to the missing lock; the in-process lock still holds.
+bool TenancyLock::files() const { return fd_ >= 0 && err_.load(std::memory_order_acquire) == 0; }
+
+void TenancyLock::fail(int e, const char* what) {
+  int expected = 0;
+  if (err_.compare_exchange_strong(expected, e))
+    std::fprintf(stderr,
+                 "liblfm: flock(%s) on %s failed: %s; the schedule-3 tenancy lock is in-process "
+                 "only from now on (another process on this GPU can stall schedule 3)\n",
+                 what, path_.c_str(), std::strerror(e));
+}
+
 void TenancyLock::lock_exclusive() {
   rw_.lock();
-  if (fd_ >= 0) {
+  if (files()) {
     std::lock_guard<std::mutex> tl(turn_mu_);
-    flock_retry(turn_, LOCK_EX);  // readers arriving from now on wait at the turnstile
-    flock_retry(fd_, LOCK_EX);    // the readers already in drain
-    flock_retry(turn_, LOCK_UN);
+    // readers arriving from now on wait at the turnstile, then the readers already in drain
+    if (int e = flock_retry(turn_, LOCK_EX)) return fail(e, "turnstile, exclusive");
+    if (int e = flock_retry(fd_, LOCK_EX)) fail(e, "lock, exclusive");
+    else fd_held_ = true;
+    if (int e = flock_retry(turn_, LOCK_UN)) fail(e, "turnstile, release");
   }
 }
 
 void TenancyLock::unlock_exclusive() {
-  if (fd_ >= 0) flock_retry(fd_, LOCK_UN);
+  if (fd_held_) {
+    fd_held_ = false;
+    if (int e = flock_retry(fd_, LOCK_UN)) fail(e, "lock, release");
+  }
   rw_.unlock();
 }
 
 void TenancyLock::lock_shared() {
   rw_.lock_shared();
-  if (fd_ >= 0) {
+  if (files()) {
     {
       std::lock_guard<std::mutex> tl(turn_mu_);
-      flock_retry(turn_, LOCK_EX);  // behind any writer waiting in another process
-      flock_retry(turn_, LOCK_UN);
+      if (int e = flock_retry(turn_, LOCK_EX)) {  // behind any writer waiting in another process
+        fail(e, "turnstile, shared");
+        return;
+      }
+      if (int e = flock_retry(turn_, LOCK_UN)) fail(e, "turnstile, release");
     }
     std::lock_guard<std::mutex> fl(fd_mu_);
-    if (readers_++ == 0) flock_retry(fd_, LOCK_SH);
+    if (readers_ == 0 && files()) {
+      if (int e = flock_retry(fd_, LOCK_SH)) {
+        fail(e, "lock, shared");
+        return;
+      }
+    }
+    ++readers_;
   }
 }
 
 void TenancyLock::unlock_shared() {
-  if (fd_ >= 0) {
+  {
     std::lock_guard<std::mutex> fl(fd_mu_);
-    if (--readers_ == 0) flock_retry(fd_, LOCK_UN);
+    if (readers_ > 0 && --readers_ == 0) {
+      if (int e = flock_retry(fd_, LOCK_UN)) fail(e, "lock, release");
+    }
   }
   rw_.unlock_shared();
 }

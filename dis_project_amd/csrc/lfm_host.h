@@ -4,6 +4,7 @@
 // (tests/native, `make -C tests/native asan`) with g++ -fsanitize=address,undefined.
 #pragma once
 
+#include <atomic>
 #include <cmath>
 #include <cstdint>
 #include <mutex>
@@ -105,9 +106,15 @@ class TenancyLock {
   void lock_shared();
   void unlock_shared();
   std::string path();
+  // 0, or the errno of the first flock failure (the lock is then in-process only)
+  int error() const { return err_.load(std::memory_order_acquire); }
   ~TenancyLock();
 
  private:
+  bool files() const;                     // the cross-process part is in use
+  void fail(int e, const char* what);     // records (and logs) the first flock failure
+  std::atomic<int> err_{0};
+  bool fd_held_ = false;  // LOCK_EX on fd_ held by this process's exclusive holder
   std::shared_mutex rw_;  // in-process readers-writer lock
   std::mutex turn_mu_;    // this process's threads at the turnstile, one at a time
   std::mutex fd_mu_;      // readers_ and the flock state of fd_

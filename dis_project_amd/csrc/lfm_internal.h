@@ -77,7 +77,10 @@ struct lfm_ctx {
                                                  // shared hold of the device's tenancy lock
   int last_sched = 0;                            // schedule the last factorisation ran (diag)
   bool s3_events = false;                        // schedule 3 ordered by events (LFM_S3_EVENTS)
-  unsigned spin_limit = 1u << 26;                // device-side wait bound (LFM_DEBUG_SPIN_LIMIT)
+  unsigned wait_ticks = 200000000u;              // device-side wait bound, 100 MHz ticks (2 s;
+                                                 // LFM_DEVICE_WAIT_MS, LFM_DEBUG_SPIN_LIMIT)
+  int64_t fallbacks = 0;                         // schedule-3 calls re-run on schedule 1 after a
+                                                 // device-side wait timed out (lfm_ctx_fallbacks)
   bool grad_direct = false;                      // gradient: per-pair path only (LFM_GRAD_DIRECT)
   bool gram_fuse = true;                         // gram in the first update (LFM_GRAM_FUSE)
   double* gtab = nullptr; size_t gtab_bytes = 0; // gradient tables (grid layout)
@@ -150,15 +153,16 @@ struct HypDev {
   double l;
 };
 
-// One problem of the fused small-N kernel (device pointers into one packed buffer).
+// One problem of the fused small-N kernel: x / y in device memory; its hyperparameters as
+// dsb = [true_d(G), true_s(G), true_b(G)] and sc = [l, obs_stddev, jitter], in device memory or
+// in pinned host memory the kernel reads directly (lfm_batch: a resident batch uploads nothing
+// per call). The kernel stages them in LDS first.
 struct SmallProb {
   const double* x;
   const double* y;
-  const double* D;
-  const double* S;
-  const double* B;
+  const double* dsb;
+  const double* sc;
   int n, G;
-  double l, jitter, noise;
 };
 constexpr int SMALL_MAX = 128;  // largest n handled by small_mll_kernel
 
@@ -212,7 +216,7 @@ int launch_grad(lfm_ctx* ctx, const HypDev& h, const double* d_x, int64_t n, con
                 int64_t lda, int64_t Mp, double obs_stddev, int negative, double* acc,
                 double* d_out, const GridLayout* lay = nullptr, const double* d_times = nullptr,
                 const int* d_bg = nullptr);
-int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn,
+int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn, int maxg,
                        int negative, double* d_out, int* d_status);
 
 // Path of the advisory lock file behind schedule 3's cross-process tenancy (lfm_api.hip;

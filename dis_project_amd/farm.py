@@ -131,41 +131,66 @@ class ResidentEvaluator:
 
 class BatchEvaluator:
     """MLL evaluations of many small problems (n <= 128 each: the C5 ablations) in one batched
-    launch per call (``lfm_mll_batch_f64``: one workgroup per problem). The datasets are
-    registered once: their x / y are held as contiguous fp64 arrays and the problem table's
-    pointers are built at construction, as ResidentEvaluator registers its one large dataset.
-    Each call reads every model's current hyperparameters (``m.hyp()``). Not PD -> NaN."""
+    launch per call, on a device-resident batch (``lfm_batch_create``: every problem's x / y in
+    HBM once). A call packs every model's current hyperparameters into one array
+    (``lfm_batch_mll_f64``'s layout: the true_d / true_s / true_b vectors of each problem, then
+    each problem's l, obs_stddev, jitter), which the kernel reads straight from pinned host
+    memory: one memcpy, one launch, one synchronise. Not PD -> NaN."""
 
     def __init__(self, ctx: _lib.Context, datasets, negative: bool = False):
         self.ctx, self.negative = ctx, bool(negative)
-        self.keep = []
-        self.probs = (_lib.LfmProblem * len(datasets))()
-        for i, d in enumerate(datasets):
+        self.datasets = list(datasets)  # held: the cache key of gpu_evaluator compares them
+        self.batch = None
+        probs = (_lib.LfmProblem * len(self.datasets))()
+        keep = []
+        for i, d in enumerate(self.datasets):
             x = np.ascontiguousarray(d.X, dtype=np.float64).reshape(-1, 3)
             y = np.ascontiguousarray(d.y, dtype=np.float64).reshape(-1)
             if y.size != x.shape[0]:
                 raise ValueError("dataset x / y lengths differ")
-            self.keep.append((x, y))
-            self.probs[i].x = x.ctypes.data
-            self.probs[i].y = y.ctypes.data
-            self.probs[i].n = x.shape[0]
-        self.status = (_lib.c_int * len(datasets))()
+            keep.append((x, y))
+            probs[i].x = x.ctypes.data
+            probs[i].y = y.ctypes.data
+            probs[i].n = x.shape[0]
+        self._probs, self._keep = probs, keep  # x / y kept: a new gene layout re-registers
+        self._genes = None
+        self.status = np.zeros(len(self.datasets), dtype=np.int32)
+
+    def _create(self, genes):
+        for i, g in enumerate(genes):
+            self._probs[i].hyp.num_genes = g
+        h = _lib.c_void_p()
+        self.ctx.check(self.ctx.lib.lfm_batch_create(self.ctx.handle, len(genes), self._probs,
+                                                     _lib.ctypes.byref(h)))
+        self.batch, self._genes = h, genes
+        nvec = 3 * sum(genes)
+        self._buf = np.empty(nvec + 3 * len(genes))
+        self._vec, self._sc = self._buf[:nvec], self._buf[nvec:]
 
     def __call__(self, models) -> np.ndarray:
         models = list(models)
-        if len(models) != len(self.keep):
+        if len(models) != len(self.datasets):
             raise ValueError("one model per registered dataset")
-        hps = [m.hyp() for m in models]  # keeps the hyperparameter buffers alive
-        for i, hp in enumerate(hps):
-            self.probs[i].hyp = hp.struct
+        genes = tuple(int(m.num_genes) for m in models)
+        if genes != self._genes:
+            if self.batch is not None:
+                self.close()
+            self._create(genes)
+        np.concatenate([a for m in models for a in (m.true_d, m.true_s, m.true_b)],
+                       out=self._vec)
+        self._sc[:] = [v for m in models for v in (m.l, m.obs_stddev, m.jitter)]
         out = np.empty(len(models))
-        rc = self.ctx.lib.lfm_mll_batch_f64(self.ctx.handle, len(models), self.probs,
-                                            int(self.negative), out.ctypes.data, self.status)
+        rc = self.ctx.lib.lfm_batch_mll_f64(self.ctx.handle, self.batch, self._buf.ctypes.data,
+                                            int(self.negative), out.ctypes.data,
+                                            self.status.ctypes.data)
         self.ctx.check(rc, allow_not_pd=True)
         return out
 
     def close(self):
-        self.keep = []
+        if self.batch is not None:
+            self.ctx.lib.lfm_batch_destroy(self.batch)
+            self.batch = None
+            self._genes = None
 
 
 def workload(kind: str, genes: int = 64, timepoints: int = 256, restarts: int = 32):
@@ -265,8 +290,9 @@ class ConcurrentEvaluator:
     streams, workspace and resident copy of x / y, each driven by its own host thread (ctypes
     releases the GIL inside the library calls), pulling the next hyperparameter set from a
     shared counter. Several evaluations in flight fill the bubbles one evaluation's chain-bound
-    tail leaves on the chip (36-37 evals/s with 3-4 workers against 34.6 for one
-    schedule-3 evaluation at a time).
+    tail leaves on the chip; since round 3's schedule-3 kernels, one schedule-3 evaluation at a
+    time is faster (36.6 evals/s against 33.8 / 35.3 / 33.7 with 2 / 3 / 4
+    schedule-1 workers), so bench.py uses this only when asked (--workers > 1).
 
     Worker 0 is the caller's context, switched to schedule 1 for the evaluator's lifetime and
     restored by ``close()`` (also when construction fails part-way): a schedule-3 context holds
@@ -355,16 +381,24 @@ def gpu_evaluator(ctx: _lib.Context, datasets, negative: bool = False, workers: 
             res = ResidentEvaluator(ctx, datasets[0], negative)
         return (lambda models, data: res(models)), res.close
     if all(d.n <= 128 for d in datasets):
-        # registered once; a round passes this rank's block of the same datasets
-        cache = {}
+        # registered once; a round passes this rank's block of the same datasets. The entry
+        # holds the datasets themselves (BatchEvaluator.datasets), so an id() can never be
+        # reused by a different dataset while its entry lives
+        cache = []
 
         def evaluate(models, data):
-            key = tuple(id(d) for d in data)
-            if key not in cache:
-                cache.clear()
-                cache[key] = BatchEvaluator(ctx, data, negative)
-            return cache[key](models)
+            ev = cache[0] if cache else None
+            if ev is None or len(ev.datasets) != len(data) or \
+                    any(a is not b for a, b in zip(ev.datasets, data)):
+                close()
+                ev = BatchEvaluator(ctx, data, negative)
+                cache.append(ev)
+            return ev(models)
 
-        return evaluate, cache.clear
+        def close():
+            while cache:
+                cache.pop().close()
+
+        return evaluate, close
     mll = CustomConjMLL(negative=negative)
     return (lambda models, data: mll.batch(models, data)), (lambda: None)

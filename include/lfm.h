@@ -21,7 +21,8 @@
  *     output is set to NaN and the failing pivot index is in lfm_last_error().
  *     LFM_E_TIMEOUT is NOT a property of the input: a bounded device-side wait of the
  *     factorisation's cross-stream hand-off ran out (e.g. a tool serialised the two
- *     streams' dispatches). The result is invalid; callers must raise, never map it to NaN.
+ *     streams' dispatches) and the in-call schedule-1 re-run (lfm_ctx_fallbacks) was
+ *     disabled or ran out too. The result is invalid; callers must raise, never map it to NaN.
  *   - Diagnostics (rate / layout probes, phase stamps) are declared in lfm_diag.h.
  */
 #ifndef LFM_H
@@ -34,7 +35,7 @@
 extern "C" {
 #endif
 
-#define LFM_ABI_VERSION 2
+#define LFM_ABI_VERSION 3
 
 enum {
   LFM_OK = 0,
@@ -117,6 +118,13 @@ int lfm_ctx_set_block(lfm_ctx* ctx, int nb);
 int lfm_ctx_set_schedule(lfm_ctx* ctx, int schedule);
 /* The schedule the next factorisation will run (1 or 3). */
 int lfm_ctx_get_schedule(const lfm_ctx* ctx, int* out);
+/* Schedule-3 calls of this context (MLL, gradient, log_prob) whose device-side waits ran past
+ * their time bound (LFM_DEVICE_WAIT_MS, default 2000: e.g. another tenant of the GPU starved
+ * the factor chain's co-resident workgroups) and that were therefore re-run on schedule 1
+ * inside the same call. Their results are valid (LFM_OK); lfm_last_error names the stall after
+ * such a call. LFM_S3_FALLBACK=0 disables the re-run (the call then returns LFM_E_TIMEOUT).
+ * Reference behaviour preserved: trainer.py:126 never fails for scheduling reasons. */
+int lfm_ctx_fallbacks(const lfm_ctx* ctx, int64_t* out);
 
 /* --------------------------------------------- ExactLFM surface (model.py) */
 /* mean_function (model.py:124-149): out[i] = (B/D)[i / (n / num_genes)] * int(x[i,2]). */
@@ -150,6 +158,23 @@ int lfm_mll_f64(lfm_ctx* ctx, const double* x, const double* y, int64_t n, const
                 int negative, double* out);
 /* nprob independent problems; out[p] per problem (NaN where not PD); status[p] optional. */
 int lfm_mll_batch_f64(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, int negative,
+                      double* out, int* status);
+
+/* A batch of small problems registered once and evaluated many times — the replicate x
+ * leave-one-gene-out ablation farm of src/notebook.py:33-75, each problem the MLL of
+ * src/objectives.py:64-78. x / y of every problem (probs[p].x, .y, .n; n <= 128, n % num_genes
+ * == 0) go to HBM here, once; of probs[p].hyp only num_genes is read (it fixes the layout of the
+ * packed hyperparameters). The caller's x / y may be freed after the call. */
+typedef struct lfm_batch lfm_batch;
+int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_batch** out);
+int lfm_batch_destroy(lfm_batch* batch);
+/* Doubles in the packed hyperparameter array: sum_p (3 G_p + 3). */
+int lfm_batch_hyp_size(const lfm_batch* batch, int64_t* out);
+/* Every problem's MLL (constant -1 if negative) in ONE launch, one workgroup per problem.
+ * hyp packed: first, for each problem in order, true_d[G_p] true_s[G_p] true_b[G_p]; then, for
+ * each problem in order, l, obs_stddev, jitter. out[p] per problem (NaN where not PD, with
+ * status[p] = LFM_E_NOT_PD; status may be NULL); returns LFM_E_NOT_PD if any problem was. */
+int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative,
                       double* out, int* status);
 
 /* Value and gradient of CustomConjMLL(negative).step — what jax.value_and_grad(loss)

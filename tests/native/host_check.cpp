@@ -2,9 +2,11 @@
 // C++ oracle (oracle/lfm_cpu.cpp) under AddressSanitizer + UBSan: built and run
 // by `make -C tests/native asan` (tests/test_host_asan.py). Exits non-zero on the first failed
 // check; the sanitizers abort on any memory / UB error.
+#include <fcntl.h>
 #include <unistd.h>
 
 #include <atomic>
+#include <cerrno>
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -310,6 +312,50 @@ static void check_tenancy() {
     CHECK(r2_at.load() >= w_at.load() + 80.0,
           "second reader overtook the waiting writer (writer %.1f, reader %.1f ms)", w_at.load(),
           r2_at.load());
+  }
+  // a flock failure (here EBADF: the lock file's descriptor swapped for an O_PATH one, which
+  // flock refuses) is recorded, not ignored: the lock turns in-process only and says so once,
+  // and the in-process part still excludes
+  {
+    const std::string p2 = std::string(dir) + "/lfm_gpu_fail.lock";
+    TenancyLock c;
+    CHECK(c.open(p2), "open p2");
+    int lock_fd = -1;
+    for (int fd = 0; fd < 1024; ++fd) {
+      char link[64], target[512];
+      std::snprintf(link, sizeof(link), "/proc/self/fd/%d", fd);
+      const ssize_t k = readlink(link, target, sizeof(target) - 1);
+      if (k <= 0) continue;
+      target[k] = 0;
+      if (p2 == target) lock_fd = fd;
+    }
+    CHECK(lock_fd >= 0, "lock file descriptor not found");
+    const int op = ::open(p2.c_str(), O_PATH | O_CLOEXEC);
+    CHECK(op >= 0 && dup2(op, lock_fd) == lock_fd, "dup2 O_PATH");
+    ::close(op);
+    CHECK(c.error() == 0, "no error before the first lock");
+    c.lock_exclusive();
+    CHECK(c.error() == EBADF, "flock failure not recorded (%d)", c.error());
+    c.unlock_exclusive();
+    int counter = 0;
+    std::vector<std::thread> ts;
+    for (int t = 0; t < 4; ++t)
+      ts.emplace_back([&] {
+        for (int i = 0; i < 500; ++i) {
+          if (i & 1) {
+            c.lock_shared();
+            c.unlock_shared();
+          }
+          c.lock_exclusive();
+          const int v = counter;
+          counter = v + 1;
+          c.unlock_exclusive();
+        }
+      });
+    for (auto& t : ts) t.join();
+    CHECK(counter == 2000, "in-process exclusion lost after the flock failure: %d", counter);
+    unlink(p2.c_str());
+    unlink((p2.substr(0, p2.size() - 5) + ".turn").c_str());
   }
   std::string turn = path.substr(0, path.size() - 5) + ".turn";
   unlink(path.c_str());

@@ -99,7 +99,7 @@ def test_rank_processes_do_not_relaunch(monkeypatch):
         bench.main(["--gpus", "2"])
 
 
-def _gather_rank(rank, world, port, fail_rank, q):
+def _gather_rank(rank, world, port, fail_rank, q, require=False):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -123,7 +123,12 @@ def _gather_rank(rank, world, port, fail_rank, q):
 
         import numpy as np
 
-        gather, kind = bench.make_gather(None, world, rank, "rccl", rccl=Stub)
+        try:
+            gather, kind = bench.make_gather(None, world, rank, "rccl", rccl=Stub,
+                                             require=require)
+        except SystemExit as e:
+            q.put((rank, "exit", Stub.closed, str(e)))
+            return
         recv = None if kind == "rccl" else gather(np.array([float(rank), float(10 + rank)]))
         q.put((rank, kind, Stub.closed, None if recv is None else recv.tolist()))
     finally:
@@ -155,3 +160,153 @@ def test_gather_falls_back_to_gloo_on_every_rank(fail_rank):
         assert kind == "gloo-fallback"
         assert recv == [0.0, 10.0, 1.0, 11.0]
         assert closed == (rank != fail_rank)
+
+
+# ------------------------------------------------- GPU count without the HIP runtime
+def _fake_kfd(root, dri, cards):
+    """A KFD topology (node 0 a CPU agent) with `cards` GPU nodes and their render nodes.
+    cards: list of (unique_id, render node present)."""
+    os.makedirs(dri, exist_ok=True)
+    n0 = os.path.join(root, "0")
+    os.makedirs(n0)
+    open(os.path.join(n0, "gpu_id"), "w").write("0\n")
+    open(os.path.join(n0, "properties"), "w").write("cpu_cores_count 16\nsimd_count 0\n")
+    for i, (uid, ok) in enumerate(cards, start=1):
+        d = os.path.join(root, str(i))
+        os.makedirs(d)
+        open(os.path.join(d, "gpu_id"), "w").write(f"{1000 + i}\n")
+        minor = 127 + i
+        open(os.path.join(d, "properties"), "w").write(
+            f"cpu_cores_count 0\nsimd_count 1024\ndrm_render_minor {minor}\nunique_id {uid}\n")
+        if ok:  # a container sees only its own cards' render nodes
+            open(os.path.join(dri, f"renderD{minor}"), "w").close()
+
+
+def _clear_visible(monkeypatch):
+    for v in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(v, raising=False)
+
+
+def test_visible_gpus_reads_the_kfd_topology(tmp_path, monkeypatch):
+    root, dri = str(tmp_path / "nodes"), str(tmp_path / "dri")
+    _fake_kfd(root, dri, [(0x11, True), (0x22, True), (0x33, False), (0x44, True)])
+    monkeypatch.setenv("LFM_KFD_TOPOLOGY", root)
+    monkeypatch.setenv("LFM_DRI_DIR", dri)
+    _clear_visible(monkeypatch)
+    assert bench.visible_gpus() == 3  # the CPU node and the inaccessible card are not counted
+
+
+def test_visible_gpus_applies_the_visibility_variables(tmp_path, monkeypatch):
+    root, dri = str(tmp_path / "nodes"), str(tmp_path / "dri")
+    _fake_kfd(root, dri, [(0xA0 + i, True) for i in range(8)])
+    monkeypatch.setenv("LFM_KFD_TOPOLOGY", root)
+    monkeypatch.setenv("LFM_DRI_DIR", dri)
+    _clear_visible(monkeypatch)
+    assert bench.visible_gpus() == 8
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "1,3,5,GPU-a7")
+    assert bench.visible_gpus() == 4
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,2")    # indices into ROCr's list
+    assert bench.visible_gpus() == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,9,1")  # parsing stops at the invalid index
+    assert bench.visible_gpus() == 1
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "")      # empty hides every device
+    assert bench.visible_gpus() == 0
+
+
+def test_launcher_refuses_without_a_topology(tmp_path, rank_script, monkeypatch):
+    """No KFD topology: exit 3 with the cause, no rank started — never a HIP-initialising
+    fallback count."""
+    monkeypatch.setenv("LFM_KFD_TOPOLOGY", str(tmp_path / "absent"))
+    a = bench.parse(["--gpus", "2"])
+    assert bench.self_launch(a, [str(tmp_path), "ok"], script=rank_script) == 3
+    assert not list(tmp_path.glob("rank*.json"))
+
+
+PROBE = textwrap.dedent("""
+    import json, os, subprocess, sys
+    sys.path.insert(0, sys.argv[1])
+    out, rank_script = sys.argv[2], sys.argv[3]
+    real_popen = subprocess.Popen
+    state = {}
+
+    def probe(args, **kw):
+        # the launcher's state at the moment it starts a rank process
+        if not state:
+            maps = open("/proc/self/maps").read()
+            fds = []
+            for fd in os.listdir("/proc/self/fd"):
+                try:
+                    fds.append(os.readlink(f"/proc/self/fd/{fd}"))
+                except OSError:
+                    pass
+            state.update(hip=[l.split()[-1] for l in maps.splitlines() if "amdhip" in l],
+                         torch="torch" in sys.modules,
+                         kfd=[f for f in fds if f.startswith("/dev/kfd") or "/dev/dri" in f])
+            json.dump(state, open(os.path.join(out, "launcher.json"), "w"))
+        return real_popen([sys.executable, rank_script, out, "ok"], **{k: v for k, v in kw.items()
+                                                                       if k == "env"})
+
+    subprocess.Popen = probe
+    import bench
+    sys.exit(bench.main(["--gpus", "2", "--workload", "c5"]))
+""")
+
+
+def test_launcher_process_stays_free_of_hip(tmp_path, rank_script):
+    """`python bench.py --gpus 2` in a fresh interpreter, up to the moment it starts its first
+    rank process: libamdhip64 is not mapped, torch is not imported and no /dev/kfd or render
+    node is open (a parent that initialised HIP must not start GPU processes)."""
+    import subprocess
+
+    root, dri = str(tmp_path / "nodes"), str(tmp_path / "dri")
+    _fake_kfd(root, dri, [(1, True), (2, True)])
+    out = tmp_path / "out"
+    out.mkdir()
+    probe = tmp_path / "probe.py"
+    probe.write_text(PROBE)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "ROCR_VISIBLE_DEVICES",
+                        "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")}
+    env.update(LFM_KFD_TOPOLOGY=root, LFM_DRI_DIR=dri)
+    r = subprocess.run([sys.executable, str(probe), ROOT, str(out), rank_script], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    st = json.load(open(out / "launcher.json"))
+    assert st == {"hip": [], "torch": False, "kfd": []}, st
+    assert sorted(p.name for p in out.glob("rank*.json")) == ["rank0.json", "rank1.json"]
+
+
+def test_require_rccl_defaults(monkeypatch):
+    assert bench.parse(["--gpus", "8"]).require_rccl is True
+    assert bench.parse(["--gpus", "2", "--share-gpus"]).require_rccl is False
+    assert bench.parse(["--gpus", "2", "--gather", "gloo"]).require_rccl is False
+    assert bench.parse(["--gpus", "2", "--share-gpus", "--require-rccl"]).require_rccl is True
+    assert bench.parse(["--gpus", "8", "--no-require-rccl"]).require_rccl is False
+
+
+@pytest.mark.parametrize("fail_rank", [0, 1])
+def test_require_rccl_ends_the_run_on_every_rank(fail_rank):
+    """--require-rccl (the default outside rehearsals): one rank's communicator failure makes
+    EVERY rank exit (SystemExit naming the cause) instead of printing a gloo-fallback line; a
+    rank whose own communicator came up closes it first."""
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = bench._free_port()
+    ps = [ctx.Process(target=_gather_rank, args=(r, 2, port, fail_rank, q, True))
+          for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    for rank, kind, closed, msg in res:
+        assert kind == "exit", (rank, kind)
+        assert "RCCL communicator unavailable" in msg and "--require-rccl" in msg
+        if rank == fail_rank:
+            assert "stand-in failure" in msg
+        else:
+            assert "failed on another rank" in msg and closed

@@ -180,3 +180,106 @@ def test_concurrent_evaluator_c3_full_size():
     v, _ = lfm_cpu.mll(d.X, d.y, m.true_d, m.true_s, m.true_b, m.l, m.obs_stddev, m.jitter,
                        negative=False, threads=16)
     assert abs(a[0] - v) <= 1e-9 * abs(v)
+
+
+@pytest.mark.gpu
+def test_allgather_wait_is_bounded_and_drops_the_communicator(monkeypatch):
+    """A collective whose peers never arrive (stood in for by LFM_DEBUG_FARM_STALL_MS: a kernel
+    holding the stream for 6 s ahead of the all-gather; the one-GPU box cannot host a second
+    rank) ends the wait with LFM_E_RCCL after LFM_RCCL_TIMEOUT_S, not when the stream drains;
+    the communicator is aborted (the next call: LFM_E_STATE) and the caller's receive buffer is
+    never written. A 1-rank all-gather before it returns the sent slots."""
+    import re
+    import time
+
+    from dis_project_amd import _lib
+
+    monkeypatch.setenv("LFM_RCCL_TIMEOUT_S", "1")
+    ctx = _lib.Context(0)
+    try:
+        g = farm.RcclGather(ctx, 1, 0, farm.RcclGather.unique_id(ctx))
+        np.testing.assert_array_equal(g(np.array([1.0, 2.0])), [1.0, 2.0])
+        monkeypatch.setenv("LFM_DEBUG_FARM_STALL_MS", "6000")
+        send = np.array([3.0, 4.0])
+        recv = np.full(2, -7.0)
+        t0 = time.monotonic()
+        rc = ctx.lib.lfm_farm_allgather_f64(ctx.handle, _lib.dptr(send), 2, _lib.dptr(recv))
+        dt = time.monotonic() - t0
+        assert rc == _lib.LFM_E_RCCL, rc
+        msg = ctx.lib.lfm_last_error(ctx.handle).decode()
+        assert "did not arrive" in msg, msg
+        # the wait gave up at the bound; ncclCommAbort then returns once the device work queued
+        # before the collective has drained (a real RCCL kernel observes the abort flag; the
+        # stand-in stall kernel does not, so the call itself lasts about the stall's 6 s)
+        waited = float(re.search(r"timed out after ([0-9.]+) s", msg).group(1))
+        assert 0.99 <= waited < 1.5, msg
+        assert dt < 9.0, dt
+        monkeypatch.delenv("LFM_DEBUG_FARM_STALL_MS")
+        assert ctx.lib.lfm_farm_allgather_f64(ctx.handle, _lib.dptr(send), 2,
+                                              _lib.dptr(recv)) == _lib.LFM_E_STATE
+        ctx.check(ctx.lib.lfm_ctx_synchronize(ctx.handle))  # the stall drains; nothing else
+        np.testing.assert_array_equal(recv, [-7.0, -7.0])   # was queued into recv
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_resident_batch_matches_the_oracle_and_the_per_call_batch():
+    """lfm_batch (x / y registered in HBM once, hyperparameters packed per call and read by the
+    kernel from pinned host memory) on the C5 workload: every value within 1e-9 of the oracle
+    and bit-identical to lfm_mll_batch_f64 (same kernel, hyperparameters staged the same way);
+    repeated calls with changed hyperparameters follow them; a non-PD problem is NaN with its
+    status, the others unaffected; a changed gene layout re-registers the batch."""
+    from dis_project_amd import _lib
+    from dis_project_amd.objectives import CustomConjMLL
+
+    ctx = _lib.get_context()
+    models, datasets = farm.workload("c5")
+    ev = farm.BatchEvaluator(ctx, datasets)
+    try:
+        a = ev(models)
+        np.testing.assert_allclose(a, _oracle_eval(models, datasets), rtol=1e-9)
+        per_call = CustomConjMLL().batch(models, datasets)
+        np.testing.assert_array_equal(a, per_call)
+        np.testing.assert_array_equal(ev(models), a)  # deterministic
+        moved = [m.replace(l=m.l * 1.1, true_s=m.true_s * 0.9) for m in models]
+        b = ev(moved)
+        np.testing.assert_allclose(b, _oracle_eval(moved, datasets), rtol=1e-9)
+        assert not np.any(a == b)
+        bad = list(models)
+        bad[4] = models[4].replace(jitter=-50.0, obs_stddev=0.0)
+        c = ev(bad)
+        assert np.isnan(c[4]) and ev.status[4] != 0
+        mask = np.arange(len(models)) != 4
+        np.testing.assert_array_equal(c[mask], a[mask])
+        assert not np.any(ev.status[mask])
+    finally:
+        ev.close()
+    # the same problems under another gene count (a new hyperparameter layout: re-registered)
+    assert datasets[0].n % 2 == 0
+    g2 = [m.replace(num_genes=2, true_d=m.true_d[:2], true_s=m.true_s[:2], true_b=m.true_b[:2])
+          for m in models[:3]]
+    ev = farm.BatchEvaluator(ctx, datasets[:3])
+    try:
+        ev(models[:3])
+        out = ev(g2)
+        np.testing.assert_allclose(out, _oracle_eval(g2, datasets[:3]), rtol=1e-9)
+    finally:
+        ev.close()
+
+
+@pytest.mark.gpu
+def test_resident_batch_rejects_bad_problems():
+    from dis_project_amd import _lib
+
+    ctx = _lib.get_context()
+    probs = (_lib.LfmProblem * 1)()
+    x = np.zeros((200, 3))
+    y = np.zeros(200)
+    probs[0].x, probs[0].y, probs[0].n = x.ctypes.data, y.ctypes.data, 200
+    probs[0].hyp.num_genes = 4
+    h = _lib.c_void_p()
+    assert ctx.lib.lfm_batch_create(ctx.handle, 1, probs, _lib.ctypes.byref(h)) == _lib.LFM_E_ARG
+    probs[0].n = 30  # 30 % 4 != 0: the mean_function broadcast (model.py:145-149)
+    assert ctx.lib.lfm_batch_create(ctx.handle, 1, probs, _lib.ctypes.byref(h)) == _lib.LFM_E_ARG
+    assert ctx.lib.lfm_batch_create(ctx.handle, 0, probs, _lib.ctypes.byref(h)) == _lib.LFM_E_ARG
