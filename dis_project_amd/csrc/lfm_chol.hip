@@ -983,6 +983,18 @@ struct Panel {
 #ifndef LFM_TALL_RR
 #define LFM_TALL_RR 1
 #endif
+// round-robin deal in groups of the LFM_TALL_SPLIT pieces of one row block (1): the pieces that
+// read the same A21 rows go to the same XCD back to back, so the second reads them from that
+// XCD's L2; else (0) piece by piece, consecutive pieces on different XCDs (round 3)
+#ifndef LFM_TALL_GROUP
+#define LFM_TALL_GROUP 1
+#endif
+// workgroups of the tall segment: a multiple of 8 (XCDs), of 8 LFM_TALL_SPLIT when grouped
+__host__ __device__ constexpr int64_t tall_grid(int64_t nt) {
+  return (LFM_TALL_RR && LFM_TALL_GROUP) ? (nt + 8 * LFM_TALL_SPLIT - 1) / (8 * LFM_TALL_SPLIT) *
+                                               (8 * LFM_TALL_SPLIT)
+                                         : (nt + 7) / 8 * 8;
+}
 // C tile loads of the trailing update: device-coherent, or plain / nontemporal (LFM_C_NT bit 0;
 // bit 1: nontemporal C stores)
 #ifndef LFM_C_NT
@@ -1338,7 +1350,15 @@ __device__ __forceinline__ void stamp_max(unsigned long long* p, bool negate = f
 __device__ __forceinline__ void tall_or_xcd_range(int seg, int64_t cnt, int64_t b, int64_t* u,
                                                   int64_t* end) {
   if (seg == 2 && LFM_TALL_RR) {
-    *u = b;
+    if (LFM_TALL_GROUP) {
+      // workgroup b runs on XCD x = b % 8 at position p = b / 8 of its queue: group j = (p / S)
+      // 8 + x, piece p % S (the segment is padded to 8 S workgroups: tall_grid)
+      constexpr int S = LFM_TALL_SPLIT;
+      const int64_t p = b / 8;
+      *u = S * ((p / S) * 8 + b % 8) + p % S;
+    } else {
+      *u = b;
+    }
     *end = cnt;
     return;
   }
@@ -2242,7 +2262,7 @@ int probe_update_launch(lfm_ctx* ctx, hipStream_t st, int T, int kd, int cio, in
       g.X = xs + xb / 8;
       g.zvec = xs;
       g.a_done = nullptr;
-      grid = (g.na + 7) / 8 * 8 + (g.nr + 7) / 8 * 8 + (g.nt + 7) / 8 * 8;
+      grid = (g.na + 7) / 8 * 8 + (g.nr + 7) / 8 * 8 + tall_grid(g.nt);
     }
     // unit-duration stamps in step slot 0 while lfm_debug_stamps is on (scripts/unit_time.py)
     g.stamps = ctx->dbg_stamps ? ctx->dbg_stamps + 256 * 16 : nullptr;
@@ -2460,7 +2480,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       if (!g.copy_from) g.copy_from = INT64_MAX;
       g.spin = ctx->wait_ticks;
       const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 + (int64_t)(g.nr + 7) / 8 * 8 +
-                           (int64_t)(g.nt + 7) / 8 * 8;
+                           tall_grid(g.nt);
       if (grid == 0) return;
       // issued: every 64 x 128 unit in full (padding rows included), tall units as GEMMs with
       // the triangular inverse; algorithmic: the update of the unpadded augmented trailing

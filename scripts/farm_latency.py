@@ -12,30 +12,42 @@ import os
 import subprocess
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CHILD = r"""
-import json, os, sys, time
-sys.path.insert(0, sys.argv[1])
+# raw ctypes on the five entry points used (older builds lack later ABI additions)
+import ctypes, json, sys, time
 import numpy as np
-from dis_project_amd import _lib, farm
-ctx = _lib.Context(0)
-g = farm.RcclGather(ctx, 1, 0, farm.RcclGather.unique_id(ctx))
+lib = ctypes.CDLL(sys.argv[1])
+vp = ctypes.c_void_p
+lib.lfm_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+lib.lfm_farm_unique_id.argtypes = [vp, ctypes.POINTER(ctypes.c_ubyte)]
+lib.lfm_farm_init.argtypes = [vp, ctypes.POINTER(ctypes.c_ubyte), ctypes.c_int, ctypes.c_int]
+lib.lfm_farm_allgather_f64.argtypes = [vp, vp, ctypes.c_int64, vp]
+lib.lfm_farm_destroy.argtypes = [vp]
+lib.lfm_ctx_destroy.argtypes = [vp]
+h = vp()
+assert lib.lfm_ctx_create(0, ctypes.byref(h)) == 0
+uid = (ctypes.c_ubyte * 128)()
+assert lib.lfm_farm_unique_id(h, uid) == 0
+assert lib.lfm_farm_init(h, uid, 1, 0) == 0
 out = {}
 for slots in (2, 4, 32):
     send = np.arange(slots, dtype=np.float64)
+    recv = np.empty(slots)
+    def g():
+        assert lib.lfm_farm_allgather_f64(h, send.ctypes.data, slots, recv.ctypes.data) == 0
     for _ in range(20):
-        g(send)
+        g()
     lat = []
     for _ in range(int(sys.argv[2])):
         t0 = time.perf_counter()
-        r = g(send)
+        g()
         lat.append((time.perf_counter() - t0) * 1e6)
-    assert np.array_equal(r, send)
+    assert np.array_equal(recv, send)
     out[str(8 * slots)] = {"median_us": float(np.median(lat)), "p10_us": float(np.percentile(lat, 10)),
                            "p90_us": float(np.percentile(lat, 90))}
-g.close()
-ctx.close()
+lib.lfm_farm_destroy(h)
+lib.lfm_ctx_destroy(h)
 print(json.dumps(out))
 """
 
@@ -50,8 +62,7 @@ def main():
     res = {lib: [] for lib in a.libs}
     for rnd in range(a.rounds):
         for lib in a.libs:
-            env = dict(os.environ, LFM_LIBRARY=os.path.abspath(lib))
-            r = subprocess.run([sys.executable, "-c", CHILD, ROOT, str(a.iters)], env=env,
+            r = subprocess.run([sys.executable, "-c", CHILD, os.path.abspath(lib), str(a.iters)],
                                capture_output=True, text=True, timeout=300)
             if r.returncode:
                 print(r.stderr, file=sys.stderr)

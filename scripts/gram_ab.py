@@ -1,6 +1,8 @@
 """Gram fill variants (env read per call), interleaved: kernel time from the library's event
 profile, fp64 at N = 16384 (C2) and fp32 at N = 65536 (C4), lower triangle, device output.
-    python scripts/gram_ab.py "LFM_GRAM_R=64" "LFM_GRAM_R=128" """
+    python scripts/gram_ab.py ["K=V ..." ...]   (no argument: the library as built)
+Round 3 A/B-ed its rows-per-tile / nontemporal / 16-B store variants this way (profiles/
+r03_ab_gram_*); those knobs were removed with the variants, so the gram has no per-call knob now."""
 import os
 import sys
 
