@@ -157,6 +157,7 @@ DIAG_SIGNATURES = [
                                 ctypes.c_int64, POINTER(ctypes.c_int64)]),
     ("lfm_debug_lock_path", c_int, [_c_ctx, ctypes.c_char_p, c_int]),
     ("lfm_probe_rsq", c_int, [_c_ctx, c_void_p, c_int64, c_void_p]),
+    ("lfm_probe_kxx_tab", c_int, [_c_ctx, _dptr, c_int64, POINTER(LfmHyp), _dptr]),
     ("lfm_probe_mfma_f64_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr]),
     ("lfm_probe_mfma4_layout", c_int, [_c_ctx, _dptr, _dptr, _dptr, _dptr]),
     ("lfm_probe_mfma_f64", c_int, [_c_ctx, c_int, c_int, _dptr, _dptr]),

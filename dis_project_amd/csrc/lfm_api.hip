@@ -710,6 +710,7 @@ void lfm_ctx_destroy(lfm_ctx* ctx) {
                   (void*)ctx->gtab})
     if (p) hipFree(p);
   if (ctx->hpin) hipHostFree(ctx->hpin);
+  if (ctx->farm_h) hipHostFree(ctx->farm_h);
   for (auto& p : ctx->pending) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);
@@ -1569,12 +1570,22 @@ int lfm_farm_allgather_f64(lfm_ctx* ctx, const double* send, int64_t count, doub
   const size_t in = (size_t)count * 8, out = in * ctx->nranks;
   int r = ensure(ctx, (void**)&ctx->farm_buf, &ctx->farm_bytes, in + out);
   if (r) return r;
-  // host side through the pinned staging buffer: a copy out of device memory into pageable
-  // memory would run synchronously and so defeat the bounded wait below
-  r = ensure_pinned(ctx, std::max<size_t>(in + out, 1 << 16));
-  if (r) return r;
-  double* hsend = ctx->hpin;
-  double* hrecv = ctx->hpin + count;
+  // host side through a pinned buffer of the farm's own: every copy is truly asynchronous (a
+  // copy into pageable memory would block past the deadline below), and a copy a timed-out call
+  // leaves queued can only ever write into this buffer — never the caller's, never the staging
+  // other calls use
+  if (!ctx->farm_h || ctx->farm_h_bytes < in + out) {
+    if (ctx->farm_h) {
+      hipStreamSynchronize(ctx->stream);
+      hipHostFree(ctx->farm_h);
+      ctx->farm_h = nullptr;
+    }
+    hipError_t e = hipHostMalloc((void**)&ctx->farm_h, in + out, hipHostMallocDefault);
+    if (e != hipSuccess) return hip_fail(ctx, e, "farm staging buffer");
+    ctx->farm_h_bytes = in + out;
+  }
+  double* hsend = ctx->farm_h;
+  double* hrecv = ctx->farm_h + count;
   double* dsend = ctx->farm_buf;
   double* drecv = ctx->farm_buf + count;
   std::memcpy(hsend, send, in);
@@ -1590,17 +1601,17 @@ int lfm_farm_allgather_f64(lfm_ctx* ctx, const double* send, int64_t count, doub
                                          (ncclComm_t)ctx->comm, ctx->stream);
   if (ctx->comm_nb && q == ncclInProgress) r = rccl_poll(ctx, (ncclComm_t)ctx->comm, "ncclAllGather");
   else r = rccl_fail(ctx, q, "ncclAllGather");
-  // the collective must have completed before its result is copied out: on a timeout nothing
-  // is left queued that could still write into the caller's buffer
-  if (!r && ctx->comm_nb) r = rccl_stream_wait(ctx, "ncclAllGather");
+  if (!r) {
+    e = hipMemcpyAsync(hrecv, drecv, out, hipMemcpyDeviceToHost, ctx->stream);
+    if (e != hipSuccess) r = hip_fail(ctx, e, "farm download");
+  }
+  // one bounded wait for the collective and the copy behind it (the latency-bound exchange has
+  // a single synchronisation point); a blocking communicator waits unbounded, as RCCL would
+  if (!r) r = ctx->comm_nb ? rccl_stream_wait(ctx, "ncclAllGather") : finish(ctx);
   if (r) {
     rccl_drop(ctx);
     return r;
   }
-  e = hipMemcpyAsync(hrecv, drecv, out, hipMemcpyDeviceToHost, ctx->stream);
-  if (e != hipSuccess) return hip_fail(ctx, e, "farm download");
-  r = finish(ctx);
-  if (r) return r;
   std::memcpy(recv, hrecv, out);
   return LFM_OK;
 }

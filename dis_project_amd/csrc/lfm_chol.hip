@@ -2725,7 +2725,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
 
 __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restrict__ probs,
                                                         int negative, double* __restrict__ out,
-                                                        int* __restrict__ status) {
+                                                        int* __restrict__ status, int tabs) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const SmallProb P = probs[blockIdx.x];
   const int n = P.n, M = n + 1, ld = n + 2, G = P.G;
@@ -2739,20 +2739,95 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
   const HypDev h{hyp, hyp + G, hyp + 2 * G, G, hyp[3 * G]};
   const double jitter = hyp[3 * G + 2], sd = hyp[3 * G + 1];
   const double noise = sd * sd;  // objectives.py:66
-  for (int idx = tid; idx < n * n; idx += 256) {
-    const int i = idx / n, c = idx - i * n;
-    if (c <= i) {
+  if (tabs) {
+    // n <= 63 (the launch's LDS holds the tables): gene-gene pairs from KxxTab, the same bits
+    // as kernel_ref with a third of its transcendentals; pairs with a latent row direct
+    double* gam = hyp + 3 * G + 3;
+    double* egg = gam + G;
+    double* erg = egg + G;
+    double* e2 = erg + G;
+    double* e1 = e2 + n;
+    const KxxTab t{gam, egg, erg, e1, e2, G};
+    small_tables(h, P.x, n, t, gam, egg, erg, e1, e2);
+    const int np = n * (n + 1) / 2;  // the lower triangle, row by row
+    for (int q = tid; q < np; q += 256) {
+      int i = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
+      while (i * (i + 1) / 2 > q) --i;
+      while ((i + 1) * (i + 2) / 2 <= q) ++i;
+      const int c = q - i * (i + 1) / 2;
       const double* xa = P.x + 3 * i;
       const double* xb = P.x + 3 * c;
-      double v = kernel_ref(h, xa[0], xa[1], xa[2], xb[0], xb[1], xb[2]);
+      double v;
+      if (flag_int(xa[2]) == 1 && flag_int(xb[2]) == 1)
+        v = kxx_tab(h, t, xa[0], gene_index(xa[1], G), i, xb[0], gene_index(xb[1], G), c);
+      else
+        v = kernel_ref(h, xa[0], xa[1], xa[2], xb[0], xb[1], xb[2]);
       if (i == c) v = (v + jitter) + noise;
       sm[i * ld + c] = v;
+    }
+  } else {
+    for (int idx = tid; idx < n * n; idx += 256) {
+      const int i = idx / n, c = idx - i * n;
+      if (c <= i) {
+        const double* xa = P.x + 3 * i;
+        const double* xb = P.x + 3 * c;
+        double v = kernel_ref(h, xa[0], xa[1], xa[2], xb[0], xb[1], xb[2]);
+        if (i == c) v = (v + jitter) + noise;
+        sm[i * ld + c] = v;
+      }
     }
   }
   const int64_t bs = n / G;
   for (int c = tid; c < n; c += 256) sm[n * ld + c] = P.y[c] - mean_at(h, P.x, c, bs);
   if (tid == 0) red[8] = 0.0;
   __syncthreads();
+  if (M <= 64) {
+    // One wave factors the augmented (n + 1)-row matrix, lane = row, left-looking: column c's
+    // entries are s_r = A[r][c] - sum_{k<c} L[r][k] L[c][k] (the terms in the same order as
+    // the right-looking sweep below, k = 0, 1, ...), the pivot is lane c's s, read by every
+    // lane. No workgroup barrier: the wave's LDS operations complete in order. 256-thread
+    // barriers were ~60 % of the kernel at n = 28 (two per column).
+    if (tid >= 64) return;
+    const int r = tid;
+    const bool act = r < M;
+    int bad = 0;
+    for (int c = 0; c < n; ++c) {
+      double s = 0.0;
+      if (act && r >= c) {
+        s = sm[r * ld + c];
+        const double* Lr = sm + r * ld;
+        const double* Lc = sm + c * ld;
+#pragma unroll 4
+        for (int k = 0; k < c; ++k) s -= Lr[k] * Lc[k];
+      }
+      const double d = rdl(s, c);
+      const double piv = sqrt(d);
+      const double inv = 1.0 / piv;
+      if (!(d > 0.0) && bad == 0) bad = c + 1;
+      if (act && r > c) sm[r * ld + c] = s * inv;
+      if (r == c) sm[c * ld + c] = piv;
+      wave_lds_fence();
+    }
+    double ldp = 0.0, qp = 0.0;
+    if (r < n) {
+      ldp = log(sm[r * ld + r]);
+      const double z = sm[n * ld + r];
+      qp = z * z;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      ldp += __shfl_xor(ldp, o);
+      qp += __shfl_xor(qp, o);
+    }
+    if (r == 0) {
+      const double two_pi = 6.283185307179586476925;
+      double mll = -0.5 * ((double)n * log(two_pi) + 2.0 * ldp + qp);
+      mll *= negative ? -1.0 : 1.0;
+      if (bad) mll = __builtin_nan("");
+      out[blockIdx.x] = mll;
+      if (status) status[blockIdx.x] = bad;
+    }
+    return;
+  }
   for (int c = 0; c < n; ++c) {
     const double d = sm[c * ld + c];
     const double piv = sqrt(d);
@@ -2803,7 +2878,11 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
 
 int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn, int maxg,
                        int negative, double* d_out, int* d_status) {
-  const size_t lds = ((size_t)(maxn + 1) * (maxn + 2) + 16 + 3 * (size_t)maxg + 3) * sizeof(double);
+  // tables (KxxTab) when every problem has n + 1 <= 64 rows: 3 G + n + n G doubles
+  const int tabs = maxn + 1 <= 64;
+  const size_t tab = tabs ? 3 * (size_t)maxg + maxn + (size_t)maxn * maxg : 0;
+  const size_t lds =
+      ((size_t)(maxn + 1) * (maxn + 2) + 16 + 3 * (size_t)maxg + 3 + tab) * sizeof(double);
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&small_mll_kernel),
@@ -2813,7 +2892,7 @@ int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int ma
   hipEvent_t ev;
   prof_begin(ctx, K_SMALL, &ev, ctx->stream);
   hipLaunchKernelGGL(small_mll_kernel, dim3(nprob), dim3(256), lds, ctx->stream,
-                     d_probs, negative, d_out, d_status);
+                     d_probs, negative, d_out, d_status, tabs);
   prof_end(ctx, K_SMALL, ev, 0, 0, ctx->stream);
   return hip_fail(ctx, hipGetLastError(), "small_mll_kernel");
 }

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "lfm_math.h"
 
@@ -261,6 +262,54 @@ int probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y) {
   return hip_fail(ctx, e, "probe rsq");
 }
 
+// kernel_ref and KxxTab's kxx_tab (small_mll_kernel's gene-gene pairs) on every pair of x, one
+// workgroup: out[0, n^2) from kernel_ref, out[n^2, 2 n^2) from the tables (pairs with a latent
+// row: kernel_ref in both halves, as the kernel does). The tables' claim is bit-identity.
+__global__ void kxx_tab_probe_kernel(const double* __restrict__ x, int n, const double* hyp, int G,
+                                     double* __restrict__ out) {
+  extern __shared__ double tb[];
+  double* gam = tb;
+  double* egg = gam + G;
+  double* erg = egg + G;
+  double* e2 = erg + G;
+  double* e1 = e2 + n;
+  const HypDev h{hyp, hyp + G, hyp + 2 * G, G, hyp[3 * G]};
+  const KxxTab t{gam, egg, erg, e1, e2, G};
+  small_tables(h, x, n, t, gam, egg, erg, e1, e2);
+  for (int q = threadIdx.x; q < n * n; q += 256) {
+    const int i = q / n, c = q - i * n;
+    const double* xa = x + 3 * i;
+    const double* xb = x + 3 * c;
+    out[q] = kernel_ref(h, xa[0], xa[1], xa[2], xb[0], xb[1], xb[2]);
+    out[n * n + q] = flag_int(xa[2]) == 1 && flag_int(xb[2]) == 1
+                         ? kxx_tab(h, t, xa[0], gene_index(xa[1], G), i, xb[0],
+                                   gene_index(xb[1], G), c)
+                         : kernel_ref(h, xa[0], xa[1], xa[2], xb[0], xb[1], xb[2]);
+  }
+}
+
+int probe_kxx_tab(lfm_ctx* ctx, const double* x, int64_t n, const lfm_hyp* hyp, double* out) {
+  const int G = (int)hyp->num_genes;
+  const size_t nh = 3 * (size_t)G + 1, nx = 3 * (size_t)n, no = 2 * (size_t)n * n;
+  double* d = nullptr;
+  hipError_t e = hipMalloc((void**)&d, (nh + nx + no) * sizeof(double));
+  if (e != hipSuccess) return hip_fail(ctx, e, "probe kxx tab");
+  std::vector<double> hh(nh);
+  std::memcpy(hh.data(), hyp->true_d, G * 8);
+  std::memcpy(hh.data() + G, hyp->true_s, G * 8);
+  std::memcpy(hh.data() + 2 * G, hyp->true_b, G * 8);
+  hh[3 * G] = hyp->l;
+  hipMemcpyAsync(d, hh.data(), nh * 8, hipMemcpyHostToDevice, ctx->stream);
+  hipMemcpyAsync(d + nh, x, nx * 8, hipMemcpyHostToDevice, ctx->stream);
+  const size_t lds = (3 * (size_t)G + n + (size_t)n * G) * sizeof(double);
+  hipLaunchKernelGGL(kxx_tab_probe_kernel, dim3(1), dim3(256), lds, ctx->stream, d + nh, (int)n,
+                     d, G, d + nh + nx);
+  hipMemcpyAsync(out, d + nh + nx, no * 8, hipMemcpyDeviceToHost, ctx->stream);
+  e = hipStreamSynchronize(ctx->stream);
+  hipFree(d);
+  return hip_fail(ctx, e, "probe kxx tab");
+}
+
 // Pseudo-random doubles in [-1/32, 1/32) (probe data: MFMA power, hence clocks, depends on it).
 __global__ void fill_hash_kernel(double* a, int64_t cnt) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < cnt; i += (int64_t)gridDim.x * 256) {
@@ -329,6 +378,13 @@ int lfm_probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y) {
   if (!ctx || !x || !y || n < 1) return LFM_E_ARG;
   DeviceGuard g(ctx->device);
   return probe_rsq(ctx, x, n, y);
+}
+
+int lfm_probe_kxx_tab(lfm_ctx* ctx, const double* x, int64_t n, const lfm_hyp* hyp, double* out) {
+  if (!ctx || !x || !hyp || !out || n < 1 || n > 63 || hyp->num_genes < 1 || hyp->num_genes > 63)
+    return LFM_E_ARG;
+  DeviceGuard g(ctx->device);
+  return probe_kxx_tab(ctx, x, n, hyp, out);
 }
 
 // enable = 1 turns on s_memrealtime (100 MHz) stamps of the schedule-3 chain kernel's phases

@@ -108,6 +108,9 @@ struct lfm_ctx {
   bool comm_nb = false;  // communicator created non-blocking (calls polled, bounded)
   int nranks = 0, rank = -1;
   double* farm_buf = nullptr; size_t farm_bytes = 0;
+  double* farm_h = nullptr; size_t farm_h_bytes = 0;  // pinned host staging of the all-gather
+                                                      // (its own: a copy left queued by a timed-
+                                                      // out call can only ever write here)
 };
 
 // ---------------------------------------------------------------- helpers

@@ -75,6 +75,64 @@ __device__ __forceinline__ double kernel_ref(const HypDev& p, double ta, double 
   return v;
 }
 
+// kernel_xx from per-problem tables (small_mll_kernel): the same operations on the same
+// operands as kxx_ref / h_ref, so the same bits, with every factor that depends on one row or
+// one gene only evaluated once per row / gene instead of once per pair:
+//   gam[g] = D_g l / 2, egg[g] = exp(gam^2), erg[g] = erf(gam)            (per gene)
+//   e2[i] = erf(t_i / l - gam[g_i]), e1[i G + g] = erf(t_i / l + gam[g])    (per row)
+// and exp(-(D_k t2 + D_j t1)), which both h terms of a pair share (the sum is the same two
+// products in the other order, and IEEE addition commutes). Left per pair: one erf and one exp
+// per h, the shared exp and the two divisions. a, b: row indices; j = g_a, k = g_b.
+struct KxxTab {
+  const double* gam;
+  const double* egg;
+  const double* erg;
+  const double* e1;
+  const double* e2;
+  int G;
+};
+__device__ __forceinline__ double h_tab(const HypDev& p, const KxxTab& t, int j, int k,
+                                        double t1, double t2, int r1, int r2, double se) {
+  #pragma clang fp contract(off)
+  const double l = p.l;
+  const double tdist = t2 - t1;
+  const double multiplier = t.egg[k] / (p.D[j] + p.D[k]);
+  const double first_multiplier = exp(-p.D[k] * tdist);
+  const double first_erf = erf((tdist / l) - t.gam[k]) + t.e1[r1 * t.G + k];
+  const double second_erf = t.e2[r2] + t.erg[k];
+  return multiplier * (first_multiplier * first_erf - se * second_erf);
+}
+__device__ __forceinline__ double kxx_tab(const HypDev& p, const KxxTab& t, double ta, int j,
+                                          int a, double tb, int k, int b) {
+  #pragma clang fp contract(off)
+  const double mult = p.S[j] * p.S[k] * p.l * kSqrtPi * 0.5;
+  const double se = exp(-(p.D[k] * tb + p.D[j] * ta));
+  return mult * (h_tab(p, t, k, j, tb, ta, b, a, se) + h_tab(p, t, j, k, ta, tb, a, b, se));
+}
+
+// KxxTab's per-gene and per-row factors of one problem, into the shared memory t points to
+// (one 256-thread workgroup; two workgroup barriers).
+__device__ __forceinline__ void small_tables(const HypDev& h, const double* __restrict__ x, int n,
+                                             const KxxTab& t, double* gam, double* egg,
+                                             double* erg, double* e1, double* e2) {
+  #pragma clang fp contract(off)
+  const int tid = threadIdx.x, G = h.G;
+  const double l = h.l;
+  for (int g = tid; g < G; g += 256) {
+    const double gk = h.D[g] * l / 2.0;  // gamma(k), model.py:367-369
+    gam[g] = gk;
+    egg[g] = exp(gk * gk);
+    erg[g] = erf(gk);
+  }
+  __syncthreads();
+  for (int i = tid; i < n; i += 256) e2[i] = erf((x[3 * i] / l) - gam[gene_index(x[3 * i + 1], G)]);
+  for (int q = tid; q < n * G; q += 256) {
+    const int i = q / G, g = q - i * G;
+    e1[q] = erf(x[3 * i] / l + gam[g]);
+  }
+  __syncthreads();
+}
+
 // mean_function, model.py:143-149: m[i] = (B/D)[i / (n/G)] * int(x[i,2]).
 __device__ __forceinline__ double mean_at(const HypDev& p, const double* x, int64_t i,
                                           int64_t bs) {

@@ -48,6 +48,11 @@ int lfm_debug_lock_path(const lfm_ctx* ctx, char* buf, int len);
 /* The diagonal factor's pivot reciprocal square root (v_rsq_f64 + one Newton step) on x[n]. */
 int lfm_probe_rsq(lfm_ctx* ctx, const double* x, int64_t n, double* y);
 
+/* The small-problem kernel's gram entries two ways, for every pair of x[n x 3] (n, num_genes
+ * <= 63): out[0, n^2) by the reference restatement kernel_ref, out[n^2, 2 n^2) by the per-row /
+ * per-gene tables small_mll_kernel uses for gene-gene pairs (KxxTab, lfm_math.h). */
+int lfm_probe_kxx_tab(lfm_ctx* ctx, const double* x, int64_t n, const lfm_hyp* hyp, double* out);
+
 /* Layout probe: D = A(16x4) * B(4x16) on one wave through v_mfma_f64_16x16x4_f64;
  * A, B, D row-major host arrays. */
 int lfm_probe_mfma_f64_layout(lfm_ctx* ctx, const double* a, const double* b, double* d);

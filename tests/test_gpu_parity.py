@@ -303,6 +303,42 @@ def test_pivot_rsqrt_one_newton_step(lfm):
     assert rel.max() <= 1e-14, rel.max()
 
 
+@pytest.mark.parametrize("G,n,seed", [(4, 28, 1), (5, 35, 2), (7, 63, 3), (1, 9, 4)])
+def test_small_kernel_tables_are_bit_identical(lfm, G, n, seed):
+    """small_mll_kernel forms gene-gene pairs from per-row / per-gene tables (KxxTab, round 4):
+    every entry bit-identical to the reference restatement kernel_ref on the same device, over
+    random times (t = 0 included), gene indices that need the JAX clamp / wrap (-1, G + 2.7) and
+    mixed flags (latent rows, a flag of 2: kernel_ref's generic switch)."""
+    from dis_project_amd import _lib
+
+    rng = np.random.default_rng(seed)
+    x = np.stack([rng.uniform(0, 12, n), rng.integers(0, G, n).astype(np.float64),
+                  np.ones(n)], -1)
+    x[0, 0] = 0.0
+    x[1 % n, 1] = -1.0
+    x[2 % n, 1] = G + 2.7
+    if n > 8:
+        x[3::7, 2] = 0.0
+        x[5, 2] = 2.0
+    m = lfm.ExactLFM(num_genes=G, true_d=rng.uniform(0.2, 1.0, G), true_s=rng.uniform(0.5, 1.5, G),
+                     true_b=rng.uniform(0.01, 0.1, G), l=rng.uniform(1.0, 4.0))
+    x = np.ascontiguousarray(x)
+    out = np.empty(2 * n * n)
+    hp = m.hyp()
+    ctx = _lib.get_context(0)
+    ctx.check(ctx.diag.lfm_probe_kxx_tab(ctx.handle, _lib.dptr(x), n, hp.ref, _lib.dptr(out)))
+    ref, tab = out[: n * n], out[n * n:]
+    assert np.array_equal(ref.view(np.uint64), tab.view(np.uint64)), \
+        np.flatnonzero(ref.view(np.uint64) != tab.view(np.uint64))[:8]
+    # and the restatement against the oracle's formula (rows with flags 0 / 1)
+    ok = np.isin(x[:, 2], (0.0, 1.0))
+    xs = x[ok]
+    K = O.cross_covariance(xs, xs, m.true_d, m.true_s, m.l)
+    scale = O.gram_error_scale(xs, xs, m.true_d, m.true_s, m.l)
+    got = ref.reshape(n, n)[np.ix_(ok, ok)]
+    assert np.all(np.abs(got - K) <= 16 * np.finfo(float).eps * scale + 1e-300)
+
+
 @pytest.mark.parametrize("env", [{"LFM_SCHED": "3"}, {"LFM_SCHED": "3", "LFM_S3_EVENTS": "1"},
                                  {"LFM_SCHED": "3", "LFM_W4_MIN": "1024"},
                                  {"LFM_SCHED": "3", "LFM_W4_MIN": "1024", "LFM_S3_EVENTS": "1"},
