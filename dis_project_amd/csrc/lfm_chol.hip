@@ -989,6 +989,13 @@ struct Panel {
 #ifndef LFM_TALL_GROUP
 #define LFM_TALL_GROUP 1
 #endif
+// tall units claimed dynamically (1): every tall workgroup takes units from a per-launch device
+// counter in enumeration order (deepest first) until none is left, so an XCD that finishes its
+// rest units early takes the tall units a later XCD's workgroups would have run; (0) the static
+// deal above
+#ifndef LFM_TALL_DYN
+#define LFM_TALL_DYN 0
+#endif
 // workgroups of the tall segment: a multiple of 8 (XCDs), of 8 LFM_TALL_SPLIT when grouped
 __host__ __device__ constexpr int64_t tall_grid(int64_t nt) {
   return (LFM_TALL_RR && LFM_TALL_GROUP) ? (nt + 8 * LFM_TALL_SPLIT - 1) / (8 * LFM_TALL_SPLIT) *
@@ -1330,6 +1337,8 @@ struct StepArgs {
   GramGen gen;       // gen.tab != NULL: the first step's update units generate Sigma (fused gram)
   int64_t rest_off;  // rest units of this launch are [rest_off, rest_off + nr) of the step's
                      // enumeration (the side-CU helper launch takes the tail of it)
+  unsigned* tall_ctr;  // LFM_TALL_DYN: this launch's tall-unit counter (zeroed per call; NULL: the
+                      // static deal)
   unsigned long long* trace;  // diagnostics (NULL: off): 4 words per workgroup (lfm_debug_trace)
   unsigned long long trace_tag;  // launch tag, bits 40+ of each record's last word
 };
@@ -1375,6 +1384,105 @@ __device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
     __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+
+// tall unit u (row slab rb, column block cb, its part hf of LFM_TALL_SPLIT) of step s + 1:
+// deepest column blocks first (longest units), so the launch ends on short ones; the split
+// halves a unit's width so the launch's last round drains in shorter pieces
+// Returns false when its device-side wait ran out (the workgroup then stops claiming units).
+__device__ __forceinline__ bool tall_unit(const StepArgs& g, int64_t u, double (*sP)[KB + LDP],
+                                          unsigned long long* const st,
+                                          unsigned long long t_unit) {
+  auto add_dur = [&](int slot) {
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(st + slot, __builtin_amdgcn_s_memrealtime() - t_unit,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  constexpr int TCW = NB / LFM_TALL_SPLIT;  // output columns per tall unit
+  const int64_t nrb = g.nt / (g.tw * LFM_TALL_SPLIT);
+  const int cb = g.tw - 1 - (int)(u / (nrb * LFM_TALL_SPLIT));
+  const int64_t rq = u % (nrb * LFM_TALL_SPLIT);
+  const int64_t rb = rq / LFM_TALL_SPLIT;
+  const int c0 = cb * NB + (int)(rq % LFM_TALL_SPLIT) * TCW;  // first output column in X_{s+1}
+  const int64_t i0 = g.tr0 + rb * 64;
+  if (i0 > g.n && i0 < g.pad_end) return true;  // identity padding rows: their X is never read
+  {
+    __shared__ int ok;
+    // relaxed polling and device-coherent operand loads below instead of an acquire fence:
+    // an agent-scope acquire invalidates this XCD's L2 under the running bulk units
+    if (threadIdx.x == 0) {
+      int why = 0;
+      bool good = !g.chain_done || spin_until<false>(g.chain_done, 1u, g.spin, g.status);
+      if (!good) why = 1;
+      // rows past step s's update (bordered: the border rows that entered the window with
+      // super-panel s + 1, zero in every earlier panel column) have no ahead unit to wait for
+      if (good && g.a_done && (i0 - g.s0) / ST < g.T) {
+        good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], 2u * g.wn, g.spin, g.status);
+        if (!good) why = 2;
+      }
+      if (!good) timeout_at(g.status, why);
+      ok = good;
+    }
+    __syncthreads();
+    if (!ok) return false;
+    if (st) stamp_max(st + 2);
+  }
+  const int W = g.tw * NB;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (i0 >= g.copy_from) {
+    // border rows: X = e_{row - copy_from} Bd, the row of Bd (written through by the chain)
+    const double* src = g.Bd + (i0 - g.copy_from) * W + c0;
+    double* dst = g.X + (i0 - g.tr0) * W + c0;
+#pragma unroll 4
+    for (int u = 0; u < 64 * TCW / 2 / 256; ++u) {
+      const int idx = tid + 256 * u, r = idx / (TCW / 2), c2 = 2 * (idx % (TCW / 2));
+      *reinterpret_cast<double2*>(&dst[r * W + c2]) = ld2<true>(&src[(int64_t)r * W + c2]);
+    }
+    if (st) {
+      __syncthreads();
+      stamp_max(st + 3);
+      add_dur(6);
+    }
+    return true;
+  }
+  const int wr = (wv >> 1) * 32, wc = (wv & 1) * (TCW / 2);
+  const int li = lane & 15, lk = lane >> 4;
+  constexpr int JR = TCW / 32;  // 16-column blocks per wave
+#if LFM_MFMA16
+  double4v acc4[2][JR];
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+    for (int jr = 0; jr < JR; ++jr) acc4[rb][jr] = (double4v){0.0, 0.0, 0.0, 0.0};
+  gemm_accumulate16<64, true, true, KB, TCW>(g.A + i0 * g.lda + g.tk0, g.lda, g.Bd + c0, W,
+                                             NB * (cb + 1), acc4, sP);
+#define ACC(ir, jr) acc4[(ir) >> 2][jr][(ir) & 3]
+#else
+  static_assert(TCW == NB, "the 4x4x4 tile body has no split tall units");
+  double acc[8][4];
+#pragma unroll
+  for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = 0.0;
+  gemm_accumulate<64, true, true>(g.A + i0 * g.lda + g.tk0, g.lda, g.Bd + cb * NB, W,
+                                  NB * (cb + 1), acc, sP);
+#define ACC(ir, jr) acc[ir][jr]
+#endif
+  double* Xb = g.X + (i0 - g.tr0 + wr + lk) * W + c0 + wc + li;
+#pragma unroll
+  for (int ir = 0; ir < 8; ++ir)
+#pragma unroll
+    for (int jr = 0; jr < JR; ++jr) {
+      Xb[(ir * 4) * W + jr * 16] = ACC(ir, jr);
+      if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + c0 + wc + jr * 16 + li] = ACC(ir, jr);
+    }
+#undef ACC
+  if (st) {
+    __syncthreads();
+    stamp_max(st + 3);
+    add_dur(6);
+  }
+  return true;
+}
 
 __device__ __forceinline__ void step_body(const StepArgs& g) {
   __shared__ double sPbuf[(64 + ST) * (LFM_STEP_KS + LDP)];
@@ -1449,93 +1557,19 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
     }
     return;
   }
-  // tall unit (row slab rb, column block cb, its part hf of LFM_TALL_SPLIT) of step s + 1:
-  // deepest column blocks first (longest units), so the launch ends on short ones; the split
-  // halves a unit's width so the launch's last round drains in shorter pieces
-  constexpr int TCW = NB / LFM_TALL_SPLIT;  // output columns per tall unit
-  const int64_t nrb = g.nt / (g.tw * LFM_TALL_SPLIT);
-  const int cb = g.tw - 1 - (int)(u / (nrb * LFM_TALL_SPLIT));
-  const int64_t rq = u % (nrb * LFM_TALL_SPLIT);
-  const int64_t rb = rq / LFM_TALL_SPLIT;
-  const int c0 = cb * NB + (int)(rq % LFM_TALL_SPLIT) * TCW;  // first output column in X_{s+1}
-  const int64_t i0 = g.tr0 + rb * 64;
-  if (i0 > g.n && i0 < g.pad_end) return;  // identity padding rows: their X is never read
-  {
-    __shared__ int ok;
-    // relaxed polling and device-coherent operand loads below instead of an acquire fence:
-    // an agent-scope acquire invalidates this XCD's L2 under the running bulk units
-    if (threadIdx.x == 0) {
-      int why = 0;
-      bool good = !g.chain_done || spin_until<false>(g.chain_done, 1u, g.spin, g.status);
-      if (!good) why = 1;
-      // rows past step s's update (bordered: the border rows that entered the window with
-      // super-panel s + 1, zero in every earlier panel column) have no ahead unit to wait for
-      if (good && g.a_done && (i0 - g.s0) / ST < g.T) {
-        good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], 2u * g.wn, g.spin, g.status);
-        if (!good) why = 2;
-      }
-      if (!good) timeout_at(g.status, why);
-      ok = good;
-    }
-    __syncthreads();
-    if (!ok) return;
-    if (st) stamp_max(st + 2);
-  }
-  const int W = g.tw * NB;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (i0 >= g.copy_from) {
-    // border rows: X = e_{row - copy_from} Bd, the row of Bd (written through by the chain)
-    const double* src = g.Bd + (i0 - g.copy_from) * W + c0;
-    double* dst = g.X + (i0 - g.tr0) * W + c0;
-#pragma unroll 4
-    for (int u = 0; u < 64 * TCW / 2 / 256; ++u) {
-      const int idx = tid + 256 * u, r = idx / (TCW / 2), c2 = 2 * (idx % (TCW / 2));
-      *reinterpret_cast<double2*>(&dst[r * W + c2]) = ld2<true>(&src[(int64_t)r * W + c2]);
-    }
-    if (st) {
+  if (LFM_TALL_DYN && g.tall_ctr) {
+    // claim units until the counter passes the last one (workgroup-uniform)
+    __shared__ int64_t su;
+    for (;;) {
+      __syncthreads();  // every thread has read the previous claim
+      if (threadIdx.x == 0)
+        su = __hip_atomic_fetch_add(g.tall_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __syncthreads();
-      stamp_max(st + 3);
-      add_dur(6);
+      const int64_t v = su;
+      if (v >= g.nt || !tall_unit(g, v, sP, st, t_unit)) return;
     }
-    return;
   }
-  const int wr = (wv >> 1) * 32, wc = (wv & 1) * (TCW / 2);
-  const int li = lane & 15, lk = lane >> 4;
-  constexpr int JR = TCW / 32;  // 16-column blocks per wave
-#if LFM_MFMA16
-  double4v acc4[2][JR];
-#pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-    for (int jr = 0; jr < JR; ++jr) acc4[rb][jr] = (double4v){0.0, 0.0, 0.0, 0.0};
-  gemm_accumulate16<64, true, true, KB, TCW>(g.A + i0 * g.lda + g.tk0, g.lda, g.Bd + c0, W,
-                                             NB * (cb + 1), acc4, sP);
-#define ACC(ir, jr) acc4[(ir) >> 2][jr][(ir) & 3]
-#else
-  static_assert(TCW == NB, "the 4x4x4 tile body has no split tall units");
-  double acc[8][4];
-#pragma unroll
-  for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-    for (int jr = 0; jr < 4; ++jr) acc[ir][jr] = 0.0;
-  gemm_accumulate<64, true, true>(g.A + i0 * g.lda + g.tk0, g.lda, g.Bd + cb * NB, W,
-                                  NB * (cb + 1), acc, sP);
-#define ACC(ir, jr) acc[ir][jr]
-#endif
-  double* Xb = g.X + (i0 - g.tr0 + wr + lk) * W + c0 + wc + li;
-#pragma unroll
-  for (int ir = 0; ir < 8; ++ir)
-#pragma unroll
-    for (int jr = 0; jr < JR; ++jr) {
-      Xb[(ir * 4) * W + jr * 16] = ACC(ir, jr);
-      if (i0 + wr + ir * 4 + lk == g.n) g.zvec[g.tk0 + c0 + wc + jr * 16 + li] = ACC(ir, jr);
-    }
-#undef ACC
-  if (st) {
-    __syncthreads();
-    stamp_max(st + 3);
-    add_dur(6);
-  }
+  tall_unit(g, u, sP, st, t_unit);
 }
 
 // Diagnostics (lfm_debug_trace): per workgroup {entry, exit} (s_memrealtime), the hardware
@@ -2409,7 +2443,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     if (!r)
       r = ensure(ctx, (void**)&ctx->linv_full, &ctx->linv_full_bytes, (size_t)NB * NB * sizeof(double));
     if (!r) r = ensure(ctx, (void**)&ctx->xd, &ctx->xd_bytes, (size_t)Wmax * Wmax * sizeof(double));
-    const size_t nflags = (size_t)S * (3 + Tmax);
+    // + one tall-unit counter per step launch (LFM_TALL_DYN; event-ordered: two launches a step)
+    const size_t nflags = (size_t)S * (3 + Tmax) + 2 * (size_t)S + 2;
     if (!r) r = ensure(ctx, (void**)&ctx->flags, &ctx->flags_bytes, nflags * sizeof(unsigned));
     if (r) return r;
     unsigned* chain_done = ctx->flags;     // [S]
@@ -2419,6 +2454,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     auto xbuf = [&](int s) { return ctx->xbuf + (size_t)(s & 1) * Mp * Wmax; };
     unsigned* bars = a_done + (size_t)S * Tmax;  // [S] grid barrier counters of chain(s)
     unsigned* xready = bars + S;                  // [S] inputs of chain(s) landed (s >= 1)
+    unsigned* tall_ctrs = xready + S;             // [2 S + 2] LFM_TALL_DYN claim counters
+    int ntall_launch = 0;
     auto wkbuf = [&](int s) { return ctx->wk + (size_t)(s & 1) * 2 * Wmax * Wmax; };
     // launch j = s - 2 (step j's update) writes the inputs of chain(s), s >= 2: the block's
     // tiles (leading rest units, w_s (w_s + 1) slabs) and its rows of the columns of super-
@@ -2479,6 +2516,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       if (!g.zero_from) g.zero_from = INT64_MAX;
       if (!g.copy_from) g.copy_from = INT64_MAX;
       g.spin = ctx->wait_ticks;
+      g.tall_ctr = LFM_TALL_DYN && g.nt > 0 ? tall_ctrs + ntall_launch++ : nullptr;
       const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 + (int64_t)(g.nr + 7) / 8 * 8 +
                            tall_grid(g.nt);
       if (grid == 0) return;
