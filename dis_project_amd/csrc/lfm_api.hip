@@ -353,11 +353,19 @@ int with_s3_fallback(lfm_ctx* ctx, F&& attempt) {
   for (hipStream_t st : {ctx->m3, ctx->s3})
     if (st) hipStreamSynchronize(st);
   const unsigned ticks = ctx->wait_ticks;
+  const bool had_side = ctx->side != nullptr;
   ctx->s3_yield = true;
   ctx->wait_ticks = std::max(ticks, kFallbackWaitTicks);
   r = attempt();
   ctx->wait_ticks = ticks;
   ctx->s3_yield = false;
+  if (!had_side && ctx->side) {
+    // schedule 1's high-priority stream was created for the re-run: give its hardware queue back
+    // (an idle queue beside the partitioned pair slows the schedule-3 calls that follow, §5)
+    hipStreamSynchronize(ctx->side);
+    hipStreamDestroy(ctx->side);
+    ctx->side = nullptr;
+  }
   if (r == LFM_OK || r == LFM_E_NOT_PD) {
     ctx->fallbacks += 1;
     if (r == LFM_OK) ctx->err = "schedule 3 stalled (" + why + "); the call was re-run on schedule 1";

@@ -365,3 +365,27 @@ def test_small_problem_cache_holds_its_datasets():
     assert len(ctx.lib.created) == 2 and len(ctx.lib.destroyed) == 1
     close()
     assert len(ctx.lib.destroyed) == 2
+
+
+@pytest.mark.gpu
+def test_resident_batch_large_small_problems():
+    """lfm_batch with problems past one wave (n + 1 > 64: the 256-thread factor, kernel_ref
+    gram; n = 84 as the pooled-replicate ablation, n = 128 the largest) beside small ones, in one
+    launch: every value within 1e-9 of the oracle."""
+    from dis_project_amd import _lib
+    from dis_project_amd.dataset import Dataset, grid_inputs
+    from dis_project_amd.model import ExactLFM
+
+    rng = np.random.default_rng(11)
+    models, datasets = [], []
+    for G, T in ((4, 21), (4, 32), (4, 7), (2, 64), (1, 128)):
+        D, S, B = rng.uniform(0.2, 1.0, G), rng.uniform(0.5, 1.5, G), rng.uniform(0.01, 0.1, G)
+        x = grid_inputs(G, T)
+        y = np.repeat(B / D, T) + 0.5 * rng.standard_normal(G * T)
+        models.append(ExactLFM(jitter=1e-4, num_genes=G, true_d=D, true_s=S, true_b=B))
+        datasets.append(Dataset(x, y))
+    ev = farm.BatchEvaluator(_lib.get_context(), datasets)
+    try:
+        np.testing.assert_allclose(ev(models), _oracle_eval(models, datasets), rtol=1e-9)
+    finally:
+        ev.close()
