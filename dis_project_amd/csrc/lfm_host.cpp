@@ -209,30 +209,27 @@ void TenancyLock::unlock_exclusive() {
 
 void TenancyLock::lock_shared() {
   rw_.lock_shared();
+  if (fd_ < 0) return;
   if (files()) {
-    {
-      std::lock_guard<std::mutex> tl(turn_mu_);
-      if (int e = flock_retry(turn_, LOCK_EX)) {  // behind any writer waiting in another process
-        fail(e, "turnstile, shared");
-        return;
-      }
-      if (int e = flock_retry(turn_, LOCK_UN)) fail(e, "turnstile, release");
-    }
-    std::lock_guard<std::mutex> fl(fd_mu_);
-    if (readers_ == 0 && files()) {
-      if (int e = flock_retry(fd_, LOCK_SH)) {
-        fail(e, "lock, shared");
-        return;
-      }
-    }
-    ++readers_;
+    std::lock_guard<std::mutex> tl(turn_mu_);
+    // behind any writer waiting in another process
+    if (int e = flock_retry(turn_, LOCK_EX)) fail(e, "turnstile, shared");
+    else if (int e2 = flock_retry(turn_, LOCK_UN)) fail(e2, "turnstile, release");
+  }
+  // every shared holder is counted, whatever the file lock's state: the LOCK_SH taken by the
+  // first is released by the last (sh_held_), also if a failure turned the files off between
+  std::lock_guard<std::mutex> fl(fd_mu_);
+  if (readers_++ == 0 && files()) {
+    if (int e = flock_retry(fd_, LOCK_SH)) fail(e, "lock, shared");
+    else sh_held_ = true;
   }
 }
 
 void TenancyLock::unlock_shared() {
-  {
+  if (fd_ >= 0) {
     std::lock_guard<std::mutex> fl(fd_mu_);
-    if (readers_ > 0 && --readers_ == 0) {
+    if (--readers_ == 0 && sh_held_) {
+      sh_held_ = false;
       if (int e = flock_retry(fd_, LOCK_UN)) fail(e, "lock, release");
     }
   }

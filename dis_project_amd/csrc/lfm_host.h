@@ -115,6 +115,7 @@ class TenancyLock {
   void fail(int e, const char* what);     // records (and logs) the first flock failure
   std::atomic<int> err_{0};
   bool fd_held_ = false;  // LOCK_EX on fd_ held by this process's exclusive holder
+  bool sh_held_ = false;  // LOCK_SH on fd_ held for this process's shared holders (fd_mu_)
   std::shared_mutex rw_;  // in-process readers-writer lock
   std::mutex turn_mu_;    // this process's threads at the turnstile, one at a time
   std::mutex fd_mu_;      // readers_ and the flock state of fd_
