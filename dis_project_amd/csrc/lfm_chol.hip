@@ -989,6 +989,10 @@ struct Panel {
 #ifndef LFM_TALL_GROUP
 #define LFM_TALL_GROUP 1
 #endif
+// 32-row ahead / rest units in the w = 1 steps (LFM_TR32 at run time; this is its default)
+#ifndef LFM_TR32_DEFAULT
+#define LFM_TR32_DEFAULT 0
+#endif
 // tall units claimed dynamically (1): every tall workgroup takes units from a per-launch device
 // counter in enumeration order (deepest first) until none is left, so an XCD that finishes its
 // rest units early takes the tall units a later XCD's workgroups would have run; (0) the static
@@ -1337,6 +1341,8 @@ struct StepArgs {
   GramGen gen;       // gen.tab != NULL: the first step's update units generate Sigma (fused gram)
   int64_t rest_off;  // rest units of this launch are [rest_off, rest_off + nr) of the step's
                      // enumeration (the side-CU helper launch takes the tail of it)
+  int sub;             // ahead / rest units per 128-row tile: 2 (64-row units, step_kernel) or 4
+                      // (32-row units, step_kernel32: the w = 1 steps, LFM_TR32)
   unsigned* tall_ctr;  // LFM_TALL_DYN: this launch's tall-unit counter (zeroed per call; NULL: the
                       // static deal)
   unsigned long long* trace;  // diagnostics (NULL: off): 4 words per workgroup (lfm_debug_trace)
@@ -1416,7 +1422,8 @@ __device__ __forceinline__ bool tall_unit(const StepArgs& g, int64_t u, double (
       // rows past step s's update (bordered: the border rows that entered the window with
       // super-panel s + 1, zero in every earlier panel column) have no ahead unit to wait for
       if (good && g.a_done && (i0 - g.s0) / ST < g.T) {
-        good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], 2u * g.wn, g.spin, g.status);
+        good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], (unsigned)(g.sub * g.wn), g.spin,
+                                 g.status);
         if (!good) why = 2;
       }
       if (!good) timeout_at(g.status, why);
@@ -1484,7 +1491,9 @@ __device__ __forceinline__ bool tall_unit(const StepArgs& g, int64_t u, double (
   return true;
 }
 
+template <int TR>
 __device__ __forceinline__ void step_body(const StepArgs& g) {
+  constexpr int SUB = ST / TR;  // units per 128-row tile
   __shared__ double sPbuf[(64 + ST) * (LFM_STEP_KS + LDP)];
   double (*sP)[KB + LDP] = reinterpret_cast<double (*)[KB + LDP]>(sPbuf);
   double (*sPu)[LFM_STEP_KS + LDP] = reinterpret_cast<double (*)[LFM_STEP_KS + LDP]>(sPbuf);
@@ -1514,13 +1523,14 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
   if (role == 1) {
     // device-coherent stores + a counter bump once they have completed: the tall units read
     // these rows with device-coherent loads (no L2 writeback / invalidate on either side)
-    syrk_unit<true, 64, true, LFM_STEP_KS>(g.A, g.lda, g.s0, g.px, g.kd, g.T, 0, g.wn, u, g.wn, sPu,
+    syrk_unit<true, TR, true, LFM_STEP_KS>(g.A, g.lda, g.s0, g.px, g.kd, g.T, 0, g.wn, u, g.wn, sPu,
                                            0, g.n, g.pad_end, g.zero_from,
                                            g.gen.tab ? &g.gen : nullptr);
     __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     // 128-tile row of the unit (the band's enumeration order, syrk_unit)
-    const int trow = LFM_BAND_ROWS ? g.wn + (int)(u / (2 * g.wn)) : g.wn + (int)(u % (2 * (g.T - g.wn))) / 2;
+    const int trow = LFM_BAND_ROWS ? g.wn + (int)(u / (SUB * g.wn))
+                                   : g.wn + (int)(u % (SUB * (g.T - g.wn))) / SUB;
     if (threadIdx.x == 0 && g.a_done)
       __hip_atomic_fetch_add(&g.a_done[trow], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0 && g.xready && trow < g.wn + g.lead)
@@ -1538,7 +1548,7 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
       c0 = __builtin_amdgcn_s_memtime();
       r0 = __builtin_amdgcn_s_memrealtime();
     }
-    const bool lead = syrk_unit<true, 64, false, LFM_STEP_KS>(g.A, g.lda, g.s0, g.px, g.kd, g.T,
+    const bool lead = syrk_unit<true, TR, false, LFM_STEP_KS>(g.A, g.lda, g.s0, g.px, g.kd, g.T,
                                                               g.wn, g.T, u + g.rest_off, 0, sPu,
                                                               g.xready ? g.wn + g.lead : 0, g.n,
                                                               g.pad_end, g.zero_from,
@@ -1574,10 +1584,11 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
 
 // Diagnostics (lfm_debug_trace): per workgroup {entry, exit} (s_memrealtime), the hardware
 // id (HW_ID | XCC_ID << 32) and the launch tag | role << 32 | unit (role 0: padding)
+template <int TR>
 __device__ __forceinline__ void step_traced(const StepArgs& g) {
   __shared__ unsigned long long t0;  // in LDS: nothing held in registers across the body
   if (threadIdx.x == 0) t0 = __builtin_amdgcn_s_memrealtime();
-  step_body(g);
+  step_body<TR>(g);
   __syncthreads();
   if (threadIdx.x == 0) {
     const int64_t b = blockIdx.x;
@@ -1600,15 +1611,19 @@ __device__ __forceinline__ void step_traced(const StepArgs& g) {
 }
 
 // (256, 4): 128 VGPRs, 4 waves / SIMD (the zero-C tile body would otherwise take 134)
-__global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) { step_body(g); }
+__global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) { step_body<64>(g); }
+// The w = 1 steps' launches with 32-row ahead / rest units (LFM_TR32): twice the units of half
+// the work, so a launch of one or two rounds of units is quantized half as coarsely
+__global__ __launch_bounds__(256, 4) void step_kernel32(StepArgs g) { step_body<32>(g); }
 // The side-CU helper's launches (rest units only): the same body under its own name, so
 // traces and counters keep the main-stream step launches apart
-__global__ __launch_bounds__(256, 4) void helper_update_kernel(StepArgs g) { step_body(g); }
+__global__ __launch_bounds__(256, 4) void helper_update_kernel(StepArgs g) { step_body<64>(g); }
 // Both with the unit trace (lfm_debug_trace on): separate symbols, so the product kernels'
 // code is the untraced body
-__global__ __launch_bounds__(256, 4) void step_kernel_traced(StepArgs g) { step_traced(g); }
+__global__ __launch_bounds__(256, 4) void step_kernel_traced(StepArgs g) { step_traced<64>(g); }
+__global__ __launch_bounds__(256, 4) void step_kernel32_traced(StepArgs g) { step_traced<32>(g); }
 __global__ __launch_bounds__(256, 4) void helper_update_kernel_traced(StepArgs g) {
-  step_traced(g);
+  step_traced<64>(g);
 }
 
 // ---------------------------------------------------------- fused panel
@@ -2264,6 +2279,7 @@ int probe_update_launch(lfm_ctx* ctx, hipStream_t st, int T, int kd, int cio, in
     // the schedule-3 step kernel's rest role alone (the production unit: 16-deep stages,
     // 4 workgroups / CU, supertile order); bit 5: no C loads (C = 0, stores kept)
     StepArgs g{};
+    g.sub = 2;
     g.A = ctx->A;
     g.lda = n;
     g.s0 = 512;
@@ -2460,9 +2476,16 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     // launch j = s - 2 (step j's update) writes the inputs of chain(s), s >= 2: the block's
     // tiles (leading rest units, w_s (w_s + 1) slabs) and its rows of the columns of super-
     // panel s - 1 (leading ahead units, 2 w_s w_{s-1} slabs); chain(s) forms X_{s-1} of its rows
+    // 32-row units (step_kernel32) for the w = 1 steps after the first (LFM_TR32, read per call;
+    // never the Sigma-generating step 0 or a bordered window)
+    const int tr32 = env_int("LFM_TR32", LFM_TR32_DEFAULT);
+    auto sub_of = [&](int s) {
+      return tr32 && !bordered && s > 0 && steps[s].second == 1 ? 4 : 2;
+    };
+    // (in 64-row slabs; launch s - 2's units are sub_of(s - 2) / 2 slabs each)
     auto xtarget = [&](int s) {
       const int ws = steps[s].second;
-      return (unsigned)(ws * (ws + 1) + 2 * ws * steps[s - 1].second);
+      return (unsigned)((ws * (ws + 1) + 2 * ws * steps[s - 1].second) * sub_of(s - 2) / 2);
     };
     // chain(s): factor block s on the side stream's CUs (one launch, see chain_kernel)
     auto chain = [&](int s, bool dev_wait = true) {
@@ -2516,6 +2539,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       if (!g.zero_from) g.zero_from = INT64_MAX;
       if (!g.copy_from) g.copy_from = INT64_MAX;
       g.spin = ctx->wait_ticks;
+      if (!g.sub) g.sub = 2;
       g.tall_ctr = LFM_TALL_DYN && g.nt > 0 ? tall_ctrs + ntall_launch++ : nullptr;
       const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 + (int64_t)(g.nr + 7) / 8 * 8 +
                            tall_grid(g.nt);
@@ -2525,7 +2549,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       // matrix (rows s0 .. n, residual row n included: it is the forward substitution) less
       // the next diagonal block (the chain's), and the triangular solve of the rows below
       // the next super-panel (rows .. n) against its W' x W' factor
-      const double issued = ((double)g.na + g.nr) * 64 * ST * 2.0 * g.kd +
+      const double issued = ((double)g.na + g.nr) * (ST / g.sub) * ST * 2.0 * g.kd +
                             (double)g.nt * 64 * (ST / LFM_TALL_SPLIT) * NB * (g.tw + 1);
       double alg = 0.0;
       if (g.na + g.nr > 0) {
@@ -2543,8 +2567,12 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       trace_launch(ctx, g, grid, false);
       hipEvent_t pe;
       prof_begin(ctx, K_SYRK, &pe, main);
-      hipLaunchKernelGGL(g.trace ? step_kernel_traced : step_kernel, dim3((unsigned)grid),
-                         dim3(256), 0, main, g);
+      if (g.sub == 4)
+        hipLaunchKernelGGL(g.trace ? step_kernel32_traced : step_kernel32, dim3((unsigned)grid),
+                           dim3(256), 0, main, g);
+      else
+        hipLaunchKernelGGL(g.trace ? step_kernel_traced : step_kernel, dim3((unsigned)grid),
+                           dim3(256), 0, main, g);
       prof_end(ctx, K_SYRK, pe, alg, 0, main, issued);
     };
     auto tall_args = [&](StepArgs& g, int s) {  // tall part of the step launch: step s's rows
@@ -2579,8 +2607,9 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.wn = wn;
       if (bordered) g.zero_from = Mp + steps[s].first * NB;
       if (fused && s == 0) g.gen = *gen;
-      g.na = 2 * wn * (T - wn);
-      g.nr = (T - wn) * (T - wn + 1);  // 2 slabs per tile of the (T - wn)-tile triangle
+      g.sub = sub_of(s);
+      g.na = g.sub * wn * (T - wn);
+      g.nr = g.sub / 2 * (T - wn) * (T - wn + 1);  // sub units per tile of the (T - wn)-tile triangle
       g.status = ctx->status;
     };
     // units of step s's rest triangle for the side-CU helper: the main launch of U unit-
@@ -2672,7 +2701,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         // units store without write-through and bump no counter, so they never include a lead
         // tile of chain(s + 2).
         const int64_t total = g.nr;  // the step's rest enumeration
-        const int64_t hu = s >= 1 && s + 2 < S
+        const int64_t hu = s >= 1 && s + 2 < S && g.sub == 2
                                ? helper_clamp(helper_share(g, steps[s + 1].second), (int)total,
                                               g.T, g.wn, g.xready ? g.lead : 0, LFM_SUPERTILE)
                                : 0;

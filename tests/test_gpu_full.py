@@ -330,3 +330,34 @@ def test_side_cu_helper_forced_on_every_step(monkeypatch, G, T):
     assert out["0"][1] == 0 and out["1"][1] > 0  # the forced run used helper launches
     assert np.isfinite(out["1"][0]) and out["1"][0] == out["0"][0]
 
+
+
+@pytest.mark.parametrize("G,T", [(16, 256), (64, 256), (10, 200)])
+def test_tr32_units_are_bit_identical(monkeypatch, G, T):
+    """32-row ahead / rest units in the w = 1 steps (LFM_TR32=1, step_kernel32: the same
+    16x16x4 MFMA sequence per output element as the 64-row units) give the MLL bit for bit;
+    the chain-input counts (xtarget, per-tile a_done) follow the unit size; N = 4096, the
+    N = 16384 bench workload and a non-aligned N = 2000 layout; also with the helper forced
+    onto every eligible step (the helper stays on 64-row units)."""
+    from dis_project_amd import _lib, configs
+
+    work = configs.grid_workload("tr32", G, T, seed_params=2, seed_y=3)
+    x = np.ascontiguousarray(work.data.X)
+    y = np.ascontiguousarray(work.data.y.reshape(-1))
+    ctx = _lib.Context(0)
+    try:
+        out = {}
+        for tr32, helper_min in (("0", None), ("1", None), ("1", "0")):
+            monkeypatch.setenv("LFM_TR32", tr32)
+            if helper_min is None:
+                monkeypatch.delenv("LFM_HELPER_MIN", raising=False)
+            else:
+                monkeypatch.setenv("LFM_HELPER_MIN", helper_min)
+            v = np.empty(1)
+            ctx.check(ctx.lib.lfm_mll_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
+                                          work.model.hyp().ref, 0, _lib.dptr(v)))
+            out[(tr32, helper_min)] = float(v[0])
+        assert np.isfinite(out[("0", None)])
+        assert out[("1", None)] == out[("0", None)] == out[("1", "0")], out
+    finally:
+        ctx.close()
