@@ -164,7 +164,9 @@ int lfm_mll_batch_f64(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, int
  * leave-one-gene-out ablation farm of src/notebook.py:33-75, each problem the MLL of
  * src/objectives.py:64-78. x / y of every problem (probs[p].x, .y, .n; n <= 128, n % num_genes
  * == 0) go to HBM here, once; of probs[p].hyp only num_genes is read (it fixes the layout of the
- * packed hyperparameters). The caller's x / y may be freed after the call. */
+ * packed hyperparameters). The caller's x / y may be freed after the call. A batch belongs to
+ * the device of the ctx that created it and, like a ctx, to one host thread at a time (its
+ * pinned hyperparameter / result buffer is reused by every call). */
 typedef struct lfm_batch lfm_batch;
 int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_batch** out);
 int lfm_batch_destroy(lfm_batch* batch);
