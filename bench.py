@@ -727,14 +727,23 @@ def main(argv=None):
                     rec = json.load(open(tf))
                     per_eval = rec.get("hbm_bytes_per_eval")
                     pmc_lpe = rec.get("launches", 0) / max(1, rec.get("evals", 1))
-                    traffic = per_eval / (syrk["launches"] / prof_steps) if per_eval else None
-                    tsrc = ("PMC (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction) bytes "
-                            "per evaluation from profiles/syrk_traffic.json, measured on the "
-                            "event-ordered schedule 3 (LFM_S3_EVENTS=1, no side-CU helper: "
-                            f"{pmc_lpe:.0f} step launches per eval) - "
-                            "device-side cross-stream waits cannot run under the counters' "
-                            "serialised dispatch - divided by this run's "
-                            f"{syrk['launches'] // prof_steps} launches per evaluation")
+                    lpe = syrk["launches"] / prof_steps
+                    if rec.get("schedule") == "LFM_S3_EVENTS=2" and round(pmc_lpe) == round(lpe):
+                        # the counters saw this schedule's own launches (serialised by events)
+                        traffic = rec.get("hbm_bytes_per_launch")
+                        tsrc = ("PMC (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction) "
+                                "per step launch, profiles/syrk_traffic.json: the timed "
+                                "schedule's own launches, serialised by stream events "
+                                f"(LFM_S3_EVENTS=2, {pmc_lpe:.0f} per evaluation, as here) so "
+                                "their device-side waits are met under the counters' serialised "
+                                "dispatch; per launch in its last_eval_launch_bytes")
+                    else:
+                        traffic = per_eval / lpe if per_eval else None
+                        tsrc = ("PMC (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction) "
+                                "bytes per evaluation from profiles/syrk_traffic.json "
+                                f"({pmc_lpe:.0f} step launches per eval, schedule "
+                                f"{rec.get('schedule', 'LFM_S3_EVENTS=1')}) divided by this "
+                                f"run's {lpe:.0f} launches per evaluation")
                 except Exception:
                     traffic = None
             line["roofline"] = {

@@ -630,7 +630,9 @@ void release_partition(lfm_ctx* ctx) {
 //   LFM_SCHED            3 (default) or 1: the look-ahead schedule of the MLL factorisation
 //                        (1: no CU partition is created; lfm_ctx_set_schedule changes it later)
 //   LFM_SIDE_CUS         CUs reserved for the schedule-3 factor chain (0: schedule 1 only)
-//   LFM_S3_EVENTS        1: schedule 3 ordered by stream events (for rocprofv3 --pmc)
+//   LFM_S3_EVENTS        1: schedule 3 ordered by stream events, tall units in launches of
+//                        their own (for rocprofv3 --pmc); 2: the timed schedule's own launches,
+//                        serialised by events so each one's device-side waits are met at dispatch
 //   LFM_DEVICE_WAIT_MS   time bound of every device-side wait (default 2000 ms; lfm_chol.hip)
 //   LFM_DEBUG_SPIN_LIMIT the same bound in raw 100 MHz ticks (tests force timeouts with 0)
 //   LFM_GRAD_DIRECT      1: the gradient's per-pair path even on a grid layout (cross-check)
@@ -638,7 +640,7 @@ void release_partition(lfm_ctx* ctx) {
 //                        generate it (cross-check: the MLL is bit-identical either way)
 hipError_t create_streams(lfm_ctx* ctx) {
   ctx->sched = env_int_api("LFM_SCHED", 3) == 1 ? 1 : 3;
-  ctx->s3_events = env_int_api("LFM_S3_EVENTS", 0) != 0;
+  ctx->s3_events = (int)env_int_api("LFM_S3_EVENTS", 0);
   ctx->grad_direct = env_int_api("LFM_GRAD_DIRECT", 0) != 0;
   ctx->gram_fuse = env_int_api("LFM_GRAM_FUSE", LFM_GRAM_FUSE_DEFAULT) != 0;
   if (const char* ms = std::getenv("LFM_DEVICE_WAIT_MS")) {

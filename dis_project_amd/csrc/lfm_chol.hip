@@ -2401,7 +2401,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   const std::vector<std::pair<int64_t, int>> steps =
       plan_steps(nblk, Mp, NB, bordered, s3, wbulk, w4min, w2min, (int)env_int("LFM_W0", 1));
   const int S = (int)steps.size();
-  r = ensure_events(ctx, 2 * (size_t)S + 3);
+  r = ensure_events(ctx, 3 * (size_t)S + 3);  // [2 S + 3, 3 S + 3): LFM_S3_EVENTS=2
   if (r) return r;
   // fused gram (GramGen): in memory only the first block column (chain(0), X_0) and the next
   // super-panel's diagonal block (chain(1)); launch 0's update units generate the rest
@@ -2627,7 +2627,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     // and waits on the device for its inputs (xready[s]) from the main launch in flight
     hipEventRecord(ev[0], main);
     hipStreamWaitEvent(side, ev[0], 0);
-    if (ctx->s3_events) {
+    if (ctx->s3_events == 1) {
       // The same work ordered by stream events only (tall units in launches of their own after
       // the factor's event, chains after the tall launch's event) — for tools that serialise
       // dispatches (rocprofv3 --pmc), under which device-side waits between the two streams
@@ -2660,7 +2660,17 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         launch_step(g);
       }
     } else {
+      // LFM_S3_EVENTS=2: these same launches, each also ordered by events after every launch
+      // its device-side waits name (chain(s + 1) after launch s - 1, launch s after chain(s + 1)),
+      // so a tool that serialises dispatches (rocprofv3 --pmc) counts the timed schedule's own
+      // launches, one for one
+      const bool serial = ctx->s3_events == 2;
+      hipEvent_t* evC = ev + 2 * S + 3;  // [S] chain(s) done (serialised only)
       chain(0);
+      if (serial) {
+        hipEventRecord(evC[0], side);
+        hipStreamWaitEvent(main, evC[0], 0);
+      }
       {
         // X_0 once the first block is factored (its units wait for chain_done[0])
         StepArgs g{};
@@ -2684,7 +2694,12 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         return a * 2.0 * kd;
       };
       for (int s = 0; s + 1 < S; ++s) {
+        if (serial && s >= 1) hipStreamWaitEvent(side, evL[2 * (s - 1)], 0);
         chain(s + 1);
+        if (serial) {
+          hipEventRecord(evC[s + 1], side);
+          hipStreamWaitEvent(main, evC[s + 1], 0);
+        }
         StepArgs g{};
         update_args(g, s);
         tall_args(g, s + 1);

@@ -76,7 +76,7 @@ struct lfm_ctx {
   bool s3_yield = false;                         // this call runs schedule 1: nested in a
                                                  // shared hold of the device's tenancy lock
   int last_sched = 0;                            // schedule the last factorisation ran (diag)
-  bool s3_events = false;                        // schedule 3 ordered by events (LFM_S3_EVENTS)
+  int s3_events = 0;  // LFM_S3_EVENTS: 1 schedule 3 ordered by events, 2 its timed launches serialised
   unsigned wait_ticks = 200000000u;              // device-side wait bound, 100 MHz ticks (2 s;
                                                  // LFM_DEVICE_WAIT_MS, LFM_DEBUG_SPIN_LIMIT)
   int64_t fallbacks = 0;                         // schedule-3 calls re-run on schedule 1 after a

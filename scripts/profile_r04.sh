@@ -8,8 +8,9 @@
 #     c4  the fp32 N = 65536 gram fill                          prof_c4
 #     c2 with LFM_GRAM_FUSE=0 (the fp64 gram as its own kernel) prof_unfused
 #     c5  the resident small-problem batch                      prof_c5
-#   PMC passes, one counter group per pass, event-ordered (LFM_S3_EVENTS=1: device-side cross-
-#   stream waits cannot be met under the counters' serialised dispatch): FETCH_SIZE and
+#   PMC passes, one counter group per pass, on the timed schedule's own launches serialised by
+#   stream events (LFM_S3_EVENTS=2: every device-side cross-stream wait is met at dispatch, which
+#   the counters' serialised dispatch needs): FETCH_SIZE and
 #   WRITE_SIZE of c2, WRITE_SIZE of c4 and of the unfused gram, MFMA busy of the production unit
 #   alone and of every c2 step launch
 #   the bench lines of c2 / c3 / c4 / c5, the step timeline, the unit trace, value_and_grad
@@ -23,9 +24,9 @@ S=scripts/gpu_step.sh
 $S prof_trace 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace \
   -o run --output-format csv -- $B --steps 5 --warmup 2 || exit $?
 grep '^{' gpurun_out/prof_trace.log | tail -1 > gpurun_out/prof_trace_bench.json || exit $?
-LFM_S3_EVENTS=1 $S prof_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch \
+LFM_S3_EVENTS=2 $S prof_fetch 300 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof_fetch \
   -o run --output-format csv -- $B --steps 2 --warmup 1 --no-profile || exit $?
-LFM_S3_EVENTS=1 $S prof_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write \
+LFM_S3_EVENTS=2 $S prof_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_write \
   -o run --output-format csv -- $B --steps 2 --warmup 1 --no-profile || exit $?
 $S prof_c4 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4 \
   -o run --output-format csv -- $B --workload c4 --steps 5 --warmup 1 || exit $?
@@ -35,14 +36,14 @@ $S prof_c4_write 300 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof_c4_write \
 LFM_GRAM_FUSE=0 $S prof_unfused 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_unfused \
   -o run --output-format csv -- $B --steps 5 --warmup 2 || exit $?
 grep '^{' gpurun_out/prof_unfused.log | tail -1 > gpurun_out/prof_unfused_bench.json || exit $?
-LFM_GRAM_FUSE=0 LFM_S3_EVENTS=1 $S prof_unfused_write 300 rocprofv3 --pmc WRITE_SIZE \
+LFM_GRAM_FUSE=0 LFM_S3_EVENTS=2 $S prof_unfused_write 300 rocprofv3 --pmc WRITE_SIZE \
   -d gpurun_out/prof_unfused_write -o run --output-format csv -- $B --steps 2 --warmup 1 --no-profile || exit $?
 $S prof_c5 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 \
   -o run --output-format csv -- $B --workload c5 --steps 200 --warmup 20 || exit $?
 PMC_T=127 PMC_KD=640 PMC_CIO=88 $S mfma_unit 120 rocprofv3 --kernel-trace \
   --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES GRBM_GUI_ACTIVE -d gpurun_out/mfma_unit \
   -o run --output-format csv -- python3 scripts/pmc_syrk.py 3 || exit $?
-LFM_S3_EVENTS=1 $S mfma_bench 180 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES \
+LFM_S3_EVENTS=2 $S mfma_bench 180 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES \
   GRBM_GUI_ACTIVE -d gpurun_out/mfma_bench -o run --output-format csv -- \
   $B --steps 2 --warmup 1 --no-profile || exit $?
 $S bench_c2 300 python bench.py --steps 20 --warmup 5 || exit $?

@@ -48,19 +48,27 @@ def main():
         lines.append(f"| {short(r['Name'])} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | "
                      f"{float(r['TotalDurationNs']) / 1e6:.2f} | {float(r['Percentage']):.2f} |")
     hbm = defaultdict(lambda: {"launches": 0, "FETCH_SIZE_KiB": 0.0, "WRITE_SIZE_KiB": 0.0})
+    # per dispatch, in dispatch order: (kernel, KiB) per pass (the passes run the same launch
+    # sequence, so the i-th dispatch of one is the i-th of the other)
+    series = {}
     for counter, sub in (("FETCH_SIZE", "prof_fetch"), ("WRITE_SIZE", "prof_write")):
         path = os.path.join(OUT, sub, "run_counter_collection.csv")
         if not os.path.exists(path):
             continue
         seen = defaultdict(set)
+        per = defaultdict(float)
+        names = {}
         for r in csv.DictReader(open(path)):
             if r["Counter_Name"] != counter:
                 continue
             k = short(r["Kernel_Name"])
             hbm[k][counter + "_KiB"] += float(r["Counter_Value"])
             seen[k].add(r["Dispatch_Id"])
+            per[int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+            names[int(r["Dispatch_Id"])] = k
         for k, s in seen.items():
             hbm[k]["launches"] = max(hbm[k]["launches"], len(s))
+        series[counter] = [(names[d], per[d]) for d in sorted(per)]
     out = {}
     for k, v in hbm.items():
         n = max(1, v["launches"])
@@ -78,15 +86,28 @@ def main():
         launches = sum(v["launches"] for _, v in syrk)
         total = sum(v["hbm_bytes_per_launch"] * v["launches"] for _, v in syrk)
         # evaluations in the PMC run = finalize launches (one per MLL evaluation; the gram kernel
-        # no longer runs once per evaluation where it is fused); the PMC passes run
-        # schedule 3 event-ordered (LFM_S3_EVENTS=1), which splits the launches differently from
-        # the bench, so bench.py converts the per-evaluation bytes to its own launch count
+        # no longer runs once per evaluation where it is fused); the PMC passes run the timed
+        # schedule's own launches serialised by events (LFM_S3_EVENTS=2; round 3: the event-
+        # ordered split, LFM_S3_EVENTS=1, whose launches bench.py had to convert to its own)
         evals = max(1, out.get("finalize_kernel", {}).get("launches", 1))
-        json.dump({"round": rnd, "source": f"profiles/{rnd}_hbm.json (PMC FETCH_SIZE x2 + WRITE_SIZE)",
-                   "kernels": [k for k, _ in syrk],
-                   "hbm_bytes_per_eval": total / evals, "evals": evals,
-                   "hbm_bytes_per_launch": total / max(1, launches), "launches": launches},
-                  open(os.path.join(PROF, "syrk_traffic.json"), "w"), indent=1)
+        rec = {"round": rnd, "source": f"profiles/{rnd}_hbm.json (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+               "kernels": [k for k, _ in syrk],
+               "hbm_bytes_per_eval": total / evals, "evals": evals,
+               "hbm_bytes_per_launch": total / max(1, launches), "launches": launches}
+        # the last evaluation's step launches one by one (bytes, dispatch order): with
+        # LFM_S3_EVENTS=2 these are the timed schedule's own launches
+        fs, ws = series.get("FETCH_SIZE", []), series.get("WRITE_SIZE", [])
+        if fs and len(fs) == len(ws) and all(a[0] == b[0] for a, b in zip(fs, ws)):
+            fin = [i for i, (k, _) in enumerate(fs) if k == "finalize_kernel"]
+            lo = fin[-2] + 1 if len(fin) >= 2 else 0
+            hi = fin[-1] if fin else len(fs)
+            pre = "step_kernel" if syrk[0][0].startswith("step_kernel") else "syrk_kernel"
+            per = [1024 * (2 * f + w) for (k, f), (_, w) in zip(fs[lo:hi], ws[lo:hi])
+                   if k.startswith(pre)]
+            rec["last_eval_launch_bytes"] = per
+            rec["last_eval_bytes"] = sum(per)
+            rec["schedule"] = os.environ.get("PMC_SCHEDULE", "LFM_S3_EVENTS=2")
+        json.dump(rec, open(os.path.join(PROF, "syrk_traffic.json"), "w"), indent=1)
     # the roofline recomputed from the trace: the step kernel's rocprof average duration and the
     # traced bench line's algorithmic flops per launch (lfm_kstat.flops, the same launches)
     step = next((r for r in rows if short(r["Name"]).startswith("step_kernel")), None)

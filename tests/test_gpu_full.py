@@ -183,6 +183,32 @@ def test_mll_n16384_other_schedules_vs_golden(full, env, monkeypatch):
         ctx.close()
 
 
+@pytest.mark.parametrize("G,T", [(10, 256), (64, 256)])
+def test_serialised_schedule3_is_bit_identical(monkeypatch, G, T):
+    """LFM_S3_EVENTS=2 (the timed schedule's own launches ordered by events, the mode the PMC
+    passes count) gives the default schedule 3's MLL bit for bit: N = 2560 and the C2 size."""
+    from dis_project_amd import _lib, configs
+
+    work = configs.grid_workload("serial", G, T, seed_params=7, seed_y=8)
+    x = np.ascontiguousarray(work.data.X)
+    y = np.ascontiguousarray(work.data.y.reshape(-1))
+    hp = work.model.hyp()
+    vals = []
+    for mode in ("0", "2"):
+        monkeypatch.setenv("LFM_SCHED", "3")
+        monkeypatch.setenv("LFM_S3_EVENTS", mode)
+        ctx = _lib.Context(0)  # read when the context is created
+        try:
+            out = np.empty(1)
+            ctx.check(ctx.lib.lfm_mll_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
+                                          hp.ref, 0, _lib.dptr(out)))
+            assert ctx.fallbacks == 0
+            vals.append(out[0])
+        finally:
+            ctx.close()
+    assert vals[0] == vals[1], vals
+
+
 @pytest.mark.parametrize("G,T", [(4, 256), (64, 256)])
 def test_fused_gram_is_bit_identical(monkeypatch, G, T):
     """The gram fused into the first trailing update (the schedule-3 default on an aligned grid
