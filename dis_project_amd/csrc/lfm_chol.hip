@@ -993,12 +993,15 @@ struct Panel {
 #ifndef LFM_TR32_DEFAULT
 #define LFM_TR32_DEFAULT 0
 #endif
-// tall units claimed dynamically (1): every tall workgroup takes units from a per-launch device
-// counter in enumeration order (deepest first) until none is left, so an XCD that finishes its
-// rest units early takes the tall units a later XCD's workgroups would have run; (0) the static
-// deal above
-#ifndef LFM_TALL_DYN
-#define LFM_TALL_DYN 0
+// rest-unit stealing across XCDs (LFM_STEAL at run time, units per XCD; this is its default):
+// the last LFM_STEAL rest units of each XCD's range are claimed from per-XCD counters, and
+// LFM_STEAL_EXTRA extra workgroups per XCD claim what a later XCD has not started, so an XCD
+// that runs its units faster takes over the end of a slower one's range
+#ifndef LFM_STEAL_DEFAULT
+#define LFM_STEAL_DEFAULT 0
+#endif
+#ifndef LFM_STEAL_EXTRA_DEFAULT
+#define LFM_STEAL_EXTRA_DEFAULT 24
 #endif
 // workgroups of the tall segment: a multiple of 8 (XCDs), of 8 LFM_TALL_SPLIT when grouped
 __host__ __device__ constexpr int64_t tall_grid(int64_t nt) {
@@ -1343,8 +1346,11 @@ struct StepArgs {
                      // enumeration (the side-CU helper launch takes the tail of it)
   int sub;             // ahead / rest units per 128-row tile: 2 (64-row units, step_kernel) or 4
                       // (32-row units, step_kernel32: the w = 1 steps, LFM_TR32)
-  unsigned* tall_ctr;  // LFM_TALL_DYN: this launch's tall-unit counter (zeroed per call; NULL: the
-                      // static deal)
+  // rest-unit stealing (0: off): the last `steal` units of each XCD's rest range are claimed
+  // from steal_ctr[16 x] (zeroed per call), by its own workgroups and by `steal_extra` extra
+  // workgroups per XCD at the end of the rest segment
+  int steal, steal_extra;
+  unsigned* steal_ctr;
   unsigned long long* trace;  // diagnostics (NULL: off): 4 words per workgroup (lfm_debug_trace)
   unsigned long long trace_tag;  // launch tag, bits 40+ of each record's last word
 };
@@ -1381,6 +1387,42 @@ __device__ __forceinline__ void tall_or_xcd_range(int seg, int64_t cnt, int64_t 
   xcd_range(cnt, (int)(b % 8), &lo, &hi);
   *u = lo + b / 8;
   *end = hi;
+}
+
+// workgroups of a step launch's rest segment (a multiple of 8: one queue per XCD)
+__host__ __device__ inline int64_t rest_wgs(const StepArgs& g) {
+  return g.steal ? 8 * ((int64_t)(g.nr + 7) / 8 + g.steal_extra) : (int64_t)(g.nr + 7) / 8 * 8;
+}
+
+// Rest unit of workgroup bq of the rest segment under stealing (-1: none left). XCD x = bq % 8
+// runs its range [lo_x, hi_x) in order up to its last t_x = min(steal, hi_x - lo_x) units, which
+// are taken from counter x: first by the workgroup's own XCD, then round the ring of the others,
+// so a workgroup reaching the end of a fast XCD's queue runs a unit a slower XCD has not
+// started. Each unit is claimed once (a counter past t_x is exhausted); a claimed unit runs at
+// once and waits on nothing, so claims add no dependence to the launch's deadlock argument.
+__device__ __forceinline__ int64_t rest_claim(const StepArgs& g, int64_t bq) {
+  const int x = (int)(bq % 8);
+  const int64_t p = bq / 8;
+  int64_t lo, hi;
+  xcd_range(g.nr, x, &lo, &hi);
+  if (p < hi - lo - min((int64_t)g.steal, hi - lo)) return lo + p;
+  __shared__ int64_t su;
+  if (threadIdx.x == 0) {
+    int64_t v = -1;
+    for (int k = 0; k < 8 && v < 0; ++k) {
+      const int y = (x + k) & 7;
+      int64_t ly, hy;
+      xcd_range(g.nr, y, &ly, &hy);
+      const unsigned ty = (unsigned)min((int64_t)g.steal, hy - ly);
+      unsigned* c = g.steal_ctr + 16 * y;
+      if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ty) continue;
+      const unsigned got = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (got < ty) v = hy - (int64_t)ty + got;
+    }
+    su = v;
+  }
+  __syncthreads();
+  return su;
 }
 
 __device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
@@ -1491,8 +1533,9 @@ __device__ __forceinline__ bool tall_unit(const StepArgs& g, int64_t u, double (
   return true;
 }
 
+// ran (diagnostics, NULL: off): thread 0 records role << 32 | unit of the unit it runs
 template <int TR>
-__device__ __forceinline__ void step_body(const StepArgs& g) {
+__device__ __forceinline__ void step_body(const StepArgs& g, unsigned long long* ran = nullptr) {
   constexpr int SUB = ST / TR;  // units per 128-row tile
   __shared__ double sPbuf[(64 + ST) * (LFM_STEP_KS + LDP)];
   double (*sP)[KB + LDP] = reinterpret_cast<double (*)[KB + LDP]>(sPbuf);
@@ -1500,17 +1543,24 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
   const int64_t b = blockIdx.x;
   // roles in blockIdx order: ahead (1), rest (2), tall (3), each padded to a multiple of 8
   const int cnt[3] = {g.na, g.nr, g.nt};
+  const int64_t width[2] = {(int64_t)(g.na + 7) / 8 * 8, rest_wgs(g)};
   int seg = 0;
   int64_t base = 0;
-  while (seg < 2 && b >= base + (cnt[seg] + 7) / 8 * 8) {
-    base += (cnt[seg] + 7) / 8 * 8;
+  while (seg < 2 && b >= base + width[seg]) {
+    base += width[seg];
     ++seg;
   }
   int64_t lo, hi;
   tall_or_xcd_range(seg, cnt[seg], b - base, &lo, &hi);
+  if (seg == 1 && g.steal) {
+    lo = rest_claim(g, b - base);
+    hi = lo + 1;
+    if (lo < 0) return;
+  }
   const int64_t u = lo;
   if (u >= hi) return;
   const int role = seg + 1;
+  if (ran && threadIdx.x == 0) *ran = ((unsigned long long)role << 32) | (unsigned long long)u;
   unsigned long long* const st = g.stamps;
   if (st) stamp_max(st, true);
   // diagnostics: summed unit durations per role (rest [5], tall [6], ahead [7]; 100 MHz)
@@ -1567,18 +1617,6 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
     }
     return;
   }
-  if (LFM_TALL_DYN && g.tall_ctr) {
-    // claim units until the counter passes the last one (workgroup-uniform)
-    __shared__ int64_t su;
-    for (;;) {
-      __syncthreads();  // every thread has read the previous claim
-      if (threadIdx.x == 0)
-        su = __hip_atomic_fetch_add(g.tall_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      const int64_t v = su;
-      if (v >= g.nt || !tall_unit(g, v, sP, st, t_unit)) return;
-    }
-  }
   tall_unit(g, u, sP, st, t_unit);
 }
 
@@ -1587,17 +1625,16 @@ __device__ __forceinline__ void step_body(const StepArgs& g) {
 template <int TR>
 __device__ __forceinline__ void step_traced(const StepArgs& g) {
   __shared__ unsigned long long t0;  // in LDS: nothing held in registers across the body
-  if (threadIdx.x == 0) t0 = __builtin_amdgcn_s_memrealtime();
-  step_body<TR>(g);
+  __shared__ unsigned long long ran;  // role << 32 | unit (0: padding, or nothing left to claim)
+  if (threadIdx.x == 0) {
+    t0 = __builtin_amdgcn_s_memrealtime();
+    ran = 0;
+  }
+  __syncthreads();
+  step_body<TR>(g, &ran);
   __syncthreads();
   if (threadIdx.x == 0) {
     const int64_t b = blockIdx.x;
-    const int64_t pa = (g.na + 7) / 8 * 8, pr = (g.nr + 7) / 8 * 8;
-    const int seg = b < pa ? 0 : b < pa + pr ? 1 : 2;
-    const int64_t base = seg == 0 ? 0 : seg == 1 ? pa : pa + pr;
-    int64_t lo, hi;
-    tall_or_xcd_range(seg, seg == 0 ? g.na : seg == 1 ? g.nr : g.nt, b - base, &lo, &hi);
-    const int64_t u = lo;
     unsigned hw, xcc;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
@@ -1605,8 +1642,7 @@ __device__ __forceinline__ void step_traced(const StepArgs& g) {
     r[0] = t0;
     r[1] = __builtin_amdgcn_s_memrealtime();
     r[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
-    r[3] = (g.trace_tag << 40) | ((unsigned long long)(u < hi ? seg + 1 : 0) << 32) |
-           (unsigned long long)(u < hi ? u : 0);
+    r[3] = (g.trace_tag << 40) | ran;
   }
 }
 
@@ -2459,8 +2495,9 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     if (!r)
       r = ensure(ctx, (void**)&ctx->linv_full, &ctx->linv_full_bytes, (size_t)NB * NB * sizeof(double));
     if (!r) r = ensure(ctx, (void**)&ctx->xd, &ctx->xd_bytes, (size_t)Wmax * Wmax * sizeof(double));
-    // + one tall-unit counter per step launch (LFM_TALL_DYN; event-ordered: two launches a step)
-    const size_t nflags = (size_t)S * (3 + Tmax) + 2 * (size_t)S + 2;
+    // + 8 rest-steal counters (64-B apart) per step launch (LFM_STEAL; event-ordered: two
+    // launches a step)
+    const size_t nflags = (size_t)S * (3 + Tmax) + 128 * (2 * (size_t)S + 2);
     if (!r) r = ensure(ctx, (void**)&ctx->flags, &ctx->flags_bytes, nflags * sizeof(unsigned));
     if (r) return r;
     unsigned* chain_done = ctx->flags;     // [S]
@@ -2470,8 +2507,13 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     auto xbuf = [&](int s) { return ctx->xbuf + (size_t)(s & 1) * Mp * Wmax; };
     unsigned* bars = a_done + (size_t)S * Tmax;  // [S] grid barrier counters of chain(s)
     unsigned* xready = bars + S;                  // [S] inputs of chain(s) landed (s >= 1)
-    unsigned* tall_ctrs = xready + S;             // [2 S + 2] LFM_TALL_DYN claim counters
-    int ntall_launch = 0;
+    unsigned* steal_ctrs = xready + S;            // [2 S + 2][128] LFM_STEAL claim counters
+    int nsteal_launch = 0;
+    // rest-unit stealing (read per call): tail units per XCD, extra workgroups per XCD; only
+    // where each XCD's range is at least four tails long
+    const int steal = (int)std::max<int64_t>(0, env_int("LFM_STEAL", LFM_STEAL_DEFAULT));
+    const int steal_extra =
+        (int)std::max<int64_t>(0, env_int("LFM_STEAL_EXTRA", LFM_STEAL_EXTRA_DEFAULT));
     auto wkbuf = [&](int s) { return ctx->wk + (size_t)(s & 1) * 2 * Wmax * Wmax; };
     // launch j = s - 2 (step j's update) writes the inputs of chain(s), s >= 2: the block's
     // tiles (leading rest units, w_s (w_s + 1) slabs) and its rows of the columns of super-
@@ -2540,9 +2582,13 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       if (!g.copy_from) g.copy_from = INT64_MAX;
       g.spin = ctx->wait_ticks;
       if (!g.sub) g.sub = 2;
-      g.tall_ctr = LFM_TALL_DYN && g.nt > 0 ? tall_ctrs + ntall_launch++ : nullptr;
-      const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 + (int64_t)(g.nr + 7) / 8 * 8 +
-                           tall_grid(g.nt);
+      g.steal = 0;
+      if (steal > 0 && g.nr / 8 >= 4 * steal && nsteal_launch < 2 * S + 2) {
+        g.steal = steal;
+        g.steal_extra = steal_extra;
+        g.steal_ctr = steal_ctrs + 128 * (size_t)nsteal_launch++;
+      }
+      const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 + rest_wgs(g) + tall_grid(g.nt);
       if (grid == 0) return;
       // issued: every 64 x 128 unit in full (padding rows included), tall units as GEMMs with
       // the triangular inverse; algorithmic: the update of the unpadded augmented trailing
@@ -2734,6 +2780,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
           h.rest_off = total - hu;
           h.nr = (int)hu;
           h.stamps = nullptr;
+          h.steal = 0;
           h.xready = nullptr;  // tail units: never the lead tiles
           trace_launch(ctx, h, (hu + 7) / 8 * 8, true);
           // X_s and step s's C input: launch s - 1 complete

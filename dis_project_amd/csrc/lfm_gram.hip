@@ -160,12 +160,7 @@ __global__ __launch_bounds__(256) void gram_grid_kernel(
 // gene k) block. The tile's Toeplitz windows of Wt/Xt (d = tau' - tau spans 319 values)
 // and its row tables are staged in LDS once; each element then costs 4 conflict-free LDS
 // reads (consecutive d across lanes), 3 wave-uniform ones and one coalesced store.
-// V16: 16-B stores (needs out 16-B aligned and ldo a multiple of 16 / sizeof(T): launch_gram_grid
-// checks); LFM_GRAM_V16 (compile time) selects it where it applies
-#ifndef LFM_GRAM_V16
-#define LFM_GRAM_V16 0
-#endif
-template <typename T, bool V16>
+template <typename T>
 __global__ __launch_bounds__(256) void gram_grid_aligned_kernel(
     const T* __restrict__ tab, int G, int Tn, const int* __restrict__ bg, int64_t n, T da1, T da2,
     int lower, T* __restrict__ out, int64_t ldo) {
@@ -216,56 +211,6 @@ __global__ __launch_bounds__(256) void gram_grid_aligned_kernel(
   const T Pj = Pt[(int64_t)j * Tn + tp];
   const T Cjk = Cm[(int64_t)j * G + k];
   __syncthreads();
-if constexpr (V16) {
-  // 16-B stores (LFM_GRAM_V16): a lane forms V = 16 / sizeof(T) consecutive columns of a row and
-  // stores them at once, a wave a whole 256-column tile row (fp32) or half of one (fp64) per
-  // store instruction; the same operations per element (bit-identical). A vector straddling
-  // the diagonal is stored element by element (nothing is written above it).
-  constexpr int V = 16 / sizeof(T), LPR = C / V, RG = 256 / LPR, RPT = R / RG;
-  __syncthreads();
-  const int cl = (tid % LPR) * V, rg = tid / LPR;
-  T pj[V], ek[V], qk[V];
-#pragma unroll
-  for (int q = 0; q < V; ++q) {
-    pj[q] = Pt[(int64_t)j * Tn + tp0 + cl + q];
-    ek[q] = Et[(int64_t)k * Tn + tp0 + cl + q];
-    qk[q] = Qt[(int64_t)k * Tn + tp0 + cl + q];
-  }
-  (void)Ek;
-  (void)Qk;
-  (void)Pj;
-#pragma unroll 2
-  for (int ii = 0; ii < RPT; ++ii) {
-    const int i = rg * RPT + ii;
-    const int64_t row = r0 + i;
-    const int64_t c = c0 + cl;
-    if (lower && c > row) continue;
-    T v[V];
-#pragma unroll
-    for (int q = 0; q < V; ++q) {
-      const int e = cl + q + (R - 1) - i;
-      T a = sWk[e] + sWj[e];
-      a = fma(-sXk[e], sPk[i], a);
-      a = fma(-sXj[e], pj[q], a);
-      a = fma(-(ek[q] * sEj[i]), qk[q] + sQj[i], a);
-      a = Cjk * a;
-      if (row == c + q) a = (a + da1) + da2;
-      v[q] = a;
-    }
-    T* op = out + row * ldo + c;
-    if (!lower || c + V - 1 <= row) {
-      if constexpr (V == 4) {
-        *reinterpret_cast<float4*>(op) = make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        *reinterpret_cast<double2*>(op) = make_double2(v[0], v[1]);
-      }
-    } else {
-#pragma unroll
-      for (int q = 0; q < V; ++q)
-        if (c + q <= row) op[q] = v[q];
-    }
-  }
-  } else {
   const int64_t c = c0 + tid;
   T* op = out + r0 * ldo + c;
 #pragma unroll 4
@@ -280,7 +225,6 @@ if constexpr (V16) {
     v = Cjk * v;
     if (row == c) v = (v + da1) + da2;
     op[(int64_t)i * ldo] = v;
-  }
   }
 }
 
@@ -314,14 +258,8 @@ int launch_gram_grid(lfm_ctx* ctx, const HypDev& h, const GridLayout& lay, const
     // lower: only the lower tiles are launched (2 Q (Q + 1) of them, Q = n / 256)
     const int64_t Q = n / 256;
     dim3 grid = lower ? dim3((unsigned)(2 * Q * (Q + 1))) : dim3((unsigned)(n / 256), (unsigned)(n / 64));
-    const bool v16 = LFM_GRAM_V16 && (uintptr_t)out % 16 == 0 &&
-                     ldo % (int64_t)(16 / sizeof(OutT)) == 0;
-    if (v16)
-      hipLaunchKernelGGL((gram_grid_aligned_kernel<OutT, true>), grid, dim3(256), 0, ctx->stream,
-                         tabT, h.G, lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out, ldo);
-    else
-      hipLaunchKernelGGL((gram_grid_aligned_kernel<OutT, false>), grid, dim3(256), 0, ctx->stream,
-                         tabT, h.G, lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out, ldo);
+    hipLaunchKernelGGL((gram_grid_aligned_kernel<OutT>), grid, dim3(256), 0, ctx->stream, tabT,
+                       h.G, lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out, ldo);
   } else {
     dim3 grid((unsigned)((n + 255) / 256), (unsigned)((n + GR - 1) / GR));
     hipLaunchKernelGGL((gram_grid_kernel<OutT, GR>), grid, dim3(256), 0, ctx->stream, tabT, h.G,

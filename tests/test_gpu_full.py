@@ -209,6 +209,44 @@ def test_serialised_schedule3_is_bit_identical(monkeypatch, G, T):
     assert vals[0] == vals[1], vals
 
 
+@pytest.mark.parametrize("G,T,steal,extra", [(10, 256, 8, 4), (16, 256, 24, 24),
+                                             (64, 256, 112, 24), (64, 256, 56, 64)])
+def test_rest_stealing_is_bit_identical(monkeypatch, G, T, steal, extra):
+    """Rest units claimed across XCDs (LFM_STEAL / LFM_STEAL_EXTRA, read per call) run the same
+    units with the same arithmetic: the MLL equals the static deal's bit for bit and the
+    gradient's bordered factorisation agrees to 1e-12 (its reductions are order-dependent);
+    no call falls back to schedule 1."""
+    from dis_project_amd import _lib, configs
+
+    monkeypatch.setenv("LFM_SCHED", "3")
+    work = configs.grid_workload("steal", G, T, seed_params=9, seed_y=10)
+    x = np.ascontiguousarray(work.data.X)
+    y = np.ascontiguousarray(work.data.y.reshape(-1))
+    hp = work.model.hyp()
+    ng = 3 * work.model.num_genes + 2
+    ctx = _lib.Context(0)
+    try:
+        vals, grads = [], []
+        for on in (False, True):
+            monkeypatch.setenv("LFM_STEAL", str(steal) if on else "0")
+            monkeypatch.setenv("LFM_STEAL_EXTRA", str(extra))
+            out, gv = np.empty(1), np.empty(ng)
+            ctx.check(ctx.lib.lfm_mll_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
+                                          hp.ref, 0, _lib.dptr(out)))
+            vals.append(out[0])
+            if G <= 16:
+                ctx.check(ctx.lib.lfm_mll_grad_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y),
+                                                   x.shape[0], hp.ref, 1, _lib.dptr(out),
+                                                   _lib.dptr(gv)))
+                grads.append(gv.copy())
+        assert vals[0] == vals[1], vals
+        if grads:  # the gradient's reductions sum in arrival order: equal to 1e-12
+            assert np.max(np.abs(grads[1] - grads[0])) <= 1e-12 * np.max(np.abs(grads[0]))
+        assert ctx.fallbacks == 0
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("G,T", [(4, 256), (64, 256)])
 def test_fused_gram_is_bit_identical(monkeypatch, G, T):
     """The gram fused into the first trailing update (the schedule-3 default on an aligned grid
