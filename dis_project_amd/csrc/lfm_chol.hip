@@ -2852,19 +2852,112 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
 // One workgroup per problem: Sigma (+ residual row) built and factored in LDS.
 // Used for n <= SMALL_MAX (configs 1 and 5: N = 35, 28).
 
+// Factor of the augmented (n + 1)-row matrix on one wave (small_mll_kernel, n + 1 <= 64): lane
+// r holds row r (row n: the residual) in registers as a window d[q] = A[r][c + q] over the
+// columns from the current one c on, right-looking. Column c: every lane scales its entry into
+// L[r][c] and puts it in colbuf[r] (LDS); every lane then reads L[c + q][c] back (all reads
+// issued at once) and updates and shifts its window in one step, d[q - 1] = d[q] - L[r][c]
+// L[c + q][c]. The pivot of column c + 1 is lane c + 1's new d[0], which that lane forms from
+// its own L[c + 1][c] without the LDS round trip, so its reciprocal square root (v_rsq_f64 and
+// one Newton step, as the large factor's leaf) is issued alongside column c's update. The
+// window halves once no more than half of it is live (W = 32 or 64, then 16, 8), so a column
+// costs about as many fused multiply-adds as it has live entries; the column loops stay rolled
+// (fully unrolled, the straight-line code was instruction-fetch bound). Per element the terms
+// are summed in the same order (k = 0, 1, ...) as before. colbuf: >= 128 doubles, zero from
+// index 64 on. Lane r ends with its pivot (r < n) and residual entry z[r] = L[n][r].
+struct SmallFactor {
+  int n, r;
+  bool act;
+  double* colbuf;
+  double dc, y;      // the current column's pivot input and 1 / sqrt of it
+  double mp, mz;     // this lane's pivot and z entry
+  int bad;
+};
+template <int W>
+__device__ __forceinline__ void small_factor_phase(double (&d)[W], int c, SmallFactor& f) {
+  // phase W: the columns while more than W / 2 of them remain (the last phase: all)
+  const int cend = W > 8 ? max(c, f.n - W / 2) : f.n;
+#pragma unroll 1
+  for (; c < cend; ++c) {
+    if (!(f.dc > 0.0) && f.bad == 0) f.bad = c + 1;
+    const double lc = f.r == c ? f.dc * f.y : d[0] * f.y;  // L[r][c]; lane c: the pivot
+    if (f.r == c) f.mp = lc;
+    const double zc = rdl(lc, f.n);  // L[n][c] = z[c]
+    if (f.r == c) f.mz = zc;
+    // the next pivot: lane c + 1's d[1] - L[c + 1][c]^2 (past the last column: unused)
+    const double dn = rdl(fma(-lc, lc, d[1]), c + 1);
+    const double yn = rsqrt_1nr(dn);
+    f.colbuf[f.r] = (f.act && f.r > c) ? lc : 0.0;
+    // the wave's LDS operations complete in order: the reads see every lane's store
+    asm volatile("" ::: "memory");
+    double col[W - 1];
+#pragma unroll
+    for (int q = 1; q < W; ++q) col[q - 1] = f.colbuf[c + q];
+    asm volatile("" ::: "memory");  // every read issued before the first use
+#pragma unroll
+    for (int q = 1; q < W; ++q) d[q - 1] = fma(-lc, col[q - 1], d[q]);
+    d[W - 1] = 0.0;
+    f.dc = dn;
+    f.y = yn;
+  }
+  if constexpr (W > 8)
+    if (c < f.n) small_factor_phase<W / 2>(*reinterpret_cast<double(*)[W / 2]>(&d[0]), c, f);
+}
+template <int MR>
+__device__ __forceinline__ void small_factor_regs(const double* __restrict__ sm, int ld, int n,
+                                                  int M, double* colbuf, double* piv_r,
+                                                  double* z_r, int* bad_out) {
+  SmallFactor f;
+  f.n = n;
+  f.r = threadIdx.x;  // wave 0
+  f.act = f.r < M;
+  f.colbuf = colbuf;
+  double d[MR];
+#pragma unroll
+  for (int q = 0; q < MR; ++q) d[q] = (f.act && q <= f.r && q < n) ? sm[f.r * ld + q] : 0.0;
+  f.dc = rdl(d[0], 0);
+  f.y = rsqrt_1nr(f.dc);
+  f.mp = f.mz = 0.0;
+  f.bad = 0;
+  small_factor_phase<MR>(d, 0, f);
+  *piv_r = f.mp;
+  *z_r = f.mz;
+  *bad_out = f.bad;
+}
+
+// timing experiment (make EXTRA=-DLFM_SMALL_SKIP=k; results invalid, never in the product
+// build): 1 no factor, 2 no gram pairs, 3 neither, 4 no pinned reads (constant hyperparameters)
+#ifndef LFM_SMALL_SKIP
+#define LFM_SMALL_SKIP 0
+#endif
+// timing experiment (make EXTRA=-DLFM_SMALL_STAMPS=1; results of problems 1-4 invalid): block 0
+// writes its phase times (µs from its start) into out[1..4]
+#ifndef LFM_SMALL_STAMPS
+#define LFM_SMALL_STAMPS 0
+#endif
 __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restrict__ probs,
                                                         int negative, double* __restrict__ out,
                                                         int* __restrict__ status, int tabs) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
+  const unsigned long long st0 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
   const SmallProb P = probs[blockIdx.x];
   const int n = P.n, M = n + 1, ld = n + 2, G = P.G;
   const int tid = threadIdx.x;
   double* red = sm + (size_t)M * ld;  // [8] reduction scratch + [1] flag
   // hyperparameters staged in LDS (they may live in pinned host memory: read once)
   double* hyp = red + 16;             // D S B (3G), l, obs_stddev, jitter
-  for (int i = tid; i < 3 * G; i += 256) hyp[i] = P.dsb[i];
-  if (tid < 3) hyp[3 * G + tid] = P.sc[tid];
+  // past the hyperparameters and the tables: the one-wave factor's column buffer (128), then
+  // x (3n) and y (n), loaded here beside the hyperparameters so that no later phase waits on
+  // HBM (the launch's LDS counts them)
+  double* colbuf = hyp + 3 * G + 3 + (tabs ? 3 * G + n + n * G : 0);
+  double* xs = colbuf + 128;
+  double* ys = xs + 3 * n;
+  for (int i = tid; i < 3 * G; i += 256) hyp[i] = LFM_SMALL_SKIP == 4 ? 0.5 : P.dsb[i];
+  if (tid < 3) hyp[3 * G + tid] = LFM_SMALL_SKIP == 4 ? (tid == 0 ? 2.5 : 1.0) : P.sc[tid];
+  for (int i = tid; i < 3 * n; i += 256) xs[i] = P.x[i];
+  for (int i = tid; i < n; i += 256) ys[i] = P.y[i];
   __syncthreads();
+  const unsigned long long st1 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
   const HypDev h{hyp, hyp + G, hyp + 2 * G, G, hyp[3 * G]};
   const double jitter = hyp[3 * G + 2], sd = hyp[3 * G + 1];
   const double noise = sd * sd;  // objectives.py:66
@@ -2877,17 +2970,19 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
     double* e2 = erg + G;
     double* e1 = e2 + n;
     const KxxTab t{gam, egg, erg, e1, e2, G};
-    small_tables(h, P.x, n, t, gam, egg, erg, e1, e2);
+    small_tables(h, xs, n, t, gam, egg, erg, e1, e2);
     const int np = n * (n + 1) / 2;  // the lower triangle, row by row
     for (int q = tid; q < np; q += 256) {
       int i = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
       while (i * (i + 1) / 2 > q) --i;
       while ((i + 1) * (i + 2) / 2 <= q) ++i;
       const int c = q - i * (i + 1) / 2;
-      const double* xa = P.x + 3 * i;
-      const double* xb = P.x + 3 * c;
+      const double* xa = xs + 3 * i;
+      const double* xb = xs + 3 * c;
       double v;
-      if (flag_int(xa[2]) == 1 && flag_int(xb[2]) == 1)
+      if (LFM_SMALL_SKIP == 2 || LFM_SMALL_SKIP == 3)
+        v = i == c ? 4.0 : 0.01;
+      else if (flag_int(xa[2]) == 1 && flag_int(xb[2]) == 1)
         v = kxx_tab(h, t, xa[0], gene_index(xa[1], G), i, xb[0], gene_index(xb[1], G), c);
       else
         v = kernel_ref(h, xa[0], xa[1], xa[2], xb[0], xb[1], xb[2]);
@@ -2898,8 +2993,8 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
     for (int idx = tid; idx < n * n; idx += 256) {
       const int i = idx / n, c = idx - i * n;
       if (c <= i) {
-        const double* xa = P.x + 3 * i;
-        const double* xb = P.x + 3 * c;
+        const double* xa = xs + 3 * i;
+        const double* xb = xs + 3 * c;
         double v = kernel_ref(h, xa[0], xa[1], xa[2], xb[0], xb[1], xb[2]);
         if (i == c) v = (v + jitter) + noise;
         sm[i * ld + c] = v;
@@ -2907,41 +3002,31 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
     }
   }
   const int64_t bs = n / G;
-  for (int c = tid; c < n; c += 256) sm[n * ld + c] = P.y[c] - mean_at(h, P.x, c, bs);
+  for (int c = tid; c < n; c += 256) sm[n * ld + c] = ys[c] - mean_at(h, xs, c, bs);
   if (tid == 0) red[8] = 0.0;
   __syncthreads();
+  const unsigned long long st2 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
   if (M <= 64) {
-    // One wave factors the augmented (n + 1)-row matrix, lane = row, left-looking: column c's
-    // entries are s_r = A[r][c] - sum_{k<c} L[r][k] L[c][k] (the terms in the same order as
-    // the right-looking sweep below, k = 0, 1, ...), the pivot is lane c's s, read by every
-    // lane. No workgroup barrier: the wave's LDS operations complete in order. 256-thread
-    // barriers were ~60 % of the kernel at n = 28 (two per column).
+    // one wave, the augmented matrix in registers (small_factor_regs); no workgroup barrier
+    // (256-thread barriers were ~60 % of the kernel at n = 28, two per column)
     if (tid >= 64) return;
     const int r = tid;
-    const bool act = r < M;
-    int bad = 0;
-    for (int c = 0; c < n; ++c) {
-      double s = 0.0;
-      if (act && r >= c) {
-        s = sm[r * ld + c];
-        const double* Lr = sm + r * ld;
-        const double* Lc = sm + c * ld;
-#pragma unroll 4
-        for (int k = 0; k < c; ++k) s -= Lr[k] * Lc[k];
-      }
-      const double d = rdl(s, c);
-      const double piv = sqrt(d);
-      const double inv = 1.0 / piv;
-      if (!(d > 0.0) && bad == 0) bad = c + 1;
-      if (act && r > c) sm[r * ld + c] = s * inv;
-      if (r == c) sm[c * ld + c] = piv;
-      wave_lds_fence();
-    }
+    double pr, zr;
+    int bad;
+    colbuf[64 + r] = 0.0;
+    if (LFM_SMALL_SKIP == 1 || LFM_SMALL_SKIP == 3) {
+      pr = sm[r * ld + r];
+      zr = sm[n * ld + r];
+      bad = 0;
+    } else if (M <= 32)
+      small_factor_regs<32>(sm, ld, n, M, colbuf, &pr, &zr, &bad);
+    else
+      small_factor_regs<64>(sm, ld, n, M, colbuf, &pr, &zr, &bad);
+    const unsigned long long st3 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
     double ldp = 0.0, qp = 0.0;
     if (r < n) {
-      ldp = log(sm[r * ld + r]);
-      const double z = sm[n * ld + r];
-      qp = z * z;
+      ldp = log(pr);
+      qp = zr * zr;
     }
     for (int o = 32; o > 0; o >>= 1) {
       ldp += __shfl_xor(ldp, o);
@@ -2952,7 +3037,14 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
       double mll = -0.5 * ((double)n * log(two_pi) + 2.0 * ldp + qp);
       mll *= negative ? -1.0 : 1.0;
       if (bad) mll = __builtin_nan("");
-      out[blockIdx.x] = mll;
+      if (LFM_SMALL_STAMPS && blockIdx.x == 0) {
+        const unsigned long long st4 = __builtin_amdgcn_s_memrealtime();
+        out[1] = (double)(st1 - st0) * 0.01;
+        out[2] = (double)(st2 - st0) * 0.01;
+        out[3] = (double)(st3 - st0) * 0.01;
+        out[4] = (double)(st4 - st0) * 0.01;
+      }
+      if (!LFM_SMALL_STAMPS || blockIdx.x == 0 || blockIdx.x > 4) out[blockIdx.x] = mll;
       if (status) status[blockIdx.x] = bad;
     }
     return;
@@ -3010,8 +3102,9 @@ int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int ma
   // tables (KxxTab) when every problem has n + 1 <= 64 rows: 3 G + n + n G doubles
   const int tabs = maxn + 1 <= 64;
   const size_t tab = tabs ? 3 * (size_t)maxg + maxn + (size_t)maxn * maxg : 0;
-  const size_t lds =
-      ((size_t)(maxn + 1) * (maxn + 2) + 16 + 3 * (size_t)maxg + 3 + tab) * sizeof(double);
+  // + 128: the one-wave factor's column buffer (small_factor_regs); + 4 n: x and y
+  const size_t lds = ((size_t)(maxn + 1) * (maxn + 2) + 16 + 3 * (size_t)maxg + 3 + tab + 128 +
+                      4 * (size_t)maxn) * sizeof(double);
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&small_mll_kernel),
