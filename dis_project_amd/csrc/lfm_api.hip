@@ -14,6 +14,7 @@
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <ctime>
 #include <memory>
@@ -1255,7 +1256,9 @@ int lfm_batch_hyp_size(const lfm_batch* batch, int64_t* out) {
 int lfm_batch_destroy(lfm_batch* batch) {
   if (!batch) return LFM_OK;
   hipSetDevice(batch->device);
-  // every evaluation ended synchronised: nothing of the batch is in flight
+  // an evaluation returns once its status words land, possibly before its kernel has retired:
+  // drain the device before the buffers go
+  hipDeviceSynchronize();
   hipFree(batch->dmem);
   hipHostFree(batch->hbuf);
   delete batch;
@@ -1272,11 +1275,31 @@ int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int neg
   double* hres = batch->hbuf + batch->nhyp;
   int* hst = reinterpret_cast<int*>(hres + np);
   std::memcpy(batch->hbuf, hyp, (size_t)batch->nhyp * 8);
+  for (int64_t q = 0; q < np; ++q) hst[q] = -1;  // a problem's status word is written last
   int r = launch_small_batch(ctx, batch->dprobs, (int)np, batch->maxn, batch->maxg, negative,
                              hres, hst);
   if (r) return r;
-  r = finish(ctx);
-  if (r) return r;
+  // Completion: every workgroup writes its result, a system-scope fence, then its status word
+  // (>= 0) into this pinned buffer, after it has read the hyperparameters, so the results are
+  // complete and the buffer free once no status word is -1: the host spins on them (~µs sooner
+  // than the kernel's end-of-dispatch signal behind hipStreamSynchronize). Past 20 ms, or when
+  // profiling (the events want the stream), it synchronises the stream instead, which also
+  // surfaces a kernel fault.
+  bool landed = false;
+  if (!ctx->prof) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      landed = true;
+      for (int64_t q = 0; q < np && landed; ++q)
+        landed = __atomic_load_n(&hst[q], __ATOMIC_ACQUIRE) != -1;
+      if (landed || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+      __builtin_ia32_pause();
+    }
+  }
+  if (!landed) {
+    r = finish(ctx);
+    if (r) return r;
+  }
   int worst = LFM_OK;
   for (int64_t q = 0; q < np; ++q) {
     out[q] = hres[q];

@@ -3045,6 +3045,9 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
         out[4] = (double)(st4 - st0) * 0.01;
       }
       if (!LFM_SMALL_STAMPS || blockIdx.x == 0 || blockIdx.x > 4) out[blockIdx.x] = mll;
+      // the status word lands after the result: the host may take it as the problem's
+      // completion (lfm_batch_mll_f64)
+      __threadfence_system();
       if (status) status[blockIdx.x] = bad;
     }
     return;
@@ -3093,6 +3096,7 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
       st = (int)red[8];  // 1-based failing pivot
     }
     out[blockIdx.x] = mll;
+    __threadfence_system();  // the result before the status word (lfm_batch_mll_f64)
     if (status) status[blockIdx.x] = st;
   }
 }
