@@ -175,7 +175,10 @@ int lfm_batch_hyp_size(const lfm_batch* batch, int64_t* out);
 /* Every problem's MLL (constant -1 if negative) in ONE launch, one workgroup per problem.
  * hyp packed: first, for each problem in order, true_d[G_p] true_s[G_p] true_b[G_p]; then, for
  * each problem in order, l, obs_stddev, jitter. out[p] per problem (NaN where not PD, with
- * status[p] = LFM_E_NOT_PD; status may be NULL); returns LFM_E_NOT_PD if any problem was. */
+ * status[p] = LFM_E_NOT_PD; status may be NULL); returns LFM_E_NOT_PD if any problem was.
+ * Returns once every problem's result has landed in host memory (the kernel may still be
+ * retiring: later work on the ctx's stream is ordered after it, and lfm_batch_destroy drains
+ * the device before it frees). */
 int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative,
                       double* out, int* status);
 
