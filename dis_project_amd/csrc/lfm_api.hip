@@ -437,6 +437,27 @@ int check_mean_shape(lfm_ctx* ctx, int64_t n, const lfm_hyp* hyp) {
 }
 
 // small-N batch through one launch; probs already validated
+}  // namespace
+
+namespace lfm {
+int64_t small_grid_pack(const double* x, int64_t n, int64_t G, SmallProb& sp, double* hd,
+                        const double* dd) {
+  sp.T = 0;
+  const GridLayout lay = detect_grid(x, n, G);
+  if (!lay.ok || tables_doubles((int)G, lay.T) > (size_t)SMALL_GRID_TAB_MAX) return 0;
+  const int64_t T = lay.T, nblk = lay.nblk;
+  std::memcpy(hd, lay.times.data(), T * 8);
+  std::memcpy(hd + T, lay.block_gene.data(), nblk * sizeof(int));
+  sp.T = (int)T;
+  sp.dt = lay.dt;
+  sp.times = dd;
+  sp.bg = reinterpret_cast<const int*>(dd + T);
+  return T + (nblk + 1) / 2;
+}
+}  // namespace lfm
+
+namespace {
+
 int small_batch(lfm_ctx* ctx, int64_t np, const lfm_problem* probs, const int64_t* idx,
                 int negative, double* out, int* status) {
   // packed device buffer: per problem x(3n) y(n) D S B (3G) l obs_stddev jitter (3) doubles;
@@ -445,10 +466,11 @@ int small_batch(lfm_ctx* ctx, int64_t np, const lfm_problem* probs, const int64_
   int maxn = 1, maxg = 1;
   for (int64_t q = 0; q < np; ++q) {
     const lfm_problem& p = probs[idx[q]];
-    nd += 4 * (size_t)p.n + 3 * (size_t)p.hyp.num_genes + 3;
+    nd += 4 * (size_t)p.n + 3 * (size_t)p.hyp.num_genes + 3 + small_grid_doubles(p.n);
     maxn = std::max<int>(maxn, (int)p.n);
     maxg = std::max<int>(maxg, (int)p.hyp.num_genes);
   }
+  int gridtab = 0;
   const size_t bytes_d = nd * 8;
   const size_t bytes_p = (size_t)np * sizeof(SmallProb);
   const size_t bytes_o = (size_t)np * (8 + 4);
@@ -485,6 +507,8 @@ int small_batch(lfm_ctx* ctx, int64_t np, const lfm_problem* probs, const int64_
     off += 3;
     sp.n = (int)n;
     sp.G = (int)G;
+    off += small_grid_pack(p.x, n, G, sp, hd + off, dd + off);
+    if (sp.T) gridtab = std::max<int>(gridtab, (int)tables_doubles((int)G, sp.T));
     hp[q] = sp;
   }
   const size_t up = round_up(bytes_d, 16) + bytes_p;
@@ -493,7 +517,7 @@ int small_batch(lfm_ctx* ctx, int64_t np, const lfm_problem* probs, const int64_
   double* d_out = reinterpret_cast<double*>(db + round_up(bytes_d, 16) + round_up(bytes_p, 16));
   int* d_st = reinterpret_cast<int*>(d_out + np);
   r = launch_small_batch(ctx, reinterpret_cast<const SmallProb*>(db + round_up(bytes_d, 16)),
-                         (int)np, maxn, maxg, negative, d_out, d_st);
+                         (int)np, maxn, maxg, gridtab, negative, d_out, d_st);
   if (r) return r;
   double* h_out = reinterpret_cast<double*>(hb + round_up(bytes_d, 16) + round_up(bytes_p, 16));
   e = hipMemcpyAsync(h_out, d_out, np * 12, hipMemcpyDeviceToHost, ctx->stream);
@@ -1168,8 +1192,9 @@ int lfm_mll_batch_f64(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, int
 struct lfm_batch {
   int device = 0;
   int64_t nprob = 0, nhyp = 0;
-  int maxn = 1, maxg = 1;
-  char* dmem = nullptr;     // device: x / y of every problem, then the SmallProb table
+  int maxn = 1, maxg = 1, gridtab = 0;
+  char* dmem = nullptr;     // device: x / y (+ grid times / block genes) of every problem, then
+                            // the SmallProb table
   SmallProb* dprobs = nullptr;
   double* hbuf = nullptr;   // pinned host: hyp [nhyp] | out [nprob] | status [nprob] (int)
 };
@@ -1191,7 +1216,7 @@ int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_
       return set_err(ctx, LFM_E_ARG, "lfm_batch: num_genes must be in [1, n]");
     r = check_mean_shape(ctx, p.n, &p.hyp);
     if (r) return r;
-    nd += 4 * p.n;
+    nd += 4 * p.n + small_grid_doubles(p.n);
     nhyp += 3 * p.hyp.num_genes + 3;
     maxn = std::max<int>(maxn, (int)p.n);
     maxg = std::max<int>(maxg, (int)p.hyp.num_genes);
@@ -1233,6 +1258,8 @@ int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_
     hs += 3;
     sp.n = (int)n;
     sp.G = (int)G;
+    off += small_grid_pack(p.x, n, G, sp, &hd[off], dd + off);
+    if (sp.T) b->gridtab = std::max<int>(b->gridtab, (int)tables_doubles((int)G, sp.T));
   }
   e = hipMemcpyAsync(b->dmem, hd.data(), (size_t)nd * 8, hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess)
@@ -1276,8 +1303,8 @@ int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int neg
   int* hst = reinterpret_cast<int*>(hres + np);
   std::memcpy(batch->hbuf, hyp, (size_t)batch->nhyp * 8);
   for (int64_t q = 0; q < np; ++q) hst[q] = -1;  // a problem's status word is written last
-  int r = launch_small_batch(ctx, batch->dprobs, (int)np, batch->maxn, batch->maxg, negative,
-                             hres, hst);
+  int r = launch_small_batch(ctx, batch->dprobs, (int)np, batch->maxn, batch->maxg,
+                             batch->gridtab, negative, hres, hst);
   if (r) return r;
   // Completion: every workgroup writes its result, a system-scope fence, then its status word
   // (>= 0) into this pinned buffer, after it has read the hyperparameters, so the results are

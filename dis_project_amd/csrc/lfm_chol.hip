@@ -2961,7 +2961,38 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
   const HypDev h{hyp, hyp + G, hyp + 2 * G, G, hyp[3 * G]};
   const double jitter = hyp[3 * G + 2], sd = hyp[3 * G + 1];
   const double noise = sd * sd;  // objectives.py:66
-  if (tabs) {
+  if (P.T > 0) {
+    // grid layout: the per-gene tables of lfm_gram.hip (tables_kernel) in LDS, then each lower
+    // element with gram_grid_kernel's operations (~10 FMAs instead of 2 erf + 3 exp)
+    double* gt = ys + n;
+    const int T = P.T, W = 2 * T - 1;
+    const int nt = (int)(2 * (int64_t)G * W + 3 * (int64_t)G * T + (int64_t)G * G);
+    for (int q = tid; q < nt; q += 256) gt[q] = grid_table_entry(h, T, P.dt, P.times, q);
+    __syncthreads();
+    const double* Wt = gt;
+    const double* Xt = Wt + G * W;
+    const double* Pt = Xt + G * W;
+    const double* Et = Pt + G * T;
+    const double* Qt = Et + G * T;
+    const double* Cm = Qt + G * T;
+    const int np = n * (n + 1) / 2;  // the lower triangle, row by row
+    for (int q = tid; q < np; q += 256) {
+      int i = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
+      while (i * (i + 1) / 2 > q) --i;
+      while ((i + 1) * (i + 2) / 2 <= q) ++i;
+      const int c = q - i * (i + 1) / 2;
+      const int bi = i / T, tau = i - bi * T, j = P.bg[bi];
+      const int bc = c / T, tp = c - bc * T, k = P.bg[bc];
+      const int d = tp - tau;
+      double v = Wt[k * W + (T - 1) + d] + Wt[j * W + (T - 1) - d];
+      v = fma(-Xt[k * W + (T - 1) + d], Pt[k * T + tau], v);
+      v = fma(-Xt[j * W + (T - 1) - d], Pt[j * T + tp], v);
+      v = fma(-(Et[k * T + tp] * Et[j * T + tau]), Qt[k * T + tp] + Qt[j * T + tau], v);
+      v = Cm[j * G + k] * v;
+      if (i == c) v = (v + jitter) + noise;
+      sm[i * ld + c] = v;
+    }
+  } else if (tabs) {
     // n <= 63 (the launch's LDS holds the tables): gene-gene pairs from KxxTab, the same bits
     // as kernel_ref with a third of its transcendentals; pairs with a latent row direct
     double* gam = hyp + 3 * G + 3;
@@ -3102,13 +3133,14 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
 }
 
 int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn, int maxg,
-                       int negative, double* d_out, int* d_status) {
+                       int gridtab, int negative, double* d_out, int* d_status) {
   // tables (KxxTab) when every problem has n + 1 <= 64 rows: 3 G + n + n G doubles
   const int tabs = maxn + 1 <= 64;
   const size_t tab = tabs ? 3 * (size_t)maxg + maxn + (size_t)maxn * maxg : 0;
-  // + 128: the one-wave factor's column buffer (small_factor_regs); + 4 n: x and y
+  // + 128: the one-wave factor's column buffer (small_factor_regs); + 4 n: x and y; + gridtab:
+  // the grid-layout tables
   const size_t lds = ((size_t)(maxn + 1) * (maxn + 2) + 16 + 3 * (size_t)maxg + 3 + tab + 128 +
-                      4 * (size_t)maxn) * sizeof(double);
+                      4 * (size_t)maxn + (size_t)gridtab) * sizeof(double);
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&small_mll_kernel),

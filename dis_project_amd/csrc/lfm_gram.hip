@@ -41,44 +41,13 @@ size_t tables_doubles(int G, int T) {
   return 2 * (size_t)G * W + 3 * (size_t)G * T + (size_t)G * G;
 }
 
-// e^{A} erfc(z) without overflow: erfcx(z) e^{A - z^2} once erfc(z) underflows towards 0.
-__device__ __forceinline__ double exp_erfc(double A, double z) {
-  return z > 0.0 ? erfcx(z) * exp(A - z * z) : exp(A) * erfc(z);
-}
-
 __global__ void tables_kernel(HypDev p, int T, double dt, const double* __restrict__ times,
                               double* __restrict__ tab, float* __restrict__ tab32) {
-  const int G = p.G;
   const int64_t W = 2 * (int64_t)T - 1;
-  const int64_t nW = (int64_t)G * W, nT = (int64_t)G * T;
-  const int64_t total = 2 * nW + 3 * nT + (int64_t)G * G;
-  const double l = p.l;
+  const int64_t total = 2 * (int64_t)p.G * W + 3 * (int64_t)p.G * T + (int64_t)p.G * p.G;
   for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
        idx += (int64_t)gridDim.x * blockDim.x) {
-    double v;
-    if (idx < 2 * nW) {
-      const int64_t q = idx < nW ? idx : idx - nW;
-      const int g = (int)(q / W);
-      const int d = (int)(q - (int64_t)g * W) - (T - 1);
-      const double gam = p.D[g] * l / 2.0;
-      const double delta = (double)d * dt;
-      const double A = gam * gam - p.D[g] * delta;
-      v = idx < nW ? exp_erfc(A, gam - delta / l) : exp(A);
-    } else if (idx < 2 * nW + 3 * nT) {
-      const int64_t q0 = idx - 2 * nW;
-      const int which = (int)(q0 / nT);
-      const int64_t q = q0 - which * nT;
-      const int g = (int)(q / T);
-      const double t = times[q - (int64_t)g * T];
-      const double gam = p.D[g] * l / 2.0;
-      if (which == 0) v = erfc(t / l + gam);
-      else if (which == 1) v = exp(-p.D[g] * t);
-      else v = exp_erfc(gam * gam, gam - t / l) - erfcx(gam);
-    } else {
-      const int64_t q = idx - 2 * nW - 3 * nT;
-      const int j = (int)(q / G), k = (int)(q - (int64_t)j * G);
-      v = p.S[j] * p.S[k] * l * kSqrtPi * 0.5 / (p.D[j] + p.D[k]);
-    }
+    const double v = grid_table_entry(p, T, dt, times, idx);
     tab[idx] = v;
     if (tab32) tab32[idx] = (float)v;
   }

@@ -166,7 +166,20 @@ struct SmallProb {
   const double* dsb;
   const double* sc;
   int n, G;
+  // grid layout (dataset_3d blocks on one uniform time grid; T = 0: none): the gram from the
+  // per-gene tables of lfm_gram.hip (tables_doubles(G, T) doubles of LDS)
+  int T = 0;
+  double dt = 0.0;
+  const double* times = nullptr;  // [T]
+  const int* bg = nullptr;        // [n / T] gene of each block
 };
+// host: detect the grid layout of problem p and, when its tables fit the kernel's budget, put
+// its times and block genes at hd (device address dd) and fill sp's grid fields; returns the
+// doubles used (at most small_grid_doubles(n))
+int64_t small_grid_pack(const double* x, int64_t n, int64_t G, SmallProb& sp, double* hd,
+                        const double* dd);
+inline int64_t small_grid_doubles(int64_t n) { return n + (n + 1) / 2; }
+constexpr int SMALL_GRID_TAB_MAX = 4096;  // largest per-problem table (doubles) in LDS
 constexpr int SMALL_MAX = 128;  // largest n handled by small_mll_kernel
 
 // gram kernels (lfm_gram.hip)
@@ -219,8 +232,9 @@ int launch_grad(lfm_ctx* ctx, const HypDev& h, const double* d_x, int64_t n, con
                 int64_t lda, int64_t Mp, double obs_stddev, int negative, double* acc,
                 double* d_out, const GridLayout* lay = nullptr, const double* d_times = nullptr,
                 const int* d_bg = nullptr);
+// gridtab: the largest grid table of the problems (doubles; 0: none on the grid path)
 int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn, int maxg,
-                       int negative, double* d_out, int* d_status);
+                       int gridtab, int negative, double* d_out, int* d_status);
 
 // Path of the advisory lock file behind schedule 3's cross-process tenancy (lfm_api.hip;
 // empty if the device has no PCI bus id)

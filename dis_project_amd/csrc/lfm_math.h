@@ -133,6 +133,45 @@ __device__ __forceinline__ void small_tables(const HypDev& h, const double* __re
   __syncthreads();
 }
 
+// e^{A} erfc(z) without overflow: erfcx(z) e^{A - z^2} once erfc(z) underflows towards 0.
+__device__ __forceinline__ double exp_erfc(double A, double z) {
+  return z > 0.0 ? erfcx(z) * exp(A - z * z) : exp(A) * erfc(z);
+}
+
+// Entry idx of the grid-layout tables (layout and identities: lfm_gram.hip, tables_kernel),
+// shared by tables_kernel and small_mll_kernel's grid path.
+__device__ __forceinline__ double grid_table_entry(const HypDev& p, int T, double dt,
+                                                   const double* __restrict__ times,
+                                                   int64_t idx) {
+  const int G = p.G;
+  const int64_t W = 2 * (int64_t)T - 1;
+  const int64_t nW = (int64_t)G * W, nT = (int64_t)G * T;
+  const double l = p.l;
+  if (idx < 2 * nW) {
+    const int64_t q = idx < nW ? idx : idx - nW;
+    const int g = (int)(q / W);
+    const int d = (int)(q - (int64_t)g * W) - (T - 1);
+    const double gam = p.D[g] * l / 2.0;
+    const double delta = (double)d * dt;
+    const double A = gam * gam - p.D[g] * delta;
+    return idx < nW ? exp_erfc(A, gam - delta / l) : exp(A);
+  }
+  if (idx < 2 * nW + 3 * nT) {
+    const int64_t q0 = idx - 2 * nW;
+    const int which = (int)(q0 / nT);
+    const int64_t q = q0 - which * nT;
+    const int g = (int)(q / T);
+    const double t = times[q - (int64_t)g * T];
+    const double gam = p.D[g] * l / 2.0;
+    if (which == 0) return erfc(t / l + gam);
+    if (which == 1) return exp(-p.D[g] * t);
+    return exp_erfc(gam * gam, gam - t / l) - erfcx(gam);
+  }
+  const int64_t q = idx - 2 * nW - 3 * nT;
+  const int j = (int)(q / G), k = (int)(q - (int64_t)j * G);
+  return p.S[j] * p.S[k] * l * kSqrtPi * 0.5 / (p.D[j] + p.D[k]);
+}
+
 // mean_function, model.py:143-149: m[i] = (B/D)[i / (n/G)] * int(x[i,2]).
 __device__ __forceinline__ double mean_at(const HypDev& p, const double* x, int64_t i,
                                           int64_t bs) {

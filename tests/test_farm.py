@@ -389,3 +389,34 @@ def test_resident_batch_large_small_problems():
         np.testing.assert_allclose(ev(models), _oracle_eval(models, datasets), rtol=1e-9)
     finally:
         ev.close()
+
+
+@pytest.mark.gpu
+def test_resident_batch_mixes_grid_and_scattered_layouts():
+    """One launch with problems on the dataset_3d time grid (the gram from the per-gene tables
+    of lfm_gram.hip) beside problems whose rows are not on one (random times, a latent row,
+    shuffled rows: the per-pair path): every value within 1e-9 of the oracle."""
+    from dis_project_amd import _lib
+    from dis_project_amd.dataset import Dataset, grid_inputs
+    from dis_project_amd.model import ExactLFM
+
+    rng = np.random.default_rng(12)
+    models, datasets = [], []
+    for kind, (G, T) in enumerate(((4, 7), (4, 7), (3, 9), (5, 7), (2, 16))):
+        D, S, B = rng.uniform(0.2, 1.0, G), rng.uniform(0.5, 1.5, G), rng.uniform(0.01, 0.1, G)
+        x = grid_inputs(G, T).copy()
+        if kind == 1:
+            x[:, 0] = rng.uniform(0.0, 12.0, G * T)  # same block layout, scattered times
+        elif kind == 3:
+            x[5, 2] = 0.0  # one latent row
+        elif kind == 4:
+            x = x[rng.permutation(G * T)]  # rows shuffled: no block layout
+        y = np.repeat(B / D, T) + 0.5 * rng.standard_normal(G * T)
+        models.append(ExactLFM(jitter=1e-4, num_genes=G, true_d=D, true_s=S, true_b=B,
+                               l=float(rng.uniform(1.0, 3.5))))
+        datasets.append(Dataset(np.ascontiguousarray(x), y))
+    ev = farm.BatchEvaluator(_lib.get_context(), datasets)
+    try:
+        np.testing.assert_allclose(ev(models), _oracle_eval(models, datasets), rtol=1e-9)
+    finally:
+        ev.close()
