@@ -3141,6 +3141,9 @@ int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int ma
   // the grid-layout tables
   const size_t lds = ((size_t)(maxn + 1) * (maxn + 2) + 16 + 3 * (size_t)maxg + 3 + tab + 128 +
                       4 * (size_t)maxn + (size_t)gridtab) * sizeof(double);
+  if (lds > 160 * 1024)
+    return set_err(ctx, LFM_E_ARG, "small batch: LDS past 160 KB (n <= 128, grid tables <= "
+                                   "SMALL_GRID_TAB_MAX)");
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&small_mll_kernel),

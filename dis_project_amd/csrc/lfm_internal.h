@@ -179,7 +179,9 @@ struct SmallProb {
 int64_t small_grid_pack(const double* x, int64_t n, int64_t G, SmallProb& sp, double* hd,
                         const double* dd);
 inline int64_t small_grid_doubles(int64_t n) { return n + (n + 1) / 2; }
-constexpr int SMALL_GRID_TAB_MAX = 4096;  // largest per-problem table (doubles) in LDS
+// largest per-problem grid table (doubles) in LDS: with n = 128 beside it the launch stays
+// within a CU's 160 KB (launch_small_batch)
+constexpr int SMALL_GRID_TAB_MAX = 2048;
 constexpr int SMALL_MAX = 128;  // largest n handled by small_mll_kernel
 
 // gram kernels (lfm_gram.hip)

@@ -369,16 +369,16 @@ def test_small_problem_cache_holds_its_datasets():
 
 @pytest.mark.gpu
 def test_resident_batch_large_small_problems():
-    """lfm_batch with problems past one wave (n + 1 > 64: the 256-thread factor, kernel_ref
-    gram; n = 84 as the pooled-replicate ablation, n = 128 the largest) beside small ones, in one
-    launch: every value within 1e-9 of the oracle."""
+    """lfm_batch with problems past one wave (n + 1 > 64: the 256-thread factor; n = 84 as the
+    pooled-replicate ablation, n = 128 the largest, 16 genes x 8 times the largest grid tables
+    here) beside small ones, in one launch: every value within 1e-9 of the oracle."""
     from dis_project_amd import _lib
     from dis_project_amd.dataset import Dataset, grid_inputs
     from dis_project_amd.model import ExactLFM
 
     rng = np.random.default_rng(11)
     models, datasets = [], []
-    for G, T in ((4, 21), (4, 32), (4, 7), (2, 64), (1, 128)):
+    for G, T in ((4, 21), (4, 32), (4, 7), (2, 64), (1, 128), (16, 8)):
         D, S, B = rng.uniform(0.2, 1.0, G), rng.uniform(0.5, 1.5, G), rng.uniform(0.01, 0.1, G)
         x = grid_inputs(G, T)
         y = np.repeat(B / D, T) + 0.5 * rng.standard_normal(G * T)
