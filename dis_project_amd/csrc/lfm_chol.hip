@@ -2860,8 +2860,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
 // L[c + q][c]. The pivot of column c + 1 is lane c + 1's new d[0], which that lane forms from
 // its own L[c + 1][c] without the LDS round trip, so its reciprocal square root (v_rsq_f64 and
 // one Newton step, as the large factor's leaf) is issued alongside column c's update. The
-// window halves once no more than half of it is live (W = 32 or 64, then 16, 8), so a column
-// costs about as many fused multiply-adds as it has live entries; the column loops stay rolled
+// window narrows as columns retire (W = 64 or 32, then 24, 16, 12, 8: small_next_w), so a
+// column costs about as many fused multiply-adds as it has live entries; the column loops stay rolled
 // (fully unrolled, the straight-line code was instruction-fetch bound). Per element the terms
 // are summed in the same order (k = 0, 1, ...) as before. colbuf: >= 128 doubles, zero from
 // index 64 on. Lane r ends with its pivot (r < n) and residual entry z[r] = L[n][r].
@@ -2873,10 +2873,16 @@ struct SmallFactor {
   double mp, mz;     // this lane's pivot and z entry
   int bad;
 };
+// window widths of the phases: 64 48 32 24 16 12 8
+template <int W>
+constexpr int small_next_w() {
+  return W == 64 ? 48 : W == 48 ? 32 : W == 32 ? 24 : W == 24 ? 16 : W == 16 ? 12 : 8;
+}
 template <int W>
 __device__ __forceinline__ void small_factor_phase(double (&d)[W], int c, SmallFactor& f) {
-  // phase W: the columns while more than W / 2 of them remain (the last phase: all)
-  const int cend = W > 8 ? max(c, f.n - W / 2) : f.n;
+  // phase W: the columns while more than the next width of them remain (the last phase: all)
+  constexpr int WN = small_next_w<W>();
+  const int cend = W > 8 ? max(c, f.n - WN) : f.n;
 #pragma unroll 1
   for (; c < cend; ++c) {
     if (!(f.dc > 0.0) && f.bad == 0) f.bad = c + 1;
@@ -2901,7 +2907,7 @@ __device__ __forceinline__ void small_factor_phase(double (&d)[W], int c, SmallF
     f.y = yn;
   }
   if constexpr (W > 8)
-    if (c < f.n) small_factor_phase<W / 2>(*reinterpret_cast<double(*)[W / 2]>(&d[0]), c, f);
+    if (c < f.n) small_factor_phase<WN>(*reinterpret_cast<double(*)[WN]>(&d[0]), c, f);
 }
 template <int MR>
 __device__ __forceinline__ void small_factor_regs(const double* __restrict__ sm, int ld, int n,

@@ -398,7 +398,7 @@ def gpu_evaluator(ctx: _lib.Context, datasets, negative: bool = False, workers: 
         def evaluate(models, data):
             ev = cache[0] if cache else None
             if ev is None or len(ev.datasets) != len(data) or \
-                    any(a is not b for a, b in zip(ev.datasets, data)):
+                    not all(map(operator.is_, ev.datasets, data)):
                 close()
                 ev = BatchEvaluator(ctx, data, negative)
                 cache.append(ev)
