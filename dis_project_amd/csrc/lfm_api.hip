@@ -1197,6 +1197,10 @@ struct lfm_batch {
                             // the SmallProb table
   SmallProb* dprobs = nullptr;
   double* hbuf = nullptr;   // pinned host: hyp [nhyp] | out [nprob] | status [nprob] (int)
+  // small enough for the kernel arguments (LFM_SMALL_KERNARG, default on; read at creation)
+  bool use_args = false;
+  std::vector<SmallProb> table;      // host copy of the problem table
+  std::vector<int> dsb_off, sc_off;  // each problem's offsets in the packed hyperparameters
 };
 
 int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_batch** out) {
@@ -1260,7 +1264,12 @@ int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_
     sp.G = (int)G;
     off += small_grid_pack(p.x, n, G, sp, &hd[off], dd + off);
     if (sp.T) b->gridtab = std::max<int>(b->gridtab, (int)tables_doubles((int)G, sp.T));
+    b->dsb_off.push_back((int)(hv - 3 * G));
+    b->sc_off.push_back((int)(nvec + hs - 3));
   }
+  b->use_args = env_int_api("LFM_SMALL_KERNARG", 1) != 0 && nprob <= SMALL_ARG_PROBS &&
+                nhyp <= SMALL_ARG_HYP;
+  b->table = table;
   e = hipMemcpyAsync(b->dmem, hd.data(), (size_t)nd * 8, hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess)
     e = hipMemcpyAsync(b->dprobs, table.data(), bytes_p, hipMemcpyHostToDevice, ctx->stream);
@@ -1301,10 +1310,24 @@ int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int neg
   const int64_t np = batch->nprob;
   double* hres = batch->hbuf + batch->nhyp;
   int* hst = reinterpret_cast<int*>(hres + np);
-  std::memcpy(batch->hbuf, hyp, (size_t)batch->nhyp * 8);
   for (int64_t q = 0; q < np; ++q) hst[q] = -1;  // a problem's status word is written last
-  int r = launch_small_batch(ctx, batch->dprobs, (int)np, batch->maxn, batch->maxg,
-                             batch->gridtab, negative, hres, hst);
+  int r;
+  if (batch->use_args) {
+    // the problem table and the hyperparameters travel in the kernel arguments
+    SmallArgs a;
+    std::memcpy(a.probs, batch->table.data(), (size_t)np * sizeof(SmallProb));
+    std::memcpy(a.hyp, hyp, (size_t)batch->nhyp * 8);
+    std::memcpy(a.dsb_off, batch->dsb_off.data(), (size_t)np * sizeof(int));
+    std::memcpy(a.sc_off, batch->sc_off.data(), (size_t)np * sizeof(int));
+    a.out = hres;
+    a.status = hst;
+    a.negative = negative;
+    r = launch_small_args(ctx, a, (int)np, batch->maxn, batch->maxg, batch->gridtab);
+  } else {
+    std::memcpy(batch->hbuf, hyp, (size_t)batch->nhyp * 8);
+    r = launch_small_batch(ctx, batch->dprobs, (int)np, batch->maxn, batch->maxg,
+                           batch->gridtab, negative, hres, hst);
+  }
   if (r) return r;
   // Completion: every workgroup writes its result, a system-scope fence, then its status word
   // (>= 0) into this pinned buffer, after it has read the hyperparameters, so the results are

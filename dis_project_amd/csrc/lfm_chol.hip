@@ -2941,12 +2941,10 @@ __device__ __forceinline__ void small_factor_regs(const double* __restrict__ sm,
 #ifndef LFM_SMALL_STAMPS
 #define LFM_SMALL_STAMPS 0
 #endif
-__global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restrict__ probs,
-                                                        int negative, double* __restrict__ out,
-                                                        int* __restrict__ status, int tabs) {
+__device__ __forceinline__ void small_body(const SmallProb P, int negative,
+                                           double* __restrict__ out, int* __restrict__ status,
+                                           int tabs, unsigned long long st0) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const unsigned long long st0 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
-  const SmallProb P = probs[blockIdx.x];
   const int n = P.n, M = n + 1, ld = n + 2, G = P.G;
   const int tid = threadIdx.x;
   double* red = sm + (size_t)M * ld;  // [8] reduction scratch + [1] flag
@@ -3138,15 +3136,58 @@ __global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restr
   }
 }
 
-int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn, int maxg,
-                       int gridtab, int negative, double* d_out, int* d_status) {
+__global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restrict__ probs,
+                                                        int negative, double* __restrict__ out,
+                                                        int* __restrict__ status, int tabs) {
+  const unsigned long long st0 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
+  small_body(probs[blockIdx.x], negative, out, status, tabs, st0);
+}
+
+// The same with the problem table and the hyperparameters in the kernel arguments (a resident
+// batch of at most SMALL_ARG_PROBS problems and SMALL_ARG_HYP hyperparameters): no dependent
+// load of the table from HBM and no read of pinned host memory before the gram.
+__global__ __launch_bounds__(256) void small_mll_kernel_args(SmallArgs a) {
+  const unsigned long long st0 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
+  SmallProb P = a.probs[blockIdx.x];
+  P.dsb = a.hyp + a.dsb_off[blockIdx.x];
+  P.sc = a.hyp + a.sc_off[blockIdx.x];
+  small_body(P, a.negative, a.out, a.status, a.tabs, st0);
+}
+
+static size_t small_lds(int maxn, int maxg, int gridtab, int* tabs_out) {
   // tables (KxxTab) when every problem has n + 1 <= 64 rows: 3 G + n + n G doubles
   const int tabs = maxn + 1 <= 64;
   const size_t tab = tabs ? 3 * (size_t)maxg + maxn + (size_t)maxn * maxg : 0;
+  *tabs_out = tabs;
   // + 128: the one-wave factor's column buffer (small_factor_regs); + 4 n: x and y; + gridtab:
   // the grid-layout tables
-  const size_t lds = ((size_t)(maxn + 1) * (maxn + 2) + 16 + 3 * (size_t)maxg + 3 + tab + 128 +
-                      4 * (size_t)maxn + (size_t)gridtab) * sizeof(double);
+  return ((size_t)(maxn + 1) * (maxn + 2) + 16 + 3 * (size_t)maxg + 3 + tab + 128 +
+          4 * (size_t)maxn + (size_t)gridtab) * sizeof(double);
+}
+
+int launch_small_args(lfm_ctx* ctx, SmallArgs& a, int nprob, int maxn, int maxg, int gridtab) {
+  int tabs;
+  const size_t lds = small_lds(maxn, maxg, gridtab, &tabs);
+  if (lds > 160 * 1024 || nprob > SMALL_ARG_PROBS)
+    return set_err(ctx, LFM_E_ARG, "small batch (kernel arguments): past its limits");
+  a.tabs = tabs;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&small_mll_kernel_args),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  hipEvent_t ev;
+  prof_begin(ctx, K_SMALL, &ev, ctx->stream);
+  hipLaunchKernelGGL(small_mll_kernel_args, dim3(nprob), dim3(256), lds, ctx->stream, a);
+  prof_end(ctx, K_SMALL, ev, 0, 0, ctx->stream);
+  return hip_fail(ctx, hipGetLastError(), "small_mll_kernel_args");
+}
+
+int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn, int maxg,
+                       int gridtab, int negative, double* d_out, int* d_status) {
+  int tabs;
+  const size_t lds = small_lds(maxn, maxg, gridtab, &tabs);
   if (lds > 160 * 1024)
     return set_err(ctx, LFM_E_ARG, "small batch: LDS past 160 KB (n <= 128, grid tables <= "
                                    "SMALL_GRID_TAB_MAX)");

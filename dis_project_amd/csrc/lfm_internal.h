@@ -234,6 +234,18 @@ int launch_grad(lfm_ctx* ctx, const HypDev& h, const double* d_x, int64_t n, con
                 int64_t lda, int64_t Mp, double obs_stddev, int negative, double* acc,
                 double* d_out, const GridLayout* lay = nullptr, const double* d_times = nullptr,
                 const int* d_bg = nullptr);
+// A resident batch small enough to travel in the kernel arguments (small_mll_kernel_args)
+constexpr int SMALL_ARG_PROBS = 16, SMALL_ARG_HYP = 320;
+struct SmallArgs {
+  SmallProb probs[SMALL_ARG_PROBS];  // dsb / sc unused: the hyperparameters are below
+  double hyp[SMALL_ARG_HYP];         // lfm_batch_mll_f64's packed layout
+  int dsb_off[SMALL_ARG_PROBS], sc_off[SMALL_ARG_PROBS];
+  double* out;
+  int* status;
+  int negative, tabs;
+};
+static_assert(sizeof(SmallArgs) <= 4096, "kernel argument block");
+int launch_small_args(lfm_ctx* ctx, SmallArgs& a, int nprob, int maxn, int maxg, int gridtab);
 // gridtab: the largest grid table of the problems (doubles; 0: none on the grid path)
 int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn, int maxg,
                        int gridtab, int negative, double* d_out, int* d_status);
