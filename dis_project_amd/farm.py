@@ -235,6 +235,12 @@ class Farm:
         self.world, self.rank, self.gather = world, rank, gather
 
     def run(self, nprob: int, evaluate: Callable[[Sequence[int]], np.ndarray]) -> np.ndarray:
+        if self.world == 1 and nprob:
+            # one rank: every problem is this rank's and the exchange is the identity
+            vals = np.asarray(evaluate(list(range(nprob))), dtype=np.float64).reshape(-1)
+            if vals.size != nprob:
+                raise ValueError("evaluate returned the wrong number of values")
+            return vals.copy()
         per = slots_per_rank(nprob, self.world)
         mine = partition(nprob, self.world, self.rank)
         send = np.full(max(per, 1), np.nan)

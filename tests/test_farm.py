@@ -96,8 +96,8 @@ def test_farm_gloo_world2(world):
 @pytest.mark.parametrize("kind,kw", [("c5", {}), ("c3", dict(genes=4, timepoints=64, restarts=6))])
 def test_farm_rccl_single_rank_liblfm(kind, kw):
     """Product path on one GPU, as bench.py --workload c3 / c5 runs it: the liblfm evaluator
-    (one batched launch for C5; the HBM-resident dataset for C3, N = 256) and the RCCL
-    all-gather (world 1), against the oracle."""
+    (one batched launch for C5; the HBM-resident dataset for C3, N = 256) against the oracle,
+    and the RCCL all-gather of its results (world 1: the identity)."""
     from dis_project_amd import _lib
 
     ctx = _lib.get_context()
@@ -106,6 +106,8 @@ def test_farm_rccl_single_rank_liblfm(kind, kw):
     g = farm.RcclGather(ctx, 1, 0, farm.RcclGather.unique_id(ctx))
     try:
         out = farm.Farm(1, 0, g).run_problems(models, datasets, evaluate)
+        # one rank's round needs no exchange (Farm.run's fast path); the all-gather itself
+        np.testing.assert_array_equal(g(out), out)
     finally:
         g.close()
         close()
