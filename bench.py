@@ -581,6 +581,10 @@ def main(argv=None):
         ctx.profile(False)
         ctx.profile_reset()
     timed, step_ms = [], []
+    # schedule-3 stalls re-run on schedule 1 inside the call (lfm_ctx_fallbacks): counted over
+    # the timed region, so a line can never price a fallback as the step kernel
+    fb0 = ctx.fallbacks
+    sched = ctx.schedule
     barrier()
     t0 = time.perf_counter()
     for s in range(a.steps):
@@ -593,6 +597,7 @@ def main(argv=None):
             ctx.profile(False)
     barrier()
     elapsed = time.perf_counter() - t0
+    fallbacks = ctx.fallbacks - fb0
     if prof:
         stats = ctx.profile_read()
     # per-step wall (each step ends on the host: its results are read back), median per rank
@@ -601,6 +606,9 @@ def main(argv=None):
         t = torch.tensor([elapsed, med_ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, med_ms = (float(v) for v in t.tolist())
+        fb = torch.tensor([fallbacks], dtype=torch.int64)
+        dist.all_reduce(fb, op=dist.ReduceOp.SUM)
+        fallbacks = int(fb.item())
     # the exchange step alone (collective latency reported separately): the same
     # all-gather of this workload's NaN-padded slots, outside the timed region
     collective = None
@@ -697,6 +705,11 @@ def main(argv=None):
                                                  "communicator failed to initialise)"}[exchange]
                                if world > 1 else "none"},
         "result_first": float(res[0][0]),
+        # the factorisation schedule the timed steps were meant to run (rank 0's context) and
+        # the schedule-3 calls of the timed region, over all ranks, that stalled and were re-run
+        # on schedule 1 (lfm_ctx_fallbacks): must be 0 for a c2 / c3 line to stand
+        "schedule": sched if a.workload in ("c2", "c3") else None,
+        "s3_fallbacks": fallbacks,
     }
     if workers is not None:
         line["config"]["workers_per_gpu"] = workers
@@ -841,6 +854,9 @@ def main(argv=None):
                              f"{ {k: v for k, v in cb.items() if 'gpu_vs' in k} }")
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if fallbacks and a.workload in ("c2", "c3"):
+        raise SystemExit(f"{fallbacks} timed schedule-3 call(s) stalled and were re-run on "
+                         "schedule 1: the line above does not measure the priced schedule")
     close()
     if world > 1:
         gather.close()

@@ -338,16 +338,11 @@ int64_t round_up(int64_t a, int64_t b) { return (a + b - 1) / b * b; }
 // LFM_S3_FALLBACK=0 turns it off (the tests of the timeout path itself).
 constexpr unsigned kFallbackWaitTicks = 3000000000u;  // 30 s of the 100 MHz clock
 
-bool s3_fallback_on() {
-  const char* v = std::getenv("LFM_S3_FALLBACK");
-  return !v || std::atoi(v) != 0;
-}
-
 template <class F>
 int with_s3_fallback(lfm_ctx* ctx, F&& attempt) {
   const bool s3 = s3_on(ctx);
   int r = attempt();
-  if (r != LFM_E_TIMEOUT || !s3 || !s3_fallback_on()) return r;
+  if (r != LFM_E_TIMEOUT || !s3 || !ctx->s3_fallback) return r;
   const std::string why = ctx->err;
   // the stalled call's waits have all ended (each within one bound, or at once after the first
   // timeout); drain both streams of the pair before the workspace is reused
@@ -663,11 +658,32 @@ void release_partition(lfm_ctx* ctx) {
 //   LFM_GRAD_DIRECT      1: the gradient's per-pair path even on a grid layout (cross-check)
 //   LFM_GRAM_FUSE        0: the full gram in its own kernel even where the first update could
 //                        generate it (cross-check: the MLL is bit-identical either way)
+//   LFM_W4_MIN / LFM_W2_MIN / LFM_W0   the step plan (lfm_chol.hip chol_factor_solve)
+//   LFM_HELPER / LFM_HELPER_TC / LFM_HELPER_MIN   schedule 3's side-CU helper and its sizing
+//   LFM_S3_FALLBACK      0: a stalled schedule-3 call returns LFM_E_TIMEOUT (no schedule-1 re-run)
+//   LFM_RCCL_TIMEOUT_S   bound on every wait of the farm communicator (default 300 s)
+//   LFM_DEBUG_FARM_STALL_MS  test stand-in for a late peer ahead of each all-gather
+//   LFM_SMALL_KERNARG    0: resident batches read their problem table / hyperparameters from
+//                        memory instead of the kernel arguments
+// Every knob is read here, once: a call never consults the environment.
 hipError_t create_streams(lfm_ctx* ctx) {
   ctx->sched = env_int_api("LFM_SCHED", 3) == 1 ? 1 : 3;
   ctx->s3_events = (int)env_int_api("LFM_S3_EVENTS", 0);
   ctx->grad_direct = env_int_api("LFM_GRAD_DIRECT", 0) != 0;
   ctx->gram_fuse = env_int_api("LFM_GRAM_FUSE", LFM_GRAM_FUSE_DEFAULT) != 0;
+  ctx->w4min = env_int_api("LFM_W4_MIN", 6144);
+  ctx->w2min = env_int_api("LFM_W2_MIN", -1);
+  ctx->w0 = std::max(1, env_int_api("LFM_W0", 1));
+  ctx->helper = env_int_api("LFM_HELPER", 1);
+  ctx->helper_tc = env_int_api("LFM_HELPER_TC", 700);
+  ctx->helper_min = env_int_api("LFM_HELPER_MIN", 1200);
+  ctx->s3_fallback = env_int_api("LFM_S3_FALLBACK", 1) != 0;
+  if (const char* v = std::getenv("LFM_RCCL_TIMEOUT_S")) {
+    const double t = std::atof(v);
+    if (t > 0.0) ctx->rccl_timeout_s = t;
+  }
+  ctx->farm_stall_ms = std::max(0, env_int_api("LFM_DEBUG_FARM_STALL_MS", 0));
+  ctx->small_kernarg = env_int_api("LFM_SMALL_KERNARG", 1) != 0;
   if (const char* ms = std::getenv("LFM_DEVICE_WAIT_MS")) {
     // 100 MHz ticks; at most ~42 s (the bound is a 32-bit tick count)
     const double t = std::min(std::max(std::atof(ms), 0.0), 42000.0);
@@ -1196,7 +1212,10 @@ struct lfm_batch {
   char* dmem = nullptr;     // device: x / y (+ grid times / block genes) of every problem, then
                             // the SmallProb table
   SmallProb* dprobs = nullptr;
-  double* hbuf = nullptr;   // pinned host: hyp [nhyp] | out [nprob] | status [nprob] (int)
+  double* hbuf = nullptr;   // pinned host, coherent: hyp [nhyp] | out [nprob] | status [nprob]
+                            // (int); the kernel reads / writes it directly and the host spins on
+                            // the status words, so it must not be cached on the device side
+  hipEvent_t done = nullptr;  // recorded after every launch on the batch: destroy waits on it
   // small enough for the kernel arguments (LFM_SMALL_KERNARG, default on; read at creation)
   bool use_args = false;
   std::vector<SmallProb> table;      // host copy of the problem table
@@ -1235,9 +1254,14 @@ int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_
   const size_t bytes_d = round_up(nd * 8, 16), bytes_p = (size_t)nprob * sizeof(SmallProb);
   hipError_t e = hipMalloc((void**)&b->dmem, bytes_d + bytes_p);
   if (e != hipSuccess) return hip_fail(ctx, e, "lfm_batch_create: device buffer");
-  e = hipHostMalloc((void**)&b->hbuf, (size_t)(nhyp + 2 * nprob) * 8, hipHostMallocDefault);
+  // coherent (fine-grained): the kernel reads the hyperparameters a call has just written and
+  // its result / status stores must reach the host's spin without a stream synchronise,
+  // whatever HIP_HOST_COHERENT says
+  e = hipHostMalloc((void**)&b->hbuf, (size_t)(nhyp + 2 * nprob) * 8, hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&b->done, hipEventDisableTiming);
   if (e != hipSuccess) {
     hipFree(b->dmem);
+    if (b->hbuf) hipHostFree(b->hbuf);
     return hip_fail(ctx, e, "lfm_batch_create: pinned buffer");
   }
   b->dprobs = reinterpret_cast<SmallProb*>(b->dmem + bytes_d);
@@ -1267,7 +1291,7 @@ int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_
     b->dsb_off.push_back((int)(hv - 3 * G));
     b->sc_off.push_back((int)(nvec + hs - 3));
   }
-  b->use_args = env_int_api("LFM_SMALL_KERNARG", 1) != 0 && nprob <= SMALL_ARG_PROBS &&
+  b->use_args = ctx->small_kernarg && nprob <= SMALL_ARG_PROBS &&
                 nhyp <= SMALL_ARG_HYP;
   b->table = table;
   e = hipMemcpyAsync(b->dmem, hd.data(), (size_t)nd * 8, hipMemcpyHostToDevice, ctx->stream);
@@ -1293,8 +1317,12 @@ int lfm_batch_destroy(lfm_batch* batch) {
   if (!batch) return LFM_OK;
   hipSetDevice(batch->device);
   // an evaluation returns once its status words land, possibly before its kernel has retired:
-  // drain the device before the buffers go
-  hipDeviceSynchronize();
+  // wait for the batch's last launch (not the whole device: other contexts' streams may be busy
+  // or stuck) before the buffers go
+  if (batch->done) {
+    hipEventSynchronize(batch->done);
+    hipEventDestroy(batch->done);
+  }
   hipFree(batch->dmem);
   hipHostFree(batch->hbuf);
   delete batch;
@@ -1329,6 +1357,7 @@ int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int neg
                            batch->gridtab, negative, hres, hst);
   }
   if (r) return r;
+  hipEventRecord(batch->done, ctx->stream);
   // Completion: every workgroup writes its result, a system-scope fence, then its status word
   // (>= 0) into this pinned buffer, after it has read the hyperparameters, so the results are
   // complete and the buffer free once no status word is -1: the host spins on them (~µs sooner
@@ -1523,13 +1552,10 @@ int rccl_fail(lfm_ctx* ctx, ncclResult_t r, const char* what) {
                  std::string(what) + ": " + (g_rccl.errStr ? g_rccl.errStr(r) : "rccl error"));
 }
 
-// Bound on every wait of a non-blocking communicator (seconds, LFM_RCCL_TIMEOUT_S, default
-// 300): a peer rank that died or never joined ends the call with LFM_E_RCCL instead of a hang.
-double rccl_timeout_s() {
-  const char* v = std::getenv("LFM_RCCL_TIMEOUT_S");
-  const double t = v ? std::atof(v) : 300.0;
-  return t > 0.0 ? t : 300.0;
-}
+// Bound on every wait of a non-blocking communicator (seconds, LFM_RCCL_TIMEOUT_S at context
+// creation, default 300): a peer rank that died or never joined ends the call with LFM_E_RCCL
+// instead of a hang.
+double rccl_timeout_s(const lfm_ctx* ctx) { return ctx->rccl_timeout_s; }
 
 double mono_s() {
   timespec ts;
@@ -1562,7 +1588,7 @@ void rccl_drop(lfm_ctx* ctx) {
 
 // Poll a non-blocking communicator until its pending operation leaves ncclInProgress.
 int rccl_poll(lfm_ctx* ctx, ncclComm_t comm, const char* what) {
-  const double end = mono_s() + rccl_timeout_s();
+  const double end = mono_s() + rccl_timeout_s(ctx);
   const Backoff bo;
   for (;;) {
     ncclResult_t st = ncclInProgress;
@@ -1578,7 +1604,7 @@ int rccl_poll(lfm_ctx* ctx, ncclComm_t comm, const char* what) {
 // Bounded wait for everything enqueued on the context's stream (the collective included): a
 // collective whose peers never arrive would otherwise block the stream, and the caller, forever.
 int rccl_stream_wait(lfm_ctx* ctx, const char* what) {
-  const double end = mono_s() + rccl_timeout_s();
+  const double end = mono_s() + rccl_timeout_s(ctx);
   const Backoff bo;
   hipError_t e;
   while ((e = hipStreamQuery(ctx->stream)) == hipErrorNotReady) {
@@ -1676,7 +1702,7 @@ int lfm_farm_allgather_f64(lfm_ctx* ctx, const double* send, int64_t count, doub
   if (e != hipSuccess) return hip_fail(ctx, e, "farm upload");
   // test instrument: a collective whose peers are late, stood in for by a kernel that holds
   // the stream for LFM_DEBUG_FARM_STALL_MS (the one-GPU box cannot host a second rank)
-  if (const int stall = env_int_api("LFM_DEBUG_FARM_STALL_MS", 0)) {
+  if (const int stall = ctx->farm_stall_ms) {
     hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, ctx->stream,
                        (unsigned long long)stall * 100000ull);
   }

@@ -989,20 +989,6 @@ struct Panel {
 #ifndef LFM_TALL_GROUP
 #define LFM_TALL_GROUP 1
 #endif
-// 32-row ahead / rest units in the w = 1 steps (LFM_TR32 at run time; this is its default)
-#ifndef LFM_TR32_DEFAULT
-#define LFM_TR32_DEFAULT 0
-#endif
-// rest-unit stealing across XCDs (LFM_STEAL at run time, units per XCD; this is its default):
-// the last LFM_STEAL rest units of each XCD's range are claimed from per-XCD counters, and
-// LFM_STEAL_EXTRA extra workgroups per XCD claim what a later XCD has not started, so an XCD
-// that runs its units faster takes over the end of a slower one's range
-#ifndef LFM_STEAL_DEFAULT
-#define LFM_STEAL_DEFAULT 0
-#endif
-#ifndef LFM_STEAL_EXTRA_DEFAULT
-#define LFM_STEAL_EXTRA_DEFAULT 24
-#endif
 // workgroups of the tall segment: a multiple of 8 (XCDs), of 8 LFM_TALL_SPLIT when grouped
 __host__ __device__ constexpr int64_t tall_grid(int64_t nt) {
   return (LFM_TALL_RR && LFM_TALL_GROUP) ? (nt + 8 * LFM_TALL_SPLIT - 1) / (8 * LFM_TALL_SPLIT) *
@@ -1344,13 +1330,6 @@ struct StepArgs {
   GramGen gen;       // gen.tab != NULL: the first step's update units generate Sigma (fused gram)
   int64_t rest_off;  // rest units of this launch are [rest_off, rest_off + nr) of the step's
                      // enumeration (the side-CU helper launch takes the tail of it)
-  int sub;             // ahead / rest units per 128-row tile: 2 (64-row units, step_kernel) or 4
-                      // (32-row units, step_kernel32: the w = 1 steps, LFM_TR32)
-  // rest-unit stealing (0: off): the last `steal` units of each XCD's rest range are claimed
-  // from steal_ctr[16 x] (zeroed per call), by its own workgroups and by `steal_extra` extra
-  // workgroups per XCD at the end of the rest segment
-  int steal, steal_extra;
-  unsigned* steal_ctr;
   unsigned long long* trace;  // diagnostics (NULL: off): 4 words per workgroup (lfm_debug_trace)
   unsigned long long trace_tag;  // launch tag, bits 40+ of each record's last word
 };
@@ -1390,40 +1369,7 @@ __device__ __forceinline__ void tall_or_xcd_range(int seg, int64_t cnt, int64_t 
 }
 
 // workgroups of a step launch's rest segment (a multiple of 8: one queue per XCD)
-__host__ __device__ inline int64_t rest_wgs(const StepArgs& g) {
-  return g.steal ? 8 * ((int64_t)(g.nr + 7) / 8 + g.steal_extra) : (int64_t)(g.nr + 7) / 8 * 8;
-}
-
-// Rest unit of workgroup bq of the rest segment under stealing (-1: none left). XCD x = bq % 8
-// runs its range [lo_x, hi_x) in order up to its last t_x = min(steal, hi_x - lo_x) units, which
-// are taken from counter x: first by the workgroup's own XCD, then round the ring of the others,
-// so a workgroup reaching the end of a fast XCD's queue runs a unit a slower XCD has not
-// started. Each unit is claimed once (a counter past t_x is exhausted); a claimed unit runs at
-// once and waits on nothing, so claims add no dependence to the launch's deadlock argument.
-__device__ __forceinline__ int64_t rest_claim(const StepArgs& g, int64_t bq) {
-  const int x = (int)(bq % 8);
-  const int64_t p = bq / 8;
-  int64_t lo, hi;
-  xcd_range(g.nr, x, &lo, &hi);
-  if (p < hi - lo - min((int64_t)g.steal, hi - lo)) return lo + p;
-  __shared__ int64_t su;
-  if (threadIdx.x == 0) {
-    int64_t v = -1;
-    for (int k = 0; k < 8 && v < 0; ++k) {
-      const int y = (x + k) & 7;
-      int64_t ly, hy;
-      xcd_range(g.nr, y, &ly, &hy);
-      const unsigned ty = (unsigned)min((int64_t)g.steal, hy - ly);
-      unsigned* c = g.steal_ctr + 16 * y;
-      if (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ty) continue;
-      const unsigned got = __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (got < ty) v = hy - (int64_t)ty + got;
-    }
-    su = v;
-  }
-  __syncthreads();
-  return su;
-}
+__host__ __device__ inline int64_t rest_wgs(const StepArgs& g) { return (int64_t)(g.nr + 7) / 8 * 8; }
 
 __device__ __forceinline__ void bump_after_stores(unsigned* ctr) {
   __builtin_amdgcn_s_waitcnt(0);  // this thread's write-through stores have completed
@@ -1464,7 +1410,7 @@ __device__ __forceinline__ bool tall_unit(const StepArgs& g, int64_t u, double (
       // rows past step s's update (bordered: the border rows that entered the window with
       // super-panel s + 1, zero in every earlier panel column) have no ahead unit to wait for
       if (good && g.a_done && (i0 - g.s0) / ST < g.T) {
-        good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], (unsigned)(g.sub * g.wn), g.spin,
+        good = spin_until<false>(&g.a_done[(i0 - g.s0) / ST], (unsigned)(2 * g.wn), g.spin,
                                  g.status);
         if (!good) why = 2;
       }
@@ -1552,11 +1498,6 @@ __device__ __forceinline__ void step_body(const StepArgs& g, unsigned long long*
   }
   int64_t lo, hi;
   tall_or_xcd_range(seg, cnt[seg], b - base, &lo, &hi);
-  if (seg == 1 && g.steal) {
-    lo = rest_claim(g, b - base);
-    hi = lo + 1;
-    if (lo < 0) return;
-  }
   const int64_t u = lo;
   if (u >= hi) return;
   const int role = seg + 1;
@@ -1648,16 +1589,12 @@ __device__ __forceinline__ void step_traced(const StepArgs& g) {
 
 // (256, 4): 128 VGPRs, 4 waves / SIMD (the zero-C tile body would otherwise take 134)
 __global__ __launch_bounds__(256, 4) void step_kernel(StepArgs g) { step_body<64>(g); }
-// The w = 1 steps' launches with 32-row ahead / rest units (LFM_TR32): twice the units of half
-// the work, so a launch of one or two rounds of units is quantized half as coarsely
-__global__ __launch_bounds__(256, 4) void step_kernel32(StepArgs g) { step_body<32>(g); }
 // The side-CU helper's launches (rest units only): the same body under its own name, so
 // traces and counters keep the main-stream step launches apart
 __global__ __launch_bounds__(256, 4) void helper_update_kernel(StepArgs g) { step_body<64>(g); }
 // Both with the unit trace (lfm_debug_trace on): separate symbols, so the product kernels'
 // code is the untraced body
 __global__ __launch_bounds__(256, 4) void step_kernel_traced(StepArgs g) { step_traced<64>(g); }
-__global__ __launch_bounds__(256, 4) void step_kernel32_traced(StepArgs g) { step_traced<32>(g); }
 __global__ __launch_bounds__(256, 4) void helper_update_kernel_traced(StepArgs g) {
   step_traced<64>(g);
 }
@@ -2289,11 +2226,6 @@ struct Launcher {
     }
   }
 };
-
-int env_int(const char* name, int def) {
-  const char* v = std::getenv(name);
-  return v ? std::atoi(v) : def;
-}
 }  // namespace
 
 // Diagnostics hook (liblfm_diag.so's lfm_probe_syrk, include/lfm_diag.h): ONE launch of the
@@ -2315,7 +2247,6 @@ int probe_update_launch(lfm_ctx* ctx, hipStream_t st, int T, int kd, int cio, in
     // the schedule-3 step kernel's rest role alone (the production unit: 16-deep stages,
     // 4 workgroups / CU, supertile order); bit 5: no C loads (C = 0, stores kept)
     StepArgs g{};
-    g.sub = 2;
     g.A = ctx->A;
     g.lda = n;
     g.s0 = 512;
@@ -2428,14 +2359,14 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   // would otherwise hold up the first w = 1 chains (measured 0.13-0.24 ms faster than going
   // straight to w = 1); its first super-panel is one block wide (its factor precedes any bulk
   // work).
-  const int64_t w4min = env_int("LFM_W4_MIN", 6144);
+  const int64_t w4min = ctx->w4min;
   // bulk width: 5 block columns (W = 640) for the MLL — its C traffic per flop is 4/5 of W = 512
   // and its chain still hides behind the update (A/B: -0.23..-0.26 ms per evaluation; W = 768
   // and 896 were slower, 1024 much slower); the bordered gradient keeps 4 (5 measured equal)
   const int wbulk = s3 ? (bordered ? LFM_WBORD : LFM_WBULK) : 4;
-  const int64_t w2min = env_int("LFM_W2_MIN", s3 ? 5120 : 4096);
+  const int64_t w2min = ctx->w2min >= 0 ? ctx->w2min : (s3 ? 5120 : 4096);
   const std::vector<std::pair<int64_t, int>> steps =
-      plan_steps(nblk, Mp, NB, bordered, s3, wbulk, w4min, w2min, (int)env_int("LFM_W0", 1));
+      plan_steps(nblk, Mp, NB, bordered, s3, wbulk, w4min, w2min, ctx->w0);
   const int S = (int)steps.size();
   r = ensure_events(ctx, 3 * (size_t)S + 3);  // [2 S + 3, 3 S + 3): LFM_S3_EVENTS=2
   if (r) return r;
@@ -2495,9 +2426,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     if (!r)
       r = ensure(ctx, (void**)&ctx->linv_full, &ctx->linv_full_bytes, (size_t)NB * NB * sizeof(double));
     if (!r) r = ensure(ctx, (void**)&ctx->xd, &ctx->xd_bytes, (size_t)Wmax * Wmax * sizeof(double));
-    // + 8 rest-steal counters (64-B apart) per step launch (LFM_STEAL; event-ordered: two
-    // launches a step)
-    const size_t nflags = (size_t)S * (3 + Tmax) + 128 * (2 * (size_t)S + 2);
+    const size_t nflags = (size_t)S * (3 + Tmax);
     if (!r) r = ensure(ctx, (void**)&ctx->flags, &ctx->flags_bytes, nflags * sizeof(unsigned));
     if (r) return r;
     unsigned* chain_done = ctx->flags;     // [S]
@@ -2507,27 +2436,14 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     auto xbuf = [&](int s) { return ctx->xbuf + (size_t)(s & 1) * Mp * Wmax; };
     unsigned* bars = a_done + (size_t)S * Tmax;  // [S] grid barrier counters of chain(s)
     unsigned* xready = bars + S;                  // [S] inputs of chain(s) landed (s >= 1)
-    unsigned* steal_ctrs = xready + S;            // [2 S + 2][128] LFM_STEAL claim counters
-    int nsteal_launch = 0;
-    // rest-unit stealing (read per call): tail units per XCD, extra workgroups per XCD; only
-    // where each XCD's range is at least four tails long
-    const int steal = (int)std::max<int64_t>(0, env_int("LFM_STEAL", LFM_STEAL_DEFAULT));
-    const int steal_extra =
-        (int)std::max<int64_t>(0, env_int("LFM_STEAL_EXTRA", LFM_STEAL_EXTRA_DEFAULT));
     auto wkbuf = [&](int s) { return ctx->wk + (size_t)(s & 1) * 2 * Wmax * Wmax; };
     // launch j = s - 2 (step j's update) writes the inputs of chain(s), s >= 2: the block's
-    // tiles (leading rest units, w_s (w_s + 1) slabs) and its rows of the columns of super-
-    // panel s - 1 (leading ahead units, 2 w_s w_{s-1} slabs); chain(s) forms X_{s-1} of its rows
-    // 32-row units (step_kernel32) for the w = 1 steps after the first (LFM_TR32, read per call;
-    // never the Sigma-generating step 0 or a bordered window)
-    const int tr32 = env_int("LFM_TR32", LFM_TR32_DEFAULT);
-    auto sub_of = [&](int s) {
-      return tr32 && !bordered && s > 0 && steps[s].second == 1 ? 4 : 2;
-    };
-    // (in 64-row slabs; launch s - 2's units are sub_of(s - 2) / 2 slabs each)
+    // tiles (leading rest units, w_s (w_s + 1) 64-row slabs) and its rows of the columns of
+    // super-panel s - 1 (leading ahead units, 2 w_s w_{s-1} slabs); chain(s) forms X_{s-1} of its
+    // rows
     auto xtarget = [&](int s) {
       const int ws = steps[s].second;
-      return (unsigned)((ws * (ws + 1) + 2 * ws * steps[s - 1].second) * sub_of(s - 2) / 2);
+      return (unsigned)(ws * (ws + 1) + 2 * ws * steps[s - 1].second);
     };
     // chain(s): factor block s on the side stream's CUs (one launch, see chain_kernel)
     auto chain = [&](int s, bool dev_wait = true) {
@@ -2581,13 +2497,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       if (!g.zero_from) g.zero_from = INT64_MAX;
       if (!g.copy_from) g.copy_from = INT64_MAX;
       g.spin = ctx->wait_ticks;
-      if (!g.sub) g.sub = 2;
-      g.steal = 0;
-      if (steal > 0 && g.nr / 8 >= 4 * steal && nsteal_launch < 2 * S + 2) {
-        g.steal = steal;
-        g.steal_extra = steal_extra;
-        g.steal_ctr = steal_ctrs + 128 * (size_t)nsteal_launch++;
-      }
       const int64_t grid = (int64_t)(g.na + 7) / 8 * 8 + rest_wgs(g) + tall_grid(g.nt);
       if (grid == 0) return;
       // issued: every 64 x 128 unit in full (padding rows included), tall units as GEMMs with
@@ -2595,7 +2504,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       // matrix (rows s0 .. n, residual row n included: it is the forward substitution) less
       // the next diagonal block (the chain's), and the triangular solve of the rows below
       // the next super-panel (rows .. n) against its W' x W' factor
-      const double issued = ((double)g.na + g.nr) * (ST / g.sub) * ST * 2.0 * g.kd +
+      const double issued = ((double)g.na + g.nr) * 64 * ST * 2.0 * g.kd +
                             (double)g.nt * 64 * (ST / LFM_TALL_SPLIT) * NB * (g.tw + 1);
       double alg = 0.0;
       if (g.na + g.nr > 0) {
@@ -2613,12 +2522,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       trace_launch(ctx, g, grid, false);
       hipEvent_t pe;
       prof_begin(ctx, K_SYRK, &pe, main);
-      if (g.sub == 4)
-        hipLaunchKernelGGL(g.trace ? step_kernel32_traced : step_kernel32, dim3((unsigned)grid),
-                           dim3(256), 0, main, g);
-      else
-        hipLaunchKernelGGL(g.trace ? step_kernel_traced : step_kernel, dim3((unsigned)grid),
-                           dim3(256), 0, main, g);
+      hipLaunchKernelGGL(g.trace ? step_kernel_traced : step_kernel, dim3((unsigned)grid),
+                         dim3(256), 0, main, g);
       prof_end(ctx, K_SYRK, pe, alg, 0, main, issued);
     };
     auto tall_args = [&](StepArgs& g, int s) {  // tall part of the step launch: step s's rows
@@ -2653,17 +2558,16 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
       g.wn = wn;
       if (bordered) g.zero_from = Mp + steps[s].first * NB;
       if (fused && s == 0) g.gen = *gen;
-      g.sub = sub_of(s);
-      g.na = g.sub * wn * (T - wn);
-      g.nr = g.sub / 2 * (T - wn) * (T - wn + 1);  // sub units per tile of the (T - wn)-tile triangle
+      g.na = 2 * wn * (T - wn);
+      g.nr = (T - wn) * (T - wn + 1);  // two 64-row units per tile of the (T - wn)-tile triangle
       g.status = ctx->status;
     };
     // units of step s's rest triangle for the side-CU helper: the main launch of U unit-
     // equivalents takes D0 = U t / (S_m o) alone; giving x units to the helper's S_h slots,
     // which start after chain(s + 1) (Tc), balances at x t (1 / S_h + 1 / S_m) = o (D0 - Tc)
-    const int helper_on = mode == CHOL_MLL || bordered ? (int)env_int("LFM_HELPER", 1) : 0;
-    const double helper_tc = env_int("LFM_HELPER_TC", 700);    // chain(s + 1) + margin, us
-    const double helper_min = env_int("LFM_HELPER_MIN", 1200);  // smallest D0 helped, us
+    const int helper_on = mode == CHOL_MLL || bordered ? ctx->helper : 0;
+    const double helper_tc = ctx->helper_tc;    // chain(s + 1) + margin, us
+    const double helper_min = ctx->helper_min;  // smallest D0 helped, us
     auto helper_share = [&](const StepArgs& g, int wnext) -> int64_t {
       if (!helper_on) return 0;
       return helper_units(g.kd, g.na, g.nr, g.nt / LFM_TALL_SPLIT, wnext, NB, ctx->cus,
@@ -2762,7 +2666,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         // units store without write-through and bump no counter, so they never include a lead
         // tile of chain(s + 2).
         const int64_t total = g.nr;  // the step's rest enumeration
-        const int64_t hu = s >= 1 && s + 2 < S && g.sub == 2
+        const int64_t hu = s >= 1 && s + 2 < S
                                ? helper_clamp(helper_share(g, steps[s + 1].second), (int)total,
                                               g.T, g.wn, g.xready ? g.lead : 0, LFM_SUPERTILE)
                                : 0;
@@ -2780,7 +2684,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
           h.rest_off = total - hu;
           h.nr = (int)hu;
           h.stamps = nullptr;
-          h.steal = 0;
           h.xready = nullptr;  // tail units: never the lead tiles
           trace_launch(ctx, h, (hu + 7) / 8 * 8, true);
           // X_s and step s's C input: launch s - 1 complete

@@ -83,6 +83,16 @@ struct lfm_ctx {
                                                  // device-side wait timed out (lfm_ctx_fallbacks)
   bool grad_direct = false;                      // gradient: per-pair path only (LFM_GRAD_DIRECT)
   bool gram_fuse = true;                         // gram in the first update (LFM_GRAM_FUSE)
+  // the other run-time knobs, also read once when the context is created
+  int64_t w4min = 6144;   // LFM_W4_MIN: bulk super-panels while the trailing matrix has this many rows
+  int64_t w2min = -1;     // LFM_W2_MIN: w = 2 down to this many rows (-1: 5120 schedule 3, else 4096)
+  int w0 = 1;             // LFM_W0: width of schedule 3's first super-panel
+  int helper = 1;         // LFM_HELPER: schedule 3's side-CU helper
+  double helper_tc = 700, helper_min = 1200;  // LFM_HELPER_TC / LFM_HELPER_MIN, microseconds
+  bool s3_fallback = true;   // LFM_S3_FALLBACK: re-run a stalled schedule-3 call on schedule 1
+  double rccl_timeout_s = 300.0;  // LFM_RCCL_TIMEOUT_S: bound on every farm collective wait
+  int farm_stall_ms = 0;  // LFM_DEBUG_FARM_STALL_MS: test stand-in for a late peer rank
+  bool small_kernarg = true;  // LFM_SMALL_KERNARG: small batches' table in the kernel arguments
   double* gtab = nullptr; size_t gtab_bytes = 0; // gradient tables (grid layout)
   double* result = nullptr;                      // [0..] scalar results
   double* gacc = nullptr; size_t gacc_bytes = 0; // gradient accumulators + output

@@ -197,11 +197,16 @@ def test_allgather_wait_is_bounded_and_drops_the_communicator(monkeypatch):
     from dis_project_amd import _lib
 
     monkeypatch.setenv("LFM_RCCL_TIMEOUT_S", "1")
+    ok = _lib.Context(0)
+    try:
+        g = farm.RcclGather(ok, 1, 0, farm.RcclGather.unique_id(ok))
+        np.testing.assert_array_equal(g(np.array([1.0, 2.0])), [1.0, 2.0])
+    finally:
+        ok.close()
+    monkeypatch.setenv("LFM_DEBUG_FARM_STALL_MS", "6000")  # read when a context is created
     ctx = _lib.Context(0)
     try:
-        g = farm.RcclGather(ctx, 1, 0, farm.RcclGather.unique_id(ctx))
-        np.testing.assert_array_equal(g(np.array([1.0, 2.0])), [1.0, 2.0])
-        monkeypatch.setenv("LFM_DEBUG_FARM_STALL_MS", "6000")
+        farm.RcclGather(ctx, 1, 0, farm.RcclGather.unique_id(ctx))
         send = np.array([3.0, 4.0])
         recv = np.full(2, -7.0)
         t0 = time.monotonic()
@@ -216,7 +221,6 @@ def test_allgather_wait_is_bounded_and_drops_the_communicator(monkeypatch):
         waited = float(re.search(r"timed out after ([0-9.]+) s", msg).group(1))
         assert 0.99 <= waited < 1.5, msg
         assert dt < 9.0, dt
-        monkeypatch.delenv("LFM_DEBUG_FARM_STALL_MS")
         assert ctx.lib.lfm_farm_allgather_f64(ctx.handle, _lib.dptr(send), 2,
                                               _lib.dptr(recv)) == _lib.LFM_E_STATE
         ctx.check(ctx.lib.lfm_ctx_synchronize(ctx.handle))  # the stall drains; nothing else
@@ -422,3 +426,27 @@ def test_resident_batch_mixes_grid_and_scattered_layouts():
         np.testing.assert_allclose(ev(models), _oracle_eval(models, datasets), rtol=1e-9)
     finally:
         ev.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kernarg,reps", [("0", 1), ("1", 2), ("0", 2)])
+def test_resident_batch_memory_path_follows_changed_hyperparameters(monkeypatch, kernarg, reps):
+    """The resident batch's memory path (more than 16 problems, or LFM_SMALL_KERNARG=0: the
+    problem table in HBM and the packed hyperparameters read by the kernel from the batch's
+    coherent pinned buffer): consecutive calls with changed hyperparameters each
+    return the oracle's values at 1e-9, never a stale line of the previous call's."""
+    from dis_project_amd import _lib
+
+    monkeypatch.setenv("LFM_SMALL_KERNARG", kernarg)
+    models, datasets = farm.workload("c5")
+    models, datasets = models * reps, datasets * reps  # reps = 2: 30 problems, past the 16
+    ctx = _lib.Context(0)  # the knob is read when the context is created
+    ev = farm.BatchEvaluator(ctx, datasets)
+    try:
+        for k in range(4):
+            moved = [m.replace(l=m.l * (1.0 + 0.07 * k), true_s=m.true_s * (1.0 - 0.05 * k),
+                               obs_stddev=m.obs_stddev * (1.0 + 0.1 * k)) for m in models]
+            np.testing.assert_allclose(ev(moved), _oracle_eval(moved, datasets), rtol=1e-9)
+    finally:
+        ev.close()
+        ctx.close()

@@ -171,7 +171,7 @@ def test_mll_n16384_other_schedules_vs_golden(full, env, monkeypatch):
     work = configs.c2()
     x = np.ascontiguousarray(work.data.X)
     y = np.ascontiguousarray(work.data.y.reshape(-1))
-    ctx = _lib.Context(0)  # schedule knobs are read when a context is created / per call
+    ctx = _lib.Context(0)  # knobs are read when a context is created
     try:
         out = np.empty(1)
         hp = work.model.hyp()
@@ -207,44 +207,6 @@ def test_serialised_schedule3_is_bit_identical(monkeypatch, G, T):
         finally:
             ctx.close()
     assert vals[0] == vals[1], vals
-
-
-@pytest.mark.parametrize("G,T,steal,extra", [(10, 256, 8, 4), (16, 256, 24, 24),
-                                             (64, 256, 112, 24), (64, 256, 56, 64)])
-def test_rest_stealing_is_bit_identical(monkeypatch, G, T, steal, extra):
-    """Rest units claimed across XCDs (LFM_STEAL / LFM_STEAL_EXTRA, read per call) run the same
-    units with the same arithmetic: the MLL equals the static deal's bit for bit and the
-    gradient's bordered factorisation agrees to 1e-12 (its reductions are order-dependent);
-    no call falls back to schedule 1."""
-    from dis_project_amd import _lib, configs
-
-    monkeypatch.setenv("LFM_SCHED", "3")
-    work = configs.grid_workload("steal", G, T, seed_params=9, seed_y=10)
-    x = np.ascontiguousarray(work.data.X)
-    y = np.ascontiguousarray(work.data.y.reshape(-1))
-    hp = work.model.hyp()
-    ng = 3 * work.model.num_genes + 2
-    ctx = _lib.Context(0)
-    try:
-        vals, grads = [], []
-        for on in (False, True):
-            monkeypatch.setenv("LFM_STEAL", str(steal) if on else "0")
-            monkeypatch.setenv("LFM_STEAL_EXTRA", str(extra))
-            out, gv = np.empty(1), np.empty(ng)
-            ctx.check(ctx.lib.lfm_mll_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
-                                          hp.ref, 0, _lib.dptr(out)))
-            vals.append(out[0])
-            if G <= 16:
-                ctx.check(ctx.lib.lfm_mll_grad_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y),
-                                                   x.shape[0], hp.ref, 1, _lib.dptr(out),
-                                                   _lib.dptr(gv)))
-                grads.append(gv.copy())
-        assert vals[0] == vals[1], vals
-        if grads:  # the gradient's reductions sum in arrival order: equal to 1e-12
-            assert np.max(np.abs(grads[1] - grads[0])) <= 1e-12 * np.max(np.abs(grads[0]))
-        assert ctx.fallbacks == 0
-    finally:
-        ctx.close()
 
 
 @pytest.mark.parametrize("G,T", [(4, 256), (64, 256)])
@@ -320,19 +282,23 @@ def test_side_cu_helper_is_bit_identical_and_flops_conserved(c2_dev, monkeypatch
     helper's share exactly)."""
     from dis_project_amd import _lib
 
-    ctx, work, dx, dy = c2_dev
+    _, work, dx, dy = c2_dev
     res = {}
     for on in ("1", "0"):
-        monkeypatch.setenv("LFM_HELPER", on)  # read per call
-        v = np.empty(1)
-        ctx.check(ctx.lib.lfm_mll_f64_dev(ctx.handle, dx, dy, work.n, work.model.hyp().ref, 0,
-                                          _lib.dptr(v)))  # warm
-        ctx.profile_reset()
-        ctx.profile(True)
-        ctx.check(ctx.lib.lfm_mll_f64_dev(ctx.handle, dx, dy, work.n, work.model.hyp().ref, 0,
-                                          _lib.dptr(v)))
-        ctx.profile(False)
-        st = ctx.profile_read()
+        monkeypatch.setenv("LFM_HELPER", on)
+        ctx = _lib.Context(0)  # knobs are read when a context is created
+        try:
+            v = np.empty(1)
+            ctx.check(ctx.lib.lfm_mll_f64_dev(ctx.handle, dx, dy, work.n, work.model.hyp().ref, 0,
+                                              _lib.dptr(v)))  # warm
+            ctx.profile_reset()
+            ctx.profile(True)
+            ctx.check(ctx.lib.lfm_mll_f64_dev(ctx.handle, dx, dy, work.n, work.model.hyp().ref, 0,
+                                              _lib.dptr(v)))
+            ctx.profile(False)
+            st = ctx.profile_read()
+        finally:
+            ctx.close()
         res[on] = (float(v[0]), st.get("syrk", {}).get("flops", 0.0),
                    st.get("syrk_side", {}).get("flops", 0.0),
                    st.get("syrk_side", {}).get("launches", 0))
@@ -352,14 +318,18 @@ def test_side_cu_helper_gradient_bit_identical(monkeypatch):
     work = configs.c2()
     x = np.ascontiguousarray(work.data.X)
     y = np.ascontiguousarray(work.data.y.reshape(-1))
-    ctx = _lib.get_context(0)
     G = work.model.num_genes
     out = {}
     for on in ("1", "0"):
         monkeypatch.setenv("LFM_HELPER", on)
-        gv, val = np.empty(3 * G + 2), np.empty(1)
-        ctx.check(ctx.lib.lfm_mll_grad_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
-                                           work.model.hyp().ref, 1, _lib.dptr(val), _lib.dptr(gv)))
+        ctx = _lib.Context(0)  # knobs are read when a context is created
+        try:
+            gv, val = np.empty(3 * G + 2), np.empty(1)
+            ctx.check(ctx.lib.lfm_mll_grad_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
+                                               work.model.hyp().ref, 1, _lib.dptr(val),
+                                               _lib.dptr(gv)))
+        finally:
+            ctx.close()
         out[on] = (float(val[0]), gv.copy())
     assert np.isfinite(out["1"][0]) and out["1"][0] == out["0"][0]
     g1, g0 = out["1"][1], out["0"][1]
@@ -377,51 +347,24 @@ def test_side_cu_helper_forced_on_every_step(monkeypatch, G, T):
     work = configs.grid_workload("helper", G, T, seed_params=2, seed_y=3)
     x = np.ascontiguousarray(work.data.X)
     y = np.ascontiguousarray(work.data.y.reshape(-1))
-    ctx = _lib.get_context(0)
     out = {}
     for env in ({"LFM_HELPER": "0"},
                 {"LFM_HELPER": "1", "LFM_HELPER_MIN": "0", "LFM_HELPER_TC": "0"}):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
-        v = np.empty(1)
-        ctx.profile_reset()
-        ctx.profile(True)
-        ctx.check(ctx.lib.lfm_mll_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
-                                      work.model.hyp().ref, 0, _lib.dptr(v)))
-        ctx.profile(False)
-        helpers = ctx.profile_read().get("syrk_side", {}).get("launches", 0)
+        ctx = _lib.Context(0)  # knobs are read when a context is created
+        try:
+            v = np.empty(1)
+            ctx.profile_reset()
+            ctx.profile(True)
+            ctx.check(ctx.lib.lfm_mll_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
+                                          work.model.hyp().ref, 0, _lib.dptr(v)))
+            ctx.profile(False)
+            helpers = ctx.profile_read().get("syrk_side", {}).get("launches", 0)
+        finally:
+            ctx.close()
         out[env["LFM_HELPER"]] = (float(v[0]), helpers)
     assert out["0"][1] == 0 and out["1"][1] > 0  # the forced run used helper launches
     assert np.isfinite(out["1"][0]) and out["1"][0] == out["0"][0]
 
 
-
-@pytest.mark.parametrize("G,T", [(16, 256), (64, 256), (10, 200)])
-def test_tr32_units_are_bit_identical(monkeypatch, G, T):
-    """32-row ahead / rest units in the w = 1 steps (LFM_TR32=1, step_kernel32: the same
-    16x16x4 MFMA sequence per output element as the 64-row units) give the MLL bit for bit;
-    the chain-input counts (xtarget, per-tile a_done) follow the unit size; N = 4096, the
-    N = 16384 bench workload and a non-aligned N = 2000 layout; also with the helper forced
-    onto every eligible step (the helper stays on 64-row units)."""
-    from dis_project_amd import _lib, configs
-
-    work = configs.grid_workload("tr32", G, T, seed_params=2, seed_y=3)
-    x = np.ascontiguousarray(work.data.X)
-    y = np.ascontiguousarray(work.data.y.reshape(-1))
-    ctx = _lib.Context(0)
-    try:
-        out = {}
-        for tr32, helper_min in (("0", None), ("1", None), ("1", "0")):
-            monkeypatch.setenv("LFM_TR32", tr32)
-            if helper_min is None:
-                monkeypatch.delenv("LFM_HELPER_MIN", raising=False)
-            else:
-                monkeypatch.setenv("LFM_HELPER_MIN", helper_min)
-            v = np.empty(1)
-            ctx.check(ctx.lib.lfm_mll_f64(ctx.handle, _lib.dptr(x), _lib.dptr(y), x.shape[0],
-                                          work.model.hyp().ref, 0, _lib.dptr(v)))
-            out[(tr32, helper_min)] = float(v[0])
-        assert np.isfinite(out[("0", None)])
-        assert out[("1", None)] == out[("0", None)] == out[("1", "0")], out
-    finally:
-        ctx.close()
