@@ -33,7 +33,7 @@ LFM_E_OOM = 4
 LFM_E_RCCL = 5
 LFM_E_STATE = 6
 LFM_E_TIMEOUT = 7
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 LFM_UPLO_FULL = 0
 LFM_UPLO_LOWER = 1
@@ -79,6 +79,19 @@ class LfmProblem(ctypes.Structure):
     _fields_ = [("x", _dptr), ("y", _dptr), ("n", c_int64), ("hyp", LfmHyp)]
 
 
+class LfmAdam(ctypes.Structure):
+    """lfm_adam (include/lfm.h): optax.adam and JaxTrainer.fit's epoch handling."""
+    _fields_ = [
+        ("learning_rate", c_double),
+        ("b1", c_double),
+        ("b2", c_double),
+        ("eps", c_double),
+        ("eps_root", c_double),
+        ("num_steps_per_epoch", c_int64),
+        ("fix_params", c_int),
+    ]
+
+
 class LfmKstat(ctypes.Structure):
     _fields_ = [
         ("name", c_char * 32),
@@ -122,6 +135,10 @@ PRODUCT_SIGNATURES = [
     ("lfm_batch_destroy", c_int, [c_void_p]),
     ("lfm_batch_hyp_size", c_int, [c_void_p, POINTER(c_int64)]),
     ("lfm_batch_mll_f64", c_int, [_c_ctx, c_void_p, _dptr, c_int, _dptr, _dptr]),
+    ("lfm_batch_mll_grad_f64", c_int, [_c_ctx, c_void_p, _dptr, c_int, _dptr, _dptr, _dptr]),
+    ("lfm_batch_fit_f64", c_int,
+     [_c_ctx, c_void_p, POINTER(LfmAdam), c_int, c_int64, c_int64, _dptr, _dptr, _dptr, _dptr,
+      _dptr]),
     ("lfm_log_prob_f64", c_int, [_c_ctx, _dptr, _dptr, c_int64, c_int64, _dptr, _dptr]),
     ("lfm_h_f64", c_int,
      [_c_ctx, POINTER(LfmHyp), POINTER(c_int64), POINTER(c_int64), _dptr, _dptr, c_int64, _dptr]),
@@ -168,7 +185,7 @@ DIAG_SIGNATURES = [
 
 # kernel classes in lfm_profile_read order (lfm_internal.h KClass)
 KCLASSES = ["tables", "gram_grid", "gram_direct", "augment", "potrf", "trsm", "syrk",
-            "finalize", "small_mll", "mean", "grad", "panel", "syrk_side"]
+            "finalize", "small_mll", "mean", "grad", "panel", "syrk_side", "small_grad"]
 
 _lib = None
 _diag = None

@@ -35,7 +35,7 @@ const char* const kClassName[K_NCLASS] = {"tables",   "gram_grid", "gram_direct"
                                           "augment",  "potrf",     "trsm",
                                           "syrk",     "finalize",  "small_mll",
                                           "mean",     "grad",      "panel",
-                                          "syrk_side"};
+                                          "syrk_side", "small_grad"};
 
 int set_err(lfm_ctx* ctx, int code, const std::string& msg) {
   if (ctx) ctx->err = msg;
@@ -1220,6 +1220,13 @@ struct lfm_batch {
   bool use_args = false;
   std::vector<SmallProb> table;      // host copy of the problem table
   std::vector<int> dsb_off, sc_off;  // each problem's offsets in the packed hyperparameters
+  int* doffs = nullptr;              // device: dsb_off then sc_off (the gradient / fit kernels)
+  double* hgrad = nullptr;           // pinned (in hbuf): the gradient, packed as hyp [nhyp]
+  size_t lds_grad = 0, lds_fit = 0;  // the gradient / fit launches' LDS (0: not possible)
+  // the fit's device buffers (grown on demand): raw mu nu [3 nhyp] | bias [2 nsteps] |
+  // history [nsteps nprob] | status [nprob]
+  char* fitbuf = nullptr;
+  size_t fit_bytes = 0;
 };
 
 int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_batch** out) {
@@ -1251,13 +1258,14 @@ int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_
   b->nhyp = nhyp;
   b->maxn = maxn;
   b->maxg = maxg;
-  const size_t bytes_d = round_up(nd * 8, 16), bytes_p = (size_t)nprob * sizeof(SmallProb);
-  hipError_t e = hipMalloc((void**)&b->dmem, bytes_d + bytes_p);
+  const size_t bytes_d = round_up(nd * 8, 16), bytes_p = round_up((size_t)nprob * sizeof(SmallProb), 16);
+  const size_t bytes_o = 2 * (size_t)nprob * sizeof(int);
+  hipError_t e = hipMalloc((void**)&b->dmem, bytes_d + bytes_p + bytes_o);
   if (e != hipSuccess) return hip_fail(ctx, e, "lfm_batch_create: device buffer");
   // coherent (fine-grained): the kernel reads the hyperparameters a call has just written and
   // its result / status stores must reach the host's spin without a stream synchronise,
   // whatever HIP_HOST_COHERENT says
-  e = hipHostMalloc((void**)&b->hbuf, (size_t)(nhyp + 2 * nprob) * 8, hipHostMallocCoherent);
+  e = hipHostMalloc((void**)&b->hbuf, (size_t)(2 * nhyp + 2 * nprob) * 8, hipHostMallocCoherent);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&b->done, hipEventDisableTiming);
   if (e != hipSuccess) {
     hipFree(b->dmem);
@@ -1265,6 +1273,8 @@ int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_
     return hip_fail(ctx, e, "lfm_batch_create: pinned buffer");
   }
   b->dprobs = reinterpret_cast<SmallProb*>(b->dmem + bytes_d);
+  b->doffs = reinterpret_cast<int*>(b->dmem + bytes_d + bytes_p);
+  b->hgrad = b->hbuf + nhyp + 2 * nprob;
   std::vector<double> hd((size_t)nd);
   std::vector<SmallProb> table((size_t)nprob);
   const double* dd = reinterpret_cast<const double*>(b->dmem);
@@ -1294,9 +1304,20 @@ int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_
   b->use_args = ctx->small_kernarg && nprob <= SMALL_ARG_PROBS &&
                 nhyp <= SMALL_ARG_HYP;
   b->table = table;
+  // the gradient / fit kernels: every problem's augmented matrix on one wave (n + 1 <= 64) and
+  // its LDS map within a CU's 160 KB
+  if (maxn <= SMALL_GRAD_MAX) {
+    b->lds_grad = small_grad_lds(table.data(), (int)nprob, 0);
+    b->lds_fit = small_grad_lds(table.data(), (int)nprob, 1);
+  }
+  std::vector<int> offs(b->dsb_off);
+  offs.insert(offs.end(), b->sc_off.begin(), b->sc_off.end());
   e = hipMemcpyAsync(b->dmem, hd.data(), (size_t)nd * 8, hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess)
-    e = hipMemcpyAsync(b->dprobs, table.data(), bytes_p, hipMemcpyHostToDevice, ctx->stream);
+    e = hipMemcpyAsync(b->dprobs, table.data(), (size_t)nprob * sizeof(SmallProb),
+                       hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(b->doffs, offs.data(), bytes_o, hipMemcpyHostToDevice, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) {
     hipFree(b->dmem);
@@ -1324,6 +1345,7 @@ int lfm_batch_destroy(lfm_batch* batch) {
     hipEventDestroy(batch->done);
   }
   hipFree(batch->dmem);
+  if (batch->fitbuf) hipFree(batch->fitbuf);
   hipHostFree(batch->hbuf);
   delete batch;
   return LFM_OK;
@@ -1387,6 +1409,163 @@ int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int neg
     if (s) worst = s;
   }
   if (worst) set_err(ctx, LFM_E_NOT_PD, "Cholesky failed: non-positive pivot in a batch problem");
+  return worst;
+}
+
+// The host side of a call whose kernel writes results and status words into the batch's
+// pinned buffer: spin on the status words (each written last, after a system-scope fence, by
+// its workgroup), past 20 ms or while profiling synchronise the stream instead (which also
+// surfaces a kernel fault).
+namespace {
+int batch_wait(lfm_ctx* ctx, int64_t np, const int* hst) {
+  bool landed = false;
+  if (!ctx->prof) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      landed = true;
+      for (int64_t q = 0; q < np && landed; ++q)
+        landed = __atomic_load_n(&hst[q], __ATOMIC_ACQUIRE) != -1;
+      if (landed || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+      __builtin_ia32_pause();
+    }
+  }
+  return landed ? LFM_OK : finish(ctx);
+}
+}  // namespace
+
+int lfm_batch_mll_grad_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative,
+                           double* value, double* grad, int* status) {
+  if (!ctx) return LFM_E_ARG;
+  if (!batch || !hyp || !value || !grad)
+    return set_err(ctx, LFM_E_ARG, "batch / hyp / value / grad is NULL");
+  if (batch->device != ctx->device) return set_err(ctx, LFM_E_ARG, "batch of another device");
+  if (!batch->lds_grad)
+    return set_err(ctx, LFM_E_ARG, "lfm_batch_mll_grad_f64: every problem needs n <= 63 (one "
+                                   "wave per augmented matrix); use lfm_mll_grad_f64");
+  DeviceGuard g(ctx->device);
+  const int64_t np = batch->nprob;
+  double* hres = batch->hbuf + batch->nhyp;
+  int* hst = reinterpret_cast<int*>(hres + np);
+  for (int64_t q = 0; q < np; ++q) hst[q] = -1;
+  int r;
+  if (batch->use_args) {
+    SmallArgs a;
+    std::memcpy(a.probs, batch->table.data(), (size_t)np * sizeof(SmallProb));
+    std::memcpy(a.hyp, hyp, (size_t)batch->nhyp * 8);
+    std::memcpy(a.dsb_off, batch->dsb_off.data(), (size_t)np * sizeof(int));
+    std::memcpy(a.sc_off, batch->sc_off.data(), (size_t)np * sizeof(int));
+    a.tabs = 1;
+    r = launch_small_grad(ctx, &a, nullptr, nullptr, (int)np, batch->lds_grad, negative, hres,
+                          batch->hgrad, hst);
+  } else {
+    std::memcpy(batch->hbuf, hyp, (size_t)batch->nhyp * 8);
+    r = launch_small_grad(ctx, nullptr, batch->dprobs, batch->doffs, (int)np, batch->lds_grad,
+                          negative, hres, batch->hgrad, hst);
+  }
+  if (r) return r;
+  hipEventRecord(batch->done, ctx->stream);
+  r = batch_wait(ctx, np, hst);
+  if (r) return r;
+  int worst = LFM_OK;
+  std::memcpy(grad, batch->hgrad, (size_t)batch->nhyp * 8);
+  for (int64_t q = 0; q < np; ++q) {
+    value[q] = hres[q];
+    const int s = hst[q] ? LFM_E_NOT_PD : LFM_OK;
+    if (status) status[q] = s;
+    if (s) worst = s;
+  }
+  if (worst) set_err(ctx, LFM_E_NOT_PD, "Cholesky failed: non-positive pivot in a batch problem");
+  return worst;
+}
+
+int lfm_batch_fit_f64(lfm_ctx* ctx, lfm_batch* batch, const lfm_adam* opt, int negative,
+                      int64_t step0, int64_t nsteps, double* raw, double* mu, double* nu,
+                      double* history, int* status) {
+  if (!ctx) return LFM_E_ARG;
+  if (!batch || !opt || !raw || !mu || !nu || (nsteps > 0 && !history) || step0 < 0 ||
+      nsteps < 0 || opt->num_steps_per_epoch < 1)
+    return set_err(ctx, LFM_E_ARG, "bad fit arguments");
+  if (batch->device != ctx->device) return set_err(ctx, LFM_E_ARG, "batch of another device");
+  if (!batch->lds_fit)
+    return set_err(ctx, LFM_E_ARG, "lfm_batch_fit_f64: every problem needs n <= 63");
+  if (nsteps == 0) return LFM_OK;
+  DeviceGuard g(ctx->device);
+  const int64_t np = batch->nprob, nh = batch->nhyp;
+  const size_t b_par = 3 * (size_t)nh * 8, b_bias = 2 * (size_t)nsteps * 8;
+  const size_t b_hist = (size_t)nsteps * np * 8, b_st = (size_t)np * sizeof(int);
+  const size_t need = b_par + b_bias + b_hist + b_st;
+  if (batch->fit_bytes < need) {
+    hipStreamSynchronize(ctx->stream);
+    if (batch->fitbuf) hipFree(batch->fitbuf);
+    batch->fitbuf = nullptr;
+    batch->fit_bytes = 0;
+    hipError_t e = hipMalloc((void**)&batch->fitbuf, need);
+    if (e != hipSuccess) return hip_fail(ctx, e, "lfm_batch_fit_f64: device buffer");
+    batch->fit_bytes = need;
+  }
+  double* d_par = reinterpret_cast<double*>(batch->fitbuf);
+  double* d_bias = d_par + 3 * nh;
+  double* d_hist = d_bias + 2 * nsteps;
+  int* d_st = reinterpret_cast<int*>(d_hist + nsteps * np);
+  // optax's bias corrections 1 - b^count, count = step0 + s + 1, with the host's pow (the
+  // restatement's numbers: dis_project_amd/trainer.py adam)
+  std::vector<double> bias((size_t)2 * nsteps), par((size_t)3 * nh);
+  for (int64_t s = 0; s < nsteps; ++s) {
+    const double count = (double)(step0 + s + 1);
+    bias[2 * s] = 1.0 - std::pow(opt->b1, count);
+    bias[2 * s + 1] = 1.0 - std::pow(opt->b2, count);
+  }
+  std::memcpy(par.data(), raw, nh * 8);
+  std::memcpy(par.data() + nh, mu, nh * 8);
+  std::memcpy(par.data() + 2 * nh, nu, nh * 8);
+  hipError_t e = hipMemcpyAsync(d_par, par.data(), b_par, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(d_bias, bias.data(), b_bias, hipMemcpyHostToDevice, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "lfm_batch_fit_f64: upload");
+  SmallFitLaunch f{};
+  f.probs = batch->dprobs;
+  f.offs = batch->doffs;
+  f.nprob = (int)np;
+  f.raw = d_par;
+  f.mu = d_par + nh;
+  f.nu = d_par + 2 * nh;
+  f.history = d_hist;
+  f.bias = d_bias;
+  f.status = d_st;
+  f.lr = opt->learning_rate;
+  f.b1 = opt->b1;
+  f.b2 = opt->b2;
+  f.eps = opt->eps;
+  f.eps_root = opt->eps_root;
+  f.step0 = step0;
+  f.nsteps = nsteps;
+  f.spe = opt->num_steps_per_epoch;
+  f.fix = opt->fix_params != 0;
+  f.negative = negative;
+  int r = launch_small_fit(ctx, f, batch->lds_fit);
+  if (r) return r;
+  hipEventRecord(batch->done, ctx->stream);
+  std::vector<int> st((size_t)np);
+  e = hipMemcpyAsync(par.data(), d_par, b_par, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(history, d_hist, b_hist, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(st.data(), d_st, b_st, hipMemcpyDeviceToHost, ctx->stream);
+  if (e != hipSuccess) return hip_fail(ctx, e, "lfm_batch_fit_f64: download");
+  r = finish(ctx);
+  if (r) return r;
+  // the packed layout's jitter slots pass through unchanged (a static field, model.py:64)
+  std::memcpy(raw, par.data(), nh * 8);
+  std::memcpy(mu, par.data() + nh, nh * 8);
+  std::memcpy(nu, par.data() + 2 * nh, nh * 8);
+  int worst = LFM_OK;
+  for (int64_t q = 0; q < np; ++q) {
+    if (status) status[q] = st[q];
+    if (st[q]) worst = LFM_E_NOT_PD;
+  }
+  if (worst)
+    set_err(ctx, LFM_E_NOT_PD, "Cholesky failed during the fit of a batch problem (its loss "
+                               "and parameters are NaN from that step on, as JAX's)");
   return worst;
 }
 

@@ -71,14 +71,6 @@ __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
 
-// Value of v held by `lane` (compile-time lane after unrolling), broadcast to the wave.
-__device__ __forceinline__ double rdl(double v, int lane) {
-  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffu), lane);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
-
 // Value of v held by lane `src` (0..15, compile-time) of each 16-lane row, broadcast to the
 // row: DPP row_newbcast (VGPR to VGPR; no SGPR round trip as with v_readlane).
 template <int SRC>
@@ -2749,363 +2741,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     hipStreamWaitEvent(ctx->stream, ev[2 * S + 2], 0);
   }
   return hip_fail(ctx, hipGetLastError(), "finalize_kernel");
-}
-
-// ------------------------------------------------------- small-N batch
-// One workgroup per problem: Sigma (+ residual row) built and factored in LDS.
-// Used for n <= SMALL_MAX (configs 1 and 5: N = 35, 28).
-
-// Factor of the augmented (n + 1)-row matrix on one wave (small_mll_kernel, n + 1 <= 64): lane
-// r holds row r (row n: the residual) in registers as a window d[q] = A[r][c + q] over the
-// columns from the current one c on, right-looking. Column c: every lane scales its entry into
-// L[r][c] and puts it in colbuf[r] (LDS); every lane then reads L[c + q][c] back (all reads
-// issued at once) and updates and shifts its window in one step, d[q - 1] = d[q] - L[r][c]
-// L[c + q][c]. The pivot of column c + 1 is lane c + 1's new d[0], which that lane forms from
-// its own L[c + 1][c] without the LDS round trip, so its reciprocal square root (v_rsq_f64 and
-// one Newton step, as the large factor's leaf) is issued alongside column c's update. The
-// window narrows as columns retire (W = 64 or 32, then 24, 16, 12, 8: small_next_w), so a
-// column costs about as many fused multiply-adds as it has live entries; the column loops stay rolled
-// (fully unrolled, the straight-line code was instruction-fetch bound). Per element the terms
-// are summed in the same order (k = 0, 1, ...) as before. colbuf: >= 128 doubles, zero from
-// index 64 on. Lane r ends with its pivot (r < n) and residual entry z[r] = L[n][r].
-struct SmallFactor {
-  int n, r;
-  bool act;
-  double* colbuf;
-  double dc, y;      // the current column's pivot input and 1 / sqrt of it
-  double mp, mz;     // this lane's pivot and z entry
-  int bad;
-};
-// window widths of the phases: 64 48 32 24 16 12 8
-template <int W>
-constexpr int small_next_w() {
-  return W == 64 ? 48 : W == 48 ? 32 : W == 32 ? 24 : W == 24 ? 16 : W == 16 ? 12 : 8;
-}
-template <int W>
-__device__ __forceinline__ void small_factor_phase(double (&d)[W], int c, SmallFactor& f) {
-  // phase W: the columns while more than the next width of them remain (the last phase: all)
-  constexpr int WN = small_next_w<W>();
-  const int cend = W > 8 ? max(c, f.n - WN) : f.n;
-#pragma unroll 1
-  for (; c < cend; ++c) {
-    if (!(f.dc > 0.0) && f.bad == 0) f.bad = c + 1;
-    const double lc = f.r == c ? f.dc * f.y : d[0] * f.y;  // L[r][c]; lane c: the pivot
-    if (f.r == c) f.mp = lc;
-    const double zc = rdl(lc, f.n);  // L[n][c] = z[c]
-    if (f.r == c) f.mz = zc;
-    // the next pivot: lane c + 1's d[1] - L[c + 1][c]^2 (past the last column: unused)
-    const double dn = rdl(fma(-lc, lc, d[1]), c + 1);
-    const double yn = rsqrt_1nr(dn);
-    f.colbuf[f.r] = (f.act && f.r > c) ? lc : 0.0;
-    // the wave's LDS operations complete in order: the reads see every lane's store
-    asm volatile("" ::: "memory");
-    double col[W - 1];
-#pragma unroll
-    for (int q = 1; q < W; ++q) col[q - 1] = f.colbuf[c + q];
-    asm volatile("" ::: "memory");  // every read issued before the first use
-#pragma unroll
-    for (int q = 1; q < W; ++q) d[q - 1] = fma(-lc, col[q - 1], d[q]);
-    d[W - 1] = 0.0;
-    f.dc = dn;
-    f.y = yn;
-  }
-  if constexpr (W > 8)
-    if (c < f.n) small_factor_phase<WN>(*reinterpret_cast<double(*)[WN]>(&d[0]), c, f);
-}
-template <int MR>
-__device__ __forceinline__ void small_factor_regs(const double* __restrict__ sm, int ld, int n,
-                                                  int M, double* colbuf, double* piv_r,
-                                                  double* z_r, int* bad_out) {
-  SmallFactor f;
-  f.n = n;
-  f.r = threadIdx.x;  // wave 0
-  f.act = f.r < M;
-  f.colbuf = colbuf;
-  double d[MR];
-#pragma unroll
-  for (int q = 0; q < MR; ++q) d[q] = (f.act && q <= f.r && q < n) ? sm[f.r * ld + q] : 0.0;
-  f.dc = rdl(d[0], 0);
-  f.y = rsqrt_1nr(f.dc);
-  f.mp = f.mz = 0.0;
-  f.bad = 0;
-  small_factor_phase<MR>(d, 0, f);
-  *piv_r = f.mp;
-  *z_r = f.mz;
-  *bad_out = f.bad;
-}
-
-// timing experiment (make EXTRA=-DLFM_SMALL_SKIP=k; results invalid, never in the product
-// build): 1 no factor, 2 no gram pairs, 3 neither, 4 no pinned reads (constant hyperparameters)
-#ifndef LFM_SMALL_SKIP
-#define LFM_SMALL_SKIP 0
-#endif
-// timing experiment (make EXTRA=-DLFM_SMALL_STAMPS=1; results of problems 1-4 invalid): block 0
-// writes its phase times (µs from its start) into out[1..4]
-#ifndef LFM_SMALL_STAMPS
-#define LFM_SMALL_STAMPS 0
-#endif
-__device__ __forceinline__ void small_body(const SmallProb P, int negative,
-                                           double* __restrict__ out, int* __restrict__ status,
-                                           int tabs, unsigned long long st0) {
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int n = P.n, M = n + 1, ld = n + 2, G = P.G;
-  const int tid = threadIdx.x;
-  double* red = sm + (size_t)M * ld;  // [8] reduction scratch + [1] flag
-  // hyperparameters staged in LDS (they may live in pinned host memory: read once)
-  double* hyp = red + 16;             // D S B (3G), l, obs_stddev, jitter
-  // past the hyperparameters and the tables: the one-wave factor's column buffer (128), then
-  // x (3n) and y (n), loaded here beside the hyperparameters so that no later phase waits on
-  // HBM (the launch's LDS counts them)
-  double* colbuf = hyp + 3 * G + 3 + (tabs ? 3 * G + n + n * G : 0);
-  double* xs = colbuf + 128;
-  double* ys = xs + 3 * n;
-  for (int i = tid; i < 3 * G; i += 256) hyp[i] = LFM_SMALL_SKIP == 4 ? 0.5 : P.dsb[i];
-  if (tid < 3) hyp[3 * G + tid] = LFM_SMALL_SKIP == 4 ? (tid == 0 ? 2.5 : 1.0) : P.sc[tid];
-  for (int i = tid; i < 3 * n; i += 256) xs[i] = P.x[i];
-  for (int i = tid; i < n; i += 256) ys[i] = P.y[i];
-  __syncthreads();
-  const unsigned long long st1 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
-  const HypDev h{hyp, hyp + G, hyp + 2 * G, G, hyp[3 * G]};
-  const double jitter = hyp[3 * G + 2], sd = hyp[3 * G + 1];
-  const double noise = sd * sd;  // objectives.py:66
-  if (P.T > 0) {
-    // grid layout: the per-gene tables of lfm_gram.hip (tables_kernel) in LDS, then each lower
-    // element with gram_grid_kernel's operations (~10 FMAs instead of 2 erf + 3 exp)
-    double* gt = ys + n;
-    const int T = P.T, W = 2 * T - 1;
-    const int nt = (int)(2 * (int64_t)G * W + 3 * (int64_t)G * T + (int64_t)G * G);
-    for (int q = tid; q < nt; q += 256) gt[q] = grid_table_entry(h, T, P.dt, P.times, q);
-    __syncthreads();
-    const double* Wt = gt;
-    const double* Xt = Wt + G * W;
-    const double* Pt = Xt + G * W;
-    const double* Et = Pt + G * T;
-    const double* Qt = Et + G * T;
-    const double* Cm = Qt + G * T;
-    const int np = n * (n + 1) / 2;  // the lower triangle, row by row
-    for (int q = tid; q < np; q += 256) {
-      int i = (int)((sqrtf(8.0f * (float)q + 1.0f) - 1.0f) * 0.5f);
-      while (i * (i + 1) / 2 > q) --i;
-      while ((i + 1) * (i + 2) / 2 <= q) ++i;
-      const int c = q - i * (i + 1) / 2;
-      const int bi = i / T, tau = i - bi * T, j = P.bg[bi];
-      const int bc = c / T, tp = c - bc * T, k = P.bg[bc];
-      const int d = tp - tau;
-      double v = Wt[k * W + (T - 1) + d] + Wt[j * W + (T - 1) - d];
-      v = fma(-Xt[k * W + (T - 1) + d], Pt[k * T + tau], v);
-      v = fma(-Xt[j * W + (T - 1) - d], Pt[j * T + tp], v);
-      v = fma(-(Et[k * T + tp] * Et[j * T + tau]), Qt[k * T + tp] + Qt[j * T + tau], v);
-      v = Cm[j * G + k] * v;
-      if (i == c) v = (v + jitter) + noise;
-      sm[i * ld + c] = v;
-    }
-  } else if (tabs) {
-    // n <= 63 (the launch's LDS holds the tables): gene-gene pairs from KxxTab, the same bits
-    // as kernel_ref with a third of its transcendentals; pairs with a latent row direct
-    double* gam = hyp + 3 * G + 3;
-    double* egg = gam + G;
-    double* erg = egg + G;
-    double* e2 = erg + G;
-    double* e1 = e2 + n;
-    const KxxTab t{gam, egg, erg, e1, e2, G};
-    small_tables(h, xs, n, t, gam, egg, erg, e1, e2);
-    const int np = n * (n + 1) / 2;  // the lower triangle, row by row
-    for (int q = tid; q < np; q += 256) {
-      int i = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
-      while (i * (i + 1) / 2 > q) --i;
-      while ((i + 1) * (i + 2) / 2 <= q) ++i;
-      const int c = q - i * (i + 1) / 2;
-      const double* xa = xs + 3 * i;
-      const double* xb = xs + 3 * c;
-      double v;
-      if (LFM_SMALL_SKIP == 2 || LFM_SMALL_SKIP == 3)
-        v = i == c ? 4.0 : 0.01;
-      else if (flag_int(xa[2]) == 1 && flag_int(xb[2]) == 1)
-        v = kxx_tab(h, t, xa[0], gene_index(xa[1], G), i, xb[0], gene_index(xb[1], G), c);
-      else
-        v = kernel_ref(h, xa[0], xa[1], xa[2], xb[0], xb[1], xb[2]);
-      if (i == c) v = (v + jitter) + noise;
-      sm[i * ld + c] = v;
-    }
-  } else {
-    for (int idx = tid; idx < n * n; idx += 256) {
-      const int i = idx / n, c = idx - i * n;
-      if (c <= i) {
-        const double* xa = xs + 3 * i;
-        const double* xb = xs + 3 * c;
-        double v = kernel_ref(h, xa[0], xa[1], xa[2], xb[0], xb[1], xb[2]);
-        if (i == c) v = (v + jitter) + noise;
-        sm[i * ld + c] = v;
-      }
-    }
-  }
-  const int64_t bs = n / G;
-  for (int c = tid; c < n; c += 256) sm[n * ld + c] = ys[c] - mean_at(h, xs, c, bs);
-  if (tid == 0) red[8] = 0.0;
-  __syncthreads();
-  const unsigned long long st2 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
-  if (M <= 64) {
-    // one wave, the augmented matrix in registers (small_factor_regs); no workgroup barrier
-    // (256-thread barriers were ~60 % of the kernel at n = 28, two per column)
-    if (tid >= 64) return;
-    const int r = tid;
-    double pr, zr;
-    int bad;
-    colbuf[64 + r] = 0.0;
-    if (LFM_SMALL_SKIP == 1 || LFM_SMALL_SKIP == 3) {
-      pr = sm[r * ld + r];
-      zr = sm[n * ld + r];
-      bad = 0;
-    } else if (M <= 32)
-      small_factor_regs<32>(sm, ld, n, M, colbuf, &pr, &zr, &bad);
-    else
-      small_factor_regs<64>(sm, ld, n, M, colbuf, &pr, &zr, &bad);
-    const unsigned long long st3 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
-    double ldp = 0.0, qp = 0.0;
-    if (r < n) {
-      ldp = log(pr);
-      qp = zr * zr;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      ldp += __shfl_xor(ldp, o);
-      qp += __shfl_xor(qp, o);
-    }
-    if (r == 0) {
-      const double two_pi = 6.283185307179586476925;
-      double mll = -0.5 * ((double)n * log(two_pi) + 2.0 * ldp + qp);
-      mll *= negative ? -1.0 : 1.0;
-      if (bad) mll = __builtin_nan("");
-      if (LFM_SMALL_STAMPS && blockIdx.x == 0) {
-        const unsigned long long st4 = __builtin_amdgcn_s_memrealtime();
-        out[1] = (double)(st1 - st0) * 0.01;
-        out[2] = (double)(st2 - st0) * 0.01;
-        out[3] = (double)(st3 - st0) * 0.01;
-        out[4] = (double)(st4 - st0) * 0.01;
-      }
-      if (!LFM_SMALL_STAMPS || blockIdx.x == 0 || blockIdx.x > 4) out[blockIdx.x] = mll;
-      // the status word lands after the result: the host may take it as the problem's
-      // completion (lfm_batch_mll_f64)
-      __threadfence_system();
-      if (status) status[blockIdx.x] = bad;
-    }
-    return;
-  }
-  for (int c = 0; c < n; ++c) {
-    const double d = sm[c * ld + c];
-    const double piv = sqrt(d);
-    const double inv = 1.0 / piv;
-    for (int r = c + 1 + tid; r < M; r += 256) sm[r * ld + c] *= inv;
-    if (tid == 0) {
-      sm[c * ld + c] = piv;
-      if (!(d > 0.0) && red[8] == 0.0) red[8] = (double)(c + 1);
-    }
-    __syncthreads();
-    const int w = M - c - 1;
-    for (int idx = tid; idx < w * w; idx += 256) {
-      const int r = c + 1 + idx / w, q = c + 1 + idx % w;
-      if (q <= r) sm[r * ld + q] -= sm[r * ld + c] * sm[q * ld + c];
-    }
-    __syncthreads();
-  }
-  double ldp = 0.0, qp = 0.0;
-  for (int c = tid; c < n; c += 256) {
-    ldp += log(sm[c * ld + c]);
-    const double z = sm[n * ld + c];
-    qp += z * z;
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    ldp += __shfl_xor(ldp, o);
-    qp += __shfl_xor(qp, o);
-  }
-  if ((tid & 63) == 0) {
-    red[tid >> 6] = ldp;
-    red[4 + (tid >> 6)] = qp;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    const double LD = 2.0 * (red[0] + red[1] + red[2] + red[3]);
-    const double Q = red[4] + red[5] + red[6] + red[7];
-    const double two_pi = 6.283185307179586476925;
-    double mll = -0.5 * ((double)n * log(two_pi) + LD + Q);
-    mll *= negative ? -1.0 : 1.0;
-    int st = 0;
-    if (red[8] != 0.0) {
-      mll = __builtin_nan("");
-      st = (int)red[8];  // 1-based failing pivot
-    }
-    out[blockIdx.x] = mll;
-    __threadfence_system();  // the result before the status word (lfm_batch_mll_f64)
-    if (status) status[blockIdx.x] = st;
-  }
-}
-
-__global__ __launch_bounds__(256) void small_mll_kernel(const SmallProb* __restrict__ probs,
-                                                        int negative, double* __restrict__ out,
-                                                        int* __restrict__ status, int tabs) {
-  const unsigned long long st0 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
-  small_body(probs[blockIdx.x], negative, out, status, tabs, st0);
-}
-
-// The same with the problem table and the hyperparameters in the kernel arguments (a resident
-// batch of at most SMALL_ARG_PROBS problems and SMALL_ARG_HYP hyperparameters): no dependent
-// load of the table from HBM and no read of pinned host memory before the gram.
-__global__ __launch_bounds__(256) void small_mll_kernel_args(SmallArgs a) {
-  const unsigned long long st0 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
-  SmallProb P = a.probs[blockIdx.x];
-  P.dsb = a.hyp + a.dsb_off[blockIdx.x];
-  P.sc = a.hyp + a.sc_off[blockIdx.x];
-  small_body(P, a.negative, a.out, a.status, a.tabs, st0);
-}
-
-static size_t small_lds(int maxn, int maxg, int gridtab, int* tabs_out) {
-  // tables (KxxTab) when every problem has n + 1 <= 64 rows: 3 G + n + n G doubles
-  const int tabs = maxn + 1 <= 64;
-  const size_t tab = tabs ? 3 * (size_t)maxg + maxn + (size_t)maxn * maxg : 0;
-  *tabs_out = tabs;
-  // + 128: the one-wave factor's column buffer (small_factor_regs); + 4 n: x and y; + gridtab:
-  // the grid-layout tables
-  return ((size_t)(maxn + 1) * (maxn + 2) + 16 + 3 * (size_t)maxg + 3 + tab + 128 +
-          4 * (size_t)maxn + (size_t)gridtab) * sizeof(double);
-}
-
-int launch_small_args(lfm_ctx* ctx, SmallArgs& a, int nprob, int maxn, int maxg, int gridtab) {
-  int tabs;
-  const size_t lds = small_lds(maxn, maxg, gridtab, &tabs);
-  if (lds > 160 * 1024 || nprob > SMALL_ARG_PROBS)
-    return set_err(ctx, LFM_E_ARG, "small batch (kernel arguments): past its limits");
-  a.tabs = tabs;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&small_mll_kernel_args),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
-  hipEvent_t ev;
-  prof_begin(ctx, K_SMALL, &ev, ctx->stream);
-  hipLaunchKernelGGL(small_mll_kernel_args, dim3(nprob), dim3(256), lds, ctx->stream, a);
-  prof_end(ctx, K_SMALL, ev, 0, 0, ctx->stream);
-  return hip_fail(ctx, hipGetLastError(), "small_mll_kernel_args");
-}
-
-int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn, int maxg,
-                       int gridtab, int negative, double* d_out, int* d_status) {
-  int tabs;
-  const size_t lds = small_lds(maxn, maxg, gridtab, &tabs);
-  if (lds > 160 * 1024)
-    return set_err(ctx, LFM_E_ARG, "small batch: LDS past 160 KB (n <= 128, grid tables <= "
-                                   "SMALL_GRID_TAB_MAX)");
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&small_mll_kernel),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
-  hipEvent_t ev;
-  prof_begin(ctx, K_SMALL, &ev, ctx->stream);
-  hipLaunchKernelGGL(small_mll_kernel, dim3(nprob), dim3(256), lds, ctx->stream,
-                     d_probs, negative, d_out, d_status, tabs);
-  prof_end(ctx, K_SMALL, ev, 0, 0, ctx->stream);
-  return hip_fail(ctx, hipGetLastError(), "small_mll_kernel");
 }
 
 }  // namespace lfm

@@ -29,6 +29,7 @@ enum KClass {
   K_GRAD,         // MLL gradient: W-weighted kernel-derivative reduction
   K_PANEL,        // fused pending update + diagonal factor + panel solve (one block column)
   K_SIDE_SYRK,    // schedule 3: the tail of a step's trailing update on the side CUs (helper)
+  K_SMALL_GRAD,   // one-workgroup-per-problem value + gradient (and the in-kernel fit)
   K_NCLASS
 };
 
@@ -193,6 +194,7 @@ inline int64_t small_grid_doubles(int64_t n) { return n + (n + 1) / 2; }
 // within a CU's 160 KB (launch_small_batch)
 constexpr int SMALL_GRID_TAB_MAX = 2048;
 constexpr int SMALL_MAX = 128;  // largest n handled by small_mll_kernel
+constexpr int SMALL_GRAD_MAX = 63;  // largest n of the batched gradient / fit (one wave per problem)
 
 // gram kernels (lfm_gram.hip)
 int launch_tables(lfm_ctx* ctx, const HypDev& h, const GridLayout& lay, const double* d_times,
@@ -253,8 +255,30 @@ struct SmallArgs {
   double* out;
   int* status;
   int negative, tabs;
+  double* grad;  // small_grad_kernel_args: the gradient, packed as hyp
 };
 static_assert(sizeof(SmallArgs) <= 4096, "kernel argument block");
+// value and gradient of a batch of small problems (n <= 63): a = the kernel-argument form
+// (problem table and hyperparameters in the arguments) or NULL (d_probs, d_offs: the table and
+// each problem's offsets of its vectors [0, nprob) and scalars [nprob, 2 nprob) in the packed
+// layout, hyperparameters read through SmallProb::dsb / sc)
+int launch_small_grad(lfm_ctx* ctx, SmallArgs* a, const SmallProb* d_probs, const int* d_offs,
+                      int nprob, size_t lds, int negative, double* out, double* grad, int* status);
+// LDS bytes of the gradient (fit = 0) or fit (fit = 1) launch over these problems (host table)
+size_t small_grad_lds(const SmallProb* probs, int nprob, int fit);
+// the fit kernel's launch: every problem's Adam steps on the device (lfm_small.hip FitArgs)
+struct SmallFitLaunch {
+  const SmallProb* probs;
+  const int* offs;
+  int nprob;
+  double *raw, *mu, *nu, *history;
+  const double* bias;
+  int* status;
+  double lr, b1, b2, eps, eps_root;
+  int64_t step0, nsteps, spe;
+  int fix, negative;
+};
+int launch_small_fit(lfm_ctx* ctx, const SmallFitLaunch& f, size_t lds);
 int launch_small_args(lfm_ctx* ctx, SmallArgs& a, int nprob, int maxn, int maxg, int gridtab);
 // gridtab: the largest grid table of the problems (doubles; 0: none on the grid path)
 int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn, int maxg,

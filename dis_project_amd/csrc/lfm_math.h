@@ -190,4 +190,12 @@ __device__ __forceinline__ double rsqrt_1nr(double x) {
   return y * fma(h * y, y, 1.5);
 }
 
+// Value of v held by `lane` (wave-uniform lane index), broadcast to the wave.
+__device__ __forceinline__ double rdl(double v, int lane) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b & 0xffffffffu), lane);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), lane);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 }  // namespace lfm

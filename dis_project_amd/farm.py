@@ -137,6 +137,20 @@ _NUM_GENES = operator.attrgetter("num_genes")
 _chain = itertools.chain.from_iterable
 
 
+def unpack_grads(packed: np.ndarray, genes) -> list:
+    """A packed gradient (lfm_batch_mll_grad_f64's layout: dD dS dB of each problem, then d l,
+    d obs_stddev, 0 of each) as one ``CustomConjMLL.value_and_grad`` dict per problem."""
+    out, off = [], 0
+    nvec = 3 * sum(genes)
+    for p, G in enumerate(genes):
+        v = packed[off:off + 3 * G]
+        sc = packed[nvec + 3 * p: nvec + 3 * p + 3]
+        out.append({"true_d": v[:G].copy(), "true_s": v[G:2 * G].copy(),
+                    "true_b": v[2 * G:].copy(), "l": float(sc[0]), "obs_stddev": float(sc[1])})
+        off += 3 * G
+    return out
+
+
 class BatchEvaluator:
     """MLL evaluations of many small problems (n <= 128 each: the C5 ablations) in one batched
     launch per call, on a device-resident batch (``lfm_batch_create``: every problem's x / y in
@@ -179,21 +193,42 @@ class BatchEvaluator:
         self._vec, self._sc = self._buf[:nvec], self._buf[nvec:]
         self._buf_ptr = self._buf.ctypes.data
 
-    def __call__(self, models) -> np.ndarray:
-        models = list(models)
-        if len(models) != len(self.datasets):
-            raise ValueError("one model per registered dataset")
-        genes = tuple(map(_NUM_GENES, models))
+    def registered(self, genes) -> int:
+        """The batch registered for this gene layout (re-registered if it changed): its handle."""
+        genes = tuple(int(g) for g in genes)
         if genes != self._genes:
             if self.batch is not None:
                 self.close()
             self._create(genes)
+        return self.batch
+
+    def _pack(self, models):
+        models = list(models)
+        if len(models) != len(self.datasets):
+            raise ValueError("one model per registered dataset")
+        self.registered(map(_NUM_GENES, models))
         np.concatenate(list(_chain(map(_VECS, models))), out=self._vec)
         self._sc[:] = list(_chain(map(_SCALARS, models)))
+        return models
+
+    def __call__(self, models) -> np.ndarray:
+        self._pack(models)
         rc = self.ctx.lib.lfm_batch_mll_f64(self.ctx.handle, self.batch, self._buf_ptr,
                                             int(self.negative), self._out_ptr, self._st_ptr)
         self.ctx.check(rc, allow_not_pd=True)
         return self._out.copy()
+
+    def value_and_grad(self, models):
+        """Every problem's value and gradient (constrained parameters, as
+        ``CustomConjMLL.value_and_grad``) in ONE launch (``lfm_batch_mll_grad_f64``; n <= 63 per
+        problem). Returns (values [P], [grads dict per problem]); NaN where not PD."""
+        models = self._pack(models)
+        grad = np.empty(self._buf.size)
+        rc = self.ctx.lib.lfm_batch_mll_grad_f64(self.ctx.handle, self.batch, self._buf_ptr,
+                                                 int(self.negative), self._out_ptr,
+                                                 _lib.dptr(grad), self._st_ptr)
+        self.ctx.check(rc, allow_not_pd=True)
+        return self._out.copy(), unpack_grads(grad, self._genes)
 
     def close(self):
         if self.batch is not None:

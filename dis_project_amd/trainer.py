@@ -15,12 +15,18 @@ parameters; the bijectors' chain rule is applied on the host:
     l:                                  tfb.Sigmoid(low=0.5, high=3.5)  (model.py:111)
 ``adam`` restates optax.adam (b1 0.9, b2 0.999, eps 1e-8, eps_root 0; main.py:45 uses
 learning rate 0.01).
+
+``BatchTrainer`` runs JaxTrainer.fit for many independent problems at once — the reference's
+ablation / replicate training runs (notebook.py:33-75, one JaxTrainer per problem; main.py:59)
+— with every step on the GPU: ``lfm_batch_fit_f64`` steps each problem's Adam loop inside one
+kernel launch (one workgroup per problem), with the same constrain / chain rule / adam /
+after_epoch arithmetic as this module's host loop.
 """
 
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Any
+from typing import Any, Sequence
 
 import numpy as np
 
@@ -161,8 +167,11 @@ class JaxTrainer:
         out = dict(params)
         out["true_s"] = np.array(params["true_s"], np.float64).copy()
         out["true_d"] = np.array(params["true_d"], np.float64).copy()
-        out["true_s"][3] = 1.0
-        out["true_d"][3] = 0.8
+        # JAX drops an out-of-bounds .at[3].set(...) (G <= 3): nothing changes then
+        if out["true_s"].size > 3:
+            out["true_s"][3] = 1.0
+        if out["true_d"].size > 3:
+            out["true_d"][3] = 0.8
         return out
 
     def fit(self, fix_params: bool = True, num_steps_per_epoch: int = 1000):
@@ -185,3 +194,97 @@ class JaxTrainer:
         if self.track_parameters:
             return self.model, self.history, self.track_parameters
         return self.model, self.history
+
+
+def pack_raw(raws: Sequence[dict], jitters: Sequence[float]) -> np.ndarray:
+    """Unconstrained parameters of P problems in lfm_batch's packed layout: raw true_d, true_s,
+    true_b of each problem in order, then raw l, raw obs_stddev and the (static, constrained)
+    jitter of each."""
+    vec = [np.concatenate([np.asarray(r["true_d"], np.float64), np.asarray(r["true_s"], np.float64),
+                           np.asarray(r["true_b"], np.float64)]) for r in raws]
+    sc = [[float(r["l"]), float(r["obs_stddev"]), float(j)] for r, j in zip(raws, jitters)]
+    return np.concatenate(vec + [np.asarray(sc, np.float64).reshape(-1)])
+
+
+def unpack_raw(packed: np.ndarray, genes: Sequence[int]) -> list:
+    """pack_raw's inverse (the jitter slots dropped)."""
+    out, off = [], 0
+    nvec = 3 * int(sum(genes))
+    for p, G in enumerate(genes):
+        v = packed[off:off + 3 * G]
+        sc = packed[nvec + 3 * p: nvec + 3 * p + 3]
+        out.append({"true_d": v[:G].copy(), "true_s": v[G:2 * G].copy(), "true_b": v[2 * G:].copy(),
+                    "l": float(sc[0]), "obs_stddev": float(sc[1])})
+        off += 3 * G
+    return out
+
+
+@dataclass
+class BatchTrainer:
+    """``JaxTrainer`` (trainer.py:36-228) over P independent (model, dataset) problems at once:
+    ``fit`` runs every problem's ``num_iters`` training steps on the GPU in ONE launch
+    (``lfm_batch_fit_f64``: one workgroup per problem, its Adam loop inside the kernel, no host
+    round trip between steps; n <= 63 per problem). Per problem the semantics are JaxTrainer's:
+    training in the bijectors' unconstrained space (trainer.py:75), the objective's value and
+    gradient at the constrained model (trainer.py:103, 126), ``optim`` (an ``adam``) on the
+    unconstrained leaves (trainer.py:127-128), ``after_epoch`` on the unconstrained model every
+    ``num_steps_per_epoch`` steps (step 0 included, trainer.py:205-210), then the constrained
+    model with ``after_epoch`` once more (trainer.py:218-222). ``objective`` is a
+    ``CustomConjMLL`` (its ``negative``). The datasets are registered in HBM once
+    (farm.BatchEvaluator); ``close()`` releases them."""
+
+    models: Sequence[ExactLFM]
+    objective: Any
+    training_data: Sequence[Dataset]
+    optim: adam
+    key: Any = None
+    num_iters: int = 150
+    ctx: Any = None
+    history: Any = None
+
+    def __post_init__(self):
+        from . import _lib
+        from .farm import BatchEvaluator
+
+        self.models = list(self.models)
+        self.training_data = list(self.training_data)
+        if len(self.models) != len(self.training_data):
+            raise ValueError("one model per dataset")
+        self._like = list(self.models)
+        self.raws = [unconstrain(m) for m in self.models]  # trainer.py:75
+        self.ctx = self.ctx or _lib.get_context()
+        self._ev = BatchEvaluator(self.ctx, self.training_data, bool(self.objective.negative))
+
+    def fit(self, fix_params: bool = True, num_steps_per_epoch: int = 1000):
+        """trainer.py:162-228 for every problem; returns (models, histories [P, num_iters])."""
+        from . import _lib
+
+        genes = [int(m.num_genes) for m in self._like]
+        batch = self._ev.registered(genes)
+        raw = pack_raw(self.raws, [m.jitter for m in self._like])
+        mu, nu = np.zeros_like(raw), np.zeros_like(raw)
+        hist = np.empty((self.num_iters, len(genes)))
+        st = np.zeros(len(genes), np.int32)
+        o = self.optim
+        opt = _lib.LfmAdam(o.learning_rate, o.b1, o.b2, o.eps, o.eps_root,
+                           int(num_steps_per_epoch), int(bool(fix_params)))
+        rc = self.ctx.lib.lfm_batch_fit_f64(self.ctx.handle, batch, _lib.ctypes.byref(opt),
+                                            int(bool(self.objective.negative)), 0, self.num_iters,
+                                            _lib.dptr(raw), _lib.dptr(mu), _lib.dptr(nu),
+                                            _lib.dptr(hist), _lib.dptr(st))
+        self.ctx.check(rc, allow_not_pd=True)
+        self.status = st
+        self.raws = unpack_raw(raw, genes)
+        out = []
+        for r, like in zip(self.raws, self._like):
+            m = constrain(r, like)
+            if fix_params:  # trainer.py:218-222, on the constrained model
+                c = JaxTrainer.after_epoch({"true_s": m.true_s, "true_d": m.true_d}, True)
+                m = m.replace(true_s=c["true_s"], true_d=c["true_d"])
+            out.append(m)
+        self.models = out
+        self.history = hist.T.copy()
+        return self.models, self.history
+
+    def close(self):
+        self._ev.close()

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define LFM_ABI_VERSION 3
+#define LFM_ABI_VERSION 4
 
 enum {
   LFM_OK = 0,
@@ -181,6 +181,44 @@ int lfm_batch_hyp_size(const lfm_batch* batch, int64_t* out);
  * the device before it frees). */
 int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative,
                       double* out, int* status);
+/* Value and gradient of every problem's CustomConjMLL(negative).step in ONE launch, one
+ * workgroup per problem — jax.value_and_grad(loss) at src/trainer.py:126 (before the
+ * bijectors' chain rule, trainer.py:103), batched over the ablation problems of
+ * src/notebook.py:33-75 / the p53 fit of src/main.py:59. Every problem needs n <= 63, else
+ * LFM_E_ARG (lfm_mll_grad_f64 takes any n). hyp as lfm_batch_mll_f64; value[p] as its out[p] (the
+ * same bits); grad packed in hyp's layout: for each problem dD[G_p] dS[G_p] dB[G_p] in order,
+ * then for each problem d l, d obs_stddev, 0 (jitter is static, model.py:64). Not PD: value and
+ * that problem's gradient NaN, status[p] = LFM_E_NOT_PD, returns LFM_E_NOT_PD. Deterministic (no
+ * atomics: the same inputs give the same bits). */
+int lfm_batch_mll_grad_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative,
+                           double* value, double* grad, int* status);
+
+/* optax.adam(learning_rate, b1, b2, eps, eps_root) and JaxTrainer.fit's epoch handling
+ * (src/trainer.py:162-228; src/main.py:45 and notebook.py:55 use adam(0.01)). */
+typedef struct {
+  double learning_rate, b1, b2, eps, eps_root;
+  int64_t num_steps_per_epoch; /* after_epoch every this many steps, step 0 included (>= 1) */
+  int fix_params;              /* after_epoch sets true_s[3] = 1.0, true_d[3] = 0.8          */
+} lfm_adam;
+/* JaxTrainer.fit of every problem of the batch at once, on the device: nsteps training steps
+ * (trainer.py:105-132 under vscan, :198-216) in ONE launch, one workgroup per problem, no host
+ * round trip between steps. Per step and problem: constrain (softplus for true_d / true_s /
+ * true_b / obs_stddev, 0.5 + 3 sigmoid for l: model.py:66-121), value and gradient (as
+ * lfm_batch_mll_grad_f64), the bijectors' chain rule, one Adam update of the unconstrained
+ * parameters, then after_epoch on them when (step0 + s) % num_steps_per_epoch == 0 and
+ * fix_params (the reference's index-3 quirk; nothing for G <= 3, as JAX drops the update).
+ *   raw    [nhyp] in/out: the UNCONSTRAINED parameters in hyp's packed layout (the jitter slots
+ *          hold the static jitter itself and are never changed)
+ *   mu, nu [nhyp] in/out: Adam's moments (zeros to start; resumable across calls with step0)
+ *   step0  steps already taken (Adam's count is step0 + s + 1)
+ *   history [nsteps x nprob], step-major: each step's loss value before its update
+ *   status [nprob] optional: 0, or 1 + the first step whose Cholesky failed (its loss and the
+ *          parameters are NaN from there on, as under JAX); returns LFM_E_NOT_PD if any did.
+ * The final constrain and after_epoch on the constrained model (trainer.py:218-222) are the
+ * caller's (dis_project_amd.trainer.BatchTrainer). n <= 63 per problem, else LFM_E_ARG. */
+int lfm_batch_fit_f64(lfm_ctx* ctx, lfm_batch* batch, const lfm_adam* opt, int negative,
+                      int64_t step0, int64_t nsteps, double* raw, double* mu, double* nu,
+                      double* history, int* status);
 
 /* Value and gradient of CustomConjMLL(negative).step — what jax.value_and_grad(loss)
  * differentiates at trainer.py:126, before the bijectors' chain rule (trainer.py:103) —

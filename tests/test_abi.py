@@ -22,7 +22,7 @@ def header_functions(name="lfm.h"):
 
 def test_library_builds_and_loads():
     lib = _lib.load_library()
-    assert lib.lfm_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.lfm_abi_version() == _lib.ABI_VERSION == 4
 
 
 @pytest.mark.parametrize("header,sigs", [("lfm.h", "PRODUCT_SIGNATURES"),
@@ -59,6 +59,17 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.LfmHyp) == 7 * 8
     assert ctypes.sizeof(_lib.LfmProblem) == 3 * 8 + 7 * 8
     assert ctypes.sizeof(_lib.LfmKstat) == 32 + 8 * 5
+    assert ctypes.sizeof(_lib.LfmAdam) == 5 * 8 + 8 + 8  # int fix_params padded to 8
+
+
+def test_no_measured_null_variants_in_the_product():
+    """The A/B variants round 4 measured inside the noise (32-row w = 1 units, rest-unit
+    stealing across XCDs) are not compiled into liblfm.so."""
+    syms = os.popen(f"nm {_lib.LIB_PATH}").read()
+    for name in ("step_kernel32", "rest_claim", "steal"):
+        assert name not in syms, name
+    src = open(os.path.join(ROOT, "dis_project_amd", "csrc", "lfm_chol.hip")).read()
+    assert "LFM_TR32" not in src and "LFM_STEAL" not in src
 
 
 def test_error_codes_match_header():
