@@ -24,6 +24,10 @@ stopped). Workloads; the default is c2 on one GPU and c3 on s
       One GPU (replicas at N > 1: every rank fills its own; weak scaling).
   c5  configs[4]: a step = the 15 replicate x leave-one-gene-out problems (N = 28), each
       rank's share in one batched launch, then the all-gather. Strong scaling.
+  c5fit  configs[4]'s actual workflow (notebook.py:55-75): a step = JaxTrainer.fit of the 15
+      problems, 150 steps of adam(0.01) on CustomConjMLL(negative=True) each, in ONE launch
+      (lfm_batch_fit_f64: every problem's value_and_grad + Adam loop inside one workgroup).
+      value = problem training steps / s (15 x 150 per step). One GPU (replicas at N > 1).
 torch.distributed (gloo, CPU) is only the control plane: barrier, max-over-ranks timing and
 shipping the RCCL unique id.
 
@@ -83,7 +87,7 @@ def parse(argv=None):
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default=None,
+    p.add_argument("--workload", choices=["c2", "c3", "c4", "c5", "c5fit"], default=None,
                    help="default: c2 on one GPU, c3 (configs[2], the multi-GPU config) on several")
     p.add_argument("--genes", type=int, default=None)
     p.add_argument("--timepoints", type=int, default=256)
@@ -92,6 +96,8 @@ def parse(argv=None):
                    help="c3: evaluations in flight per GPU (farm.ConcurrentEvaluator, schedule-1 "
                         "worker contexts); 1 = one schedule-3 context, one evaluation at a time; "
                         "0 (default) = farm.choose_workers for the rank's share")
+    p.add_argument("--fit-iters", type=int, default=150,
+                   help="c5fit: Adam steps per fit (notebook.py:64 / main.py:54: 150)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-profile", action="store_true",
@@ -371,6 +377,47 @@ def cpu_baseline_c5(models, datasets, gpu_values, min_seconds=2.0):
     }
 
 
+def cpu_baseline_c5fit(models, datasets, raw0, iters, gpu_final, min_seconds=2.0):
+    """The C5 fit on the CPU: oracle/lfm_cpu.cpp's JaxTrainer.fit (value and gradient by dual
+    numbers of the reference's erf formulas, explicit Sigma^{-1}, the same Adam loop) of the 15
+    problems sequentially on ONE core, repeated until min_seconds have passed; the final losses
+    check the GPU fit's."""
+    from dis_project_amd import trainer as TR
+    from oracle import lfm_cpu
+
+    genes = [m.num_genes for m in models]
+    nvec = 3 * sum(genes)
+    rounds, finals = 0, None
+    t0 = time.perf_counter()
+    while True:
+        finals, off = [], 0
+        for p, (m, d) in enumerate(zip(models, datasets)):
+            G = genes[p]
+            r = np.concatenate([raw0[off:off + 3 * G], raw0[nvec + 3 * p: nvec + 3 * p + 3]])
+            off += 3 * G
+            h, _ = lfm_cpu.fit(d.X, d.y, G, r, iters, lr=0.01, spe=1000, fix=False,
+                               negative=True)
+            finals.append(h[-1])
+        rounds += 1
+        if time.perf_counter() - t0 >= min_seconds:
+            break
+    t = time.perf_counter() - t0
+    ref = np.asarray(finals)
+    rel = np.abs(ref - np.asarray(gpu_final)) / np.abs(ref)
+    per_step = len(models) * iters
+    return {
+        "value": rounds * per_step / t,
+        "unit": "problem training steps/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"oracle/lfm_cpu.cpp fit: the {len(models)} problems (N={datasets[0].n}) x "
+                   f"{iters} Adam steps sequentially on 1 thread, {rounds} full fits in "
+                   f"{t:.2f} s ({t / rounds * 1e3:.0f} ms per fit); timed in full"),
+        "host_cpus": os.cpu_count(),
+        "gpu_vs_cpu_rel": float(rel.max()),
+    }
+
+
 def cpu_baseline_c4(work, threads, gpu_rows, check_rows):
     """C4 on the CPU: the reference formula (fp64, every kernel branch, std::erf; stored as
     float) over every 4th row of the N = 65536 lower triangle (a quarter of the rows, ~1/4 of
@@ -549,6 +596,28 @@ def main(argv=None):
 
         def step():
             return fm.run(world, lambda idx: one_fill())
+    elif a.workload == "c5fit":
+        from dis_project_amd import trainer as TR
+
+        models, datasets = farm.workload("c5")
+        n = datasets[0].n
+        fit_ev = farm.BatchEvaluator(ctx, datasets, negative=True)
+        close = fit_ev.close
+        batch = fit_ev.registered([m.num_genes for m in models])
+        raw0 = TR.pack_raw([TR.unconstrain(m) for m in models], [m.jitter for m in models])
+        # notebook.py:55-75: adam(0.01), fix_params=False, num_steps_per_epoch=1000
+        fit_opt = _lib.LfmAdam(0.01, 0.9, 0.999, 1e-8, 0.0, 1000, 0)
+        iters = a.fit_iters
+        per_step = world * len(models) * iters  # replicas: every rank fits the 15 problems
+        fit_hist = np.empty((iters, len(models)))
+
+        def step():
+            raw = raw0.copy()
+            mu, nu = np.zeros_like(raw), np.zeros_like(raw)
+            ctx.check(lib.lfm_batch_fit_f64(h, batch, _lib.ctypes.byref(fit_opt), 1, 0, iters,
+                                            _lib.dptr(raw), _lib.dptr(mu), _lib.dptr(nu),
+                                            _lib.dptr(fit_hist), None))
+            return fit_hist[-1].copy()  # each problem's final loss
     else:
         models, datasets = farm.workload(a.workload, a.genes, a.timepoints, a.restarts)
         n = datasets[0].n
@@ -573,10 +642,10 @@ def main(argv=None):
     # event record between two dependent launches widens the dispatch gap, ≈ 0.5 ms per
     # evaluation with all step launches instrumented; one instrumented step of K costs
     # 0.5 / K ms); c4 in every step (one fill launch per step)
-    prof = not a.no_profile and a.workload in ("c2", "c4")
+    prof = not a.no_profile and a.workload in ("c2", "c4", "c5fit")
     prof_steps = (1 if a.workload == "c2" else a.steps) if prof else 0
-    classes = (["syrk", "gram_grid", "potrf", "syrk_side"] if a.workload == "c2"
-               else ["gram_grid", "tables"])
+    classes = {"c2": ["syrk", "gram_grid", "potrf", "syrk_side"], "c4": ["gram_grid", "tables"],
+               "c5fit": ["small_grad"]}.get(a.workload)
     if prof:
         ctx.profile(False)
         ctx.profile_reset()
@@ -673,14 +742,22 @@ def main(argv=None):
     elif a.workload == "c4":
         wl = (f"configs[3]: one fp32 lower-triangle gram fill per rank, {a.genes} genes x "
               f"{a.timepoints} timepoints, N={n} (Sigma stored as an N x N fp32 buffer)")
+    elif a.workload == "c5fit":
+        wl = (f"configs[4]'s training workflow (notebook.py:55-75): JaxTrainer.fit of the 15 "
+              f"replicate x leave-one-gene-out problems (N={n}), {a.fit_iters} adam(0.01) steps "
+              f"each, fix_params=False, in one launch per fit (lfm_batch_fit_f64)")
     else:
         wl = (f"configs[4]: 3 replicates x 5 leave-one-gene-out ablations (N={n}) per step, "
               f"farmed over {world} GPU(s), one batched launch per rank")
     c4 = a.workload == "c4"
+    fit = a.workload == "c5fit"
     line = {
-        "metric": METRIC if not c4 else "fp32 gram fills/sec at N=65536 (configs[3])",
+        "metric": ("fp32 gram fills/sec at N=65536 (configs[3])" if c4 else
+                   "MLL value_and_grad + Adam training steps/sec (configs[4] fit, 15 problems x "
+                   f"{a.fit_iters} steps)" if fit else METRIC),
         "value": value,
-        "unit": "MLL evals/s" if not c4 else "fp32 gram fills/s",
+        "unit": ("fp32 gram fills/s" if c4 else "problem training steps/s" if fit
+                 else "MLL evals/s"),
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
@@ -696,8 +773,8 @@ def main(argv=None):
         "data": "synthetic (seeded numpy: D~U[.2,1], S~U[.5,1.5], B~U[.01,.1], y = B/D + "
                 "0.5 N(0,1), t = linspace(0,12,T))",
         "config": {"workload": wl, "N": n,
-                   "genes": a.genes if a.workload != "c5" else 4,
-                   "timepoints": a.timepoints if a.workload != "c5" else 7,
+                   "genes": a.genes if a.workload not in ("c5", "c5fit") else 4,
+                   "timepoints": a.timepoints if a.workload not in ("c5", "c5fit") else 7,
                    "problems_per_step": per_step, "parallelism": f"replicas{world}",
                    "exchange": {"rccl": "RCCL all-gather of NaN-padded per-rank result slots",
                                 "gloo": "gloo all-gather (rehearsal)",
@@ -815,6 +892,46 @@ def main(argv=None):
                     "bytes_per_launch": gram["bytes"] / gram["launches"],
                     "avg_launch_ms": gram["total_ms"] / gram["launches"],
                 }
+    if prof and rank == 0 and fit:
+        sg = stats.get("small_grad", {})
+        if sg.get("launches"):
+            launch_ms = sg["total_ms"] / sg["launches"]
+            # algorithmic fp64 work of one training step of one problem (n = 28): the Cholesky
+            # of the augmented matrix ((n+1)^3 / 3), the triangular inverse (n^3 / 3) and
+            # Sigma^{-1} = X^T X (n^3 / 3); the kernel evaluations are transcendental-bound VALU
+            # work on top. One workgroup per problem: 15 of the chip's 256 CUs — the bound is the
+            # latency of one problem's step chain, not a throughput roofline
+            fl = ((n + 1) ** 3 / 3.0 + 2 * n ** 3 / 3.0) * per_step
+            ach = fl / (launch_ms * 1e-3) / 1e12
+            line["roofline"] = {
+                "kernel": "small_fit_kernel (one workgroup per problem, 150 steps in-kernel)",
+                "bound": "mfma", "achieved": ach, "peak": FP64_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": ach / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
+                "note": "latency-bound: 15 workgroups on 256 CUs; frac is of the whole chip",
+                "launches": sg["launches"], "avg_launch_ms": launch_ms,
+                "us_per_training_step": launch_ms * 1e3 / a.fit_iters,
+            }
+        # the per-call path this replaces: 15 sequential lfm_mll_grad_f64 calls per training step
+        # (each the large-N machinery: a bordered 256 x 256 factorisation, several launches)
+        seq = []
+        hp = [m.hyp() for m in models]
+        gbuf = np.empty(3 * max(m.num_genes for m in models) + 2)
+        vbuf = np.empty(1)
+        xs = [np.ascontiguousarray(d.X) for d in datasets]
+        ys = [np.ascontiguousarray(d.y.reshape(-1)) for d in datasets]
+        for r in range(12):
+            t1 = time.perf_counter()
+            for m, hpp, x_, y_ in zip(models, hp, xs, ys):
+                ctx.check(lib.lfm_mll_grad_f64(h, _lib.dptr(x_), _lib.dptr(y_), x_.shape[0],
+                                               hpp.ref, 1, _lib.dptr(vbuf), _lib.dptr(gbuf)))
+            seq.append((time.perf_counter() - t1) * 1e6)
+        seq_us = float(np.median(seq[2:]))
+        line["per_call_path"] = {
+            "op": "15 sequential lfm_mll_grad_f64 calls (one training step's gradients)",
+            "us_per_training_step": seq_us,
+            "speedup_of_fit_kernel": (seq_us / line["roofline"]["us_per_training_step"]
+                                      if "roofline" in line else None),
+        }
     if prof and rank == 0 and c4:
         gram = stats.get("gram_grid", {})
         tab = stats.get("tables", {})
@@ -842,6 +959,9 @@ def main(argv=None):
             bad = not cb["gpu_vs_cpu_rel"] <= PARITY_RTOL
         elif a.workload == "c5":
             cb = cpu_baseline_c5(models, datasets, res[0])
+            bad = not cb["gpu_vs_cpu_rel"] <= PARITY_RTOL
+        elif a.workload == "c5fit":
+            cb = cpu_baseline_c5fit(models, datasets, raw0, a.fit_iters, res[0])
             bad = not cb["gpu_vs_cpu_rel"] <= PARITY_RTOL
         else:
             check = np.array([0, 4, 256, 32768, n - 4, 4 * 5000, 4 * 9999, 4 * 16000])

@@ -22,6 +22,13 @@
 // algorithm, not its code): an unblocked diagonal factor, a row-parallel triangular solve
 // of the panel and an OpenMP tile-parallel trailing update with an AVX2/FMA micro-kernel.
 // Built with -ffp-contract=off so the kernel formulas round every product like XLA-CPU.
+//
+// The training step (lfm_cpu_mll_grad, lfm_cpu_fit): jax.value_and_grad of the MLL (trainer.py:126)
+// with the kernel's derivatives in (D_row, D_col, l) by forward-mode duals of the same erf-form
+// formulas (d erf(u) = 2/sqrt(pi) e^{-u^2} du), Sigma^{-1} explicitly from the Cholesky factor,
+// 1/2 tr((a a^T - Sigma^{-1}) dSigma) + a^T dm; then JaxTrainer.fit's loop (trainer.py:162-228)
+// with optax.adam as dis_project_amd/trainer.py restates it. The batched fit's CPU baseline
+// (bench.py --workload c5fit).
 #include <immintrin.h>
 #include <omp.h>
 
@@ -254,6 +261,190 @@ int64_t potrf_blocked(double* A, int64_t n, int64_t lda) {
   return -1;
 }
 
+// ---------------------------------------------------------------- gradient (duals)
+// value and derivatives in (D_row, D_col, l)
+struct Dd {
+  double v, a, b, c;
+};
+inline Dd dc(double v) { return {v, 0, 0, 0}; }
+inline Dd operator+(Dd x, Dd y) { return {x.v + y.v, x.a + y.a, x.b + y.b, x.c + y.c}; }
+inline Dd operator-(Dd x, Dd y) { return {x.v - y.v, x.a - y.a, x.b - y.b, x.c - y.c}; }
+inline Dd operator-(Dd x) { return {-x.v, -x.a, -x.b, -x.c}; }
+inline Dd operator*(Dd x, Dd y) {
+  return {x.v * y.v, x.a * y.v + x.v * y.a, x.b * y.v + x.v * y.b, x.c * y.v + x.v * y.c};
+}
+inline Dd operator/(Dd x, Dd y) {
+  const double q = x.v / y.v;
+  return {q, (x.a - q * y.a) / y.v, (x.b - q * y.b) / y.v, (x.c - q * y.c) / y.v};
+}
+inline Dd dexp(Dd x) {
+  const double e = std::exp(x.v);
+  return {e, e * x.a, e * x.b, e * x.c};
+}
+inline Dd derf(Dd x) {
+  const double g = 1.1283791670955125739 * std::exp(-x.v * x.v);
+  return {std::erf(x.v), g * x.a, g * x.b, g * x.c};
+}
+
+// h of model.py:315-365 on duals (Dj, Dk: the genes' decays as variables)
+inline Dd h_d(Dd Dj, Dd Dk, Dd l, double t1, double t2) {
+  const double t_dist = t2 - t1;
+  const Dd gk = (Dk * l) / dc(2.0);
+  const Dd multiplier = dexp(gk * gk) / (Dj + Dk);
+  const Dd first_multiplier = dexp(-(Dk * dc(t_dist)));
+  const Dd first_erf_terms = derf(dc(t_dist) / l - gk) + derf(dc(t1) / l + gk);
+  const Dd second_multiplier = dexp(-(Dk * dc(t2) + Dj * dc(t1)));
+  const Dd second_erf_terms = derf(dc(t2) / l - gk) + derf(gk);
+  return multiplier * (first_multiplier * first_erf_terms - second_multiplier * second_erf_terms);
+}
+
+struct PairD {
+  double dDr, dDc, dSr, dSc, dl;
+};
+
+// the flag-switched kernel (model.py:152-195) of rows a, b: derivatives into o (row / column
+// gene accumulators), scaled by wgt
+void kernel_grad_cpu(const Hyp& p, const double* a, const double* b, double wgt, PairD& o) {
+  const int64_t f1 = flag_int(a[2]), f2 = flag_int(b[2]);
+  const Dd L{p.l, 0, 0, 1};
+  if (f1 * f2 != 0) {
+    const int64_t ja = gene_index(a[1], p.G), jb = gene_index(b[1], p.G);
+    const Dd Dr{p.D[ja], 1, 0, 0}, Dc{p.D[jb], 0, 1, 0};
+    // kernel_xx: S_ja S_jb l sqrt(pi)/2 (h(jb, ja, tb, ta) + h(ja, jb, ta, tb))
+    const Dd u = (L * dc(kSqrtPi * 0.5)) * (h_d(Dc, Dr, L, b[0], a[0]) + h_d(Dr, Dc, L, a[0], b[0]));
+    const double w = wgt * (double)(f1 * f2), ss = p.S[ja] * p.S[jb];
+    o.dDr += w * ss * u.a;
+    o.dDc += w * ss * u.b;
+    o.dl += w * ss * u.c;
+    o.dSr += w * p.S[jb] * u.v;
+    o.dSc += w * p.S[ja] * u.v;
+  }
+  if ((1 - f1) * (1 - f2) != 0) {  // kernel_ff: exp(-(d^2) / (2 l))
+    const double d = a[0] - b[0];
+    const double q = d * d / (2.0 * p.l);
+    o.dl += wgt * (double)((1 - f1) * (1 - f2)) * std::exp(-q) * q / p.l;
+  }
+  auto kxf = [&](const double* ra, const double* rb, bool a_is_row, int64_t sw) {
+    // kernel_xf(ra, rb): the row whose flag is 0 is the latent one (model.py:237-282)
+    const bool a_lat = ra[2] == 0.0;
+    const double tg = a_lat ? rb[0] : ra[0], gg = a_lat ? rb[1] : ra[1], tl = a_lat ? ra[0] : rb[0];
+    const int64_t j = gene_index(gg, p.G);
+    const bool gene_is_row = a_is_row != a_lat;  // the gene row is ra unless ra is latent
+    const Dd Dg = gene_is_row ? Dd{p.D[j], 1, 0, 0} : Dd{p.D[j], 0, 1, 0};
+    const double t_dist = tg - tl;
+    const Dd gj = (Dg * L) / dc(2.0);
+    const Dd u = (dc(0.5) * L * dc(kSqrtPi)) * dexp(gj * gj) * dexp(-(Dg * dc(t_dist))) *
+                 (derf(dc(t_dist) / L - gj) + derf(dc(tl) / L + gj));
+    const double w = wgt * (double)sw, s = p.S[j];
+    if (gene_is_row) {
+      o.dDr += w * s * u.a;
+      o.dSr += w * u.v;
+    } else {
+      o.dDc += w * s * u.b;
+      o.dSc += w * u.v;
+    }
+    o.dl += w * s * u.c;
+  };
+  if (f1 * (1 - f2) != 0) kxf(a, b, true, f1 * (1 - f2));
+  if ((1 - f1) * f2 != 0) kxf(b, a, false, (1 - f1) * f2);
+}
+
+// value and gradient of CustomConjMLL(negative).step (constrained parameters); grad[3G + 2]:
+// dD dS dB, dl, d obs_stddev. Work: 3 n^2 + 4 n doubles (allocated here if NULL). NaN if not PD.
+double mll_grad_cpu(const double* x, const double* y, int64_t n, int64_t G, const double* D,
+                    const double* S, const double* B, double l, double sd, double jitter,
+                    int negative, double* grad, std::vector<double>& work) {
+  const Hyp p{D, S, G, l};
+  work.resize((size_t)3 * n * n + 4 * n);
+  double* Sg = work.data();           // Sigma, then L (lower)
+  double* Xi = Sg + n * n;            // X = L^{-1} (lower)
+  double* Wm = Xi + n * n;            // W = a a^T - Sigma^{-1} (full)
+  double* r = Wm + n * n;
+  double* a = r + n;
+  double* z = a + n;
+  const double noise = sd * sd;
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t j = 0; j <= i; ++j) {
+      double v = kernel(p, x + 3 * i, x + 3 * j);
+      if (i == j) v = (v + jitter) + noise;
+      Sg[i * n + j] = v;
+    }
+  const double nan = std::nan("");
+  if (potrf_unblocked(Sg, n, n) >= 0) {
+    for (int64_t k = 0; k < 3 * G + 2; ++k) grad[k] = nan;
+    return nan;
+  }
+  const int64_t bs = n / G;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t g = std::min<int64_t>(i / bs, G - 1);
+    r[i] = y[i] - (B[g] / D[g]) * (double)flag_int(x[3 * i + 2]);
+  }
+  double logdet = 0.0, quad = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    double v = r[i];
+    for (int64_t q = 0; q < i; ++q) v -= Sg[i * n + q] * z[q];
+    z[i] = v / Sg[i * n + i];
+    logdet += std::log(Sg[i * n + i]);
+    quad += z[i] * z[i];
+  }
+  double mll = -0.5 * ((double)n * std::log(2.0 * M_PI) + 2.0 * logdet + quad);
+  // X = L^{-1} column by column; a = X^T z; Sigma^{-1} = X^T X
+  for (int64_t j = 0; j < n; ++j)
+    for (int64_t i = 0; i < n; ++i) {
+      if (i < j) {
+        Xi[i * n + j] = 0.0;
+        continue;
+      }
+      double v = i == j ? 1.0 : 0.0;
+      for (int64_t q = j; q < i; ++q) v -= Sg[i * n + q] * Xi[q * n + j];
+      Xi[i * n + j] = v / Sg[i * n + i];
+    }
+  for (int64_t i = 0; i < n; ++i) {
+    double v = 0.0;
+    for (int64_t k = i; k < n; ++k) v += Xi[k * n + i] * z[k];
+    a[i] = v;
+  }
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t j = 0; j <= i; ++j) {
+      double s = 0.0;
+      for (int64_t k = i; k < n; ++k) s += Xi[k * n + i] * Xi[k * n + j];
+      Wm[i * n + j] = Wm[j * n + i] = a[i] * a[j] - s;
+    }
+  std::vector<double> acc((size_t)2 * G + 1, 0.0);
+  double tr = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    tr += Wm[i * n + i];
+    const int64_t gi = gene_index(x[3 * i + 1], G);
+    for (int64_t j = 0; j <= i; ++j) {
+      PairD o{0, 0, 0, 0, 0};
+      kernel_grad_cpu(p, x + 3 * i, x + 3 * j, i == j ? 0.5 * Wm[i * n + i] : Wm[i * n + j], o);
+      const int64_t gj = gene_index(x[3 * j + 1], G);
+      acc[gi] += o.dDr;
+      acc[gj] += o.dDc;
+      acc[G + gi] += o.dSr;
+      acc[G + gj] += o.dSc;
+      acc[2 * G] += o.dl;
+    }
+  }
+  const double sign = negative ? -1.0 : 1.0;
+  for (int64_t g = 0; g < G; ++g) {
+    double af = 0.0;
+    for (int64_t i = g * bs; i < (g + 1) * bs; ++i) af += a[i] * (double)flag_int(x[3 * i + 2]);
+    grad[g] = sign * (acc[g] - B[g] / (D[g] * D[g]) * af);
+    grad[G + g] = sign * acc[G + g];
+    grad[2 * G + g] = sign * (af / D[g]);
+  }
+  grad[3 * G] = sign * acc[2 * G];
+  grad[3 * G + 1] = sign * sd * tr;
+  return sign * mll;
+}
+
+inline double softplus_c(double x) { return x >= 0.0 ? x + std::log1p(std::exp(-x)) : std::log1p(std::exp(x)); }
+inline double sigmoid_c(double x) {
+  const double e = std::exp(-std::fabs(x));
+  return x >= 0.0 ? 1.0 / (1.0 + e) : e / (1.0 + e);
+}
+
 }  // namespace
 
 extern "C" {
@@ -368,6 +559,52 @@ double lfm_cpu_mll(const double* x, const double* y, int64_t n, int64_t G, const
     info[7] = (double)omp_get_max_threads();
   }
   return mll;
+}
+
+
+// Value and gradient of CustomConjMLL(negative).step at the constrained parameters (trainer.py:126
+// before the chain rule); grad[3G + 2] = dD dS dB, dl, d obs_stddev. Returns the value (NaN and a
+// NaN gradient when Sigma is not PD).
+double lfm_cpu_mll_grad(const double* x, const double* y, int64_t n, int64_t G, const double* D,
+                        const double* S, const double* B, double l, double obs_stddev,
+                        double jitter, int negative, double* grad) {
+  std::vector<double> work;
+  return mll_grad_cpu(x, y, n, G, D, S, B, l, obs_stddev, jitter, negative, grad, work);
+}
+
+// JaxTrainer.fit of ONE problem (trainer.py:162-228; dis_project_amd/trainer.py's loop):
+// raw[3G + 3] in/out, the unconstrained parameters (d s b, l, obs_stddev) and the static jitter;
+// iters Adam steps (step0 = 0, fresh moments) with after_epoch every spe steps when fix; the loss
+// history[iters]. Returns the number of steps whose factorisation failed.
+int lfm_cpu_fit(const double* x, const double* y, int64_t n, int64_t G, double* raw, int64_t iters,
+                double lr, double b1, double b2, double eps, double eps_root, int64_t spe, int fix,
+                int negative, double* history) {
+  const int64_t np = 3 * G + 2;
+  std::vector<double> mu((size_t)np, 0.0), nu((size_t)np, 0.0), hyp((size_t)np), g((size_t)np), work;
+  int failed = 0;
+  for (int64_t s = 0; s < iters; ++s) {
+    for (int64_t i = 0; i < np; ++i)
+      hyp[i] = i == 3 * G ? 0.5 + 3.0 * sigmoid_c(raw[i]) : softplus_c(raw[i]);
+    const double v = mll_grad_cpu(x, y, n, G, hyp.data(), hyp.data() + G, hyp.data() + 2 * G,
+                                  hyp[3 * G], hyp[3 * G + 1], raw[3 * G + 2], negative, g.data(),
+                                  work);
+    if (std::isnan(v)) ++failed;
+    history[s] = v;
+    const double count = (double)(s + 1);
+    const double c1 = 1.0 - std::pow(b1, count), c2 = 1.0 - std::pow(b2, count);
+    for (int64_t i = 0; i < np; ++i) {
+      const double sg = sigmoid_c(raw[i]);
+      const double gr = i == 3 * G ? g[i] * 3.0 * sg * (1.0 - sg) : g[i] * sg;
+      mu[i] = b1 * mu[i] + (1.0 - b1) * gr;
+      nu[i] = b2 * nu[i] + (1.0 - b2) * (gr * gr);
+      raw[i] = raw[i] + -lr * (mu[i] / c1) / (std::sqrt(nu[i] / c2 + eps_root) + eps);
+    }
+    if (fix && s % spe == 0 && G > 3) {
+      raw[G + 3] = 1.0;
+      raw[3] = 0.8;
+    }
+  }
+  return failed;
 }
 
 }  // extern "C"

@@ -38,6 +38,12 @@ def load():
         lib.lfm_cpu_mll.restype = c_double
         lib.lfm_cpu_mll.argtypes = [_dp, _dp, c_int64, c_int64, _dp, _dp, _dp, c_double, c_double,
                                     c_double, c_int, c_int, _dp, _dp]
+        lib.lfm_cpu_mll_grad.restype = c_double
+        lib.lfm_cpu_mll_grad.argtypes = [_dp, _dp, c_int64, c_int64, _dp, _dp, _dp, c_double,
+                                         c_double, c_double, c_int, _dp]
+        lib.lfm_cpu_fit.restype = c_int
+        lib.lfm_cpu_fit.argtypes = [_dp, _dp, c_int64, c_int64, _dp, c_int64, c_double, c_double,
+                                    c_double, c_double, c_double, c_int64, c_int, c_int, _dp]
         _lib = lib
     return _lib
 
@@ -107,3 +113,28 @@ def potrf(A, threads=0):
     lib = load()
     assert A.dtype == np.float64 and A.flags.c_contiguous and A.shape[0] == A.shape[1]
     return int(lib.lfm_cpu_potrf(_p(A), A.shape[0], A.shape[0], int(threads)))
+
+
+def mll_grad(x, y, D, S, B, l, obs_stddev, jitter, negative=False):
+    """Value and gradient (constrained parameters) of CustomConjMLL(negative).step on one core:
+    (value, grad[3G + 2] = dD dS dB, dl, d obs_stddev)."""
+    lib = load()
+    x, y, D, S, B = (_f64(v) for v in (x, y, D, S, B))
+    x = x.reshape(-1, 3)
+    g = np.empty(3 * D.size + 2)
+    v = lib.lfm_cpu_mll_grad(_p(x), _p(y.reshape(-1)), x.shape[0], D.size, _p(D), _p(S), _p(B),
+                             float(l), float(obs_stddev), float(jitter), int(bool(negative)), _p(g))
+    return float(v), g
+
+
+def fit(x, y, G, raw, iters, lr=0.01, b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0, spe=1000,
+        fix=False, negative=True):
+    """JaxTrainer.fit of one problem on one core: raw [3G + 3] (d s b, l, obs_stddev, jitter;
+    unconstrained, the jitter static) is updated in place. Returns (history[iters], failures)."""
+    lib = load()
+    x, y = _f64(x).reshape(-1, 3), _f64(y).reshape(-1)
+    assert raw.dtype == np.float64 and raw.flags.c_contiguous and raw.size == 3 * G + 3
+    hist = np.empty(int(iters))
+    bad = lib.lfm_cpu_fit(_p(x), _p(y), x.shape[0], int(G), _p(raw), int(iters), lr, b1, b2, eps,
+                          eps_root, int(spe), int(bool(fix)), int(bool(negative)), _p(hist))
+    return hist, int(bad)

@@ -1,0 +1,143 @@
+"""Host side of the batched fit (CPU): the packed parameter layout of lfm_batch_fit_f64 /
+lfm_batch_mll_grad_f64, BatchTrainer's unpacking and final after_epoch (with a stand-in library),
+and the C++ port's gradient and fit (oracle/lfm_cpu.cpp, bench.py's c5fit CPU baseline) against
+the numpy oracle and the golden trajectories."""
+
+import ctypes
+
+import numpy as np
+import pytest
+
+from dis_project_amd import _lib, farm
+from dis_project_amd import trainer as TR
+from oracle import lfm_cpu
+from oracle import lfm_oracle as O
+from tests.conftest import load_golden
+
+
+def test_pack_unpack_round_trip():
+    models, _ = farm.workload("c5")
+    raws = [TR.unconstrain(m) for m in models]
+    packed = TR.pack_raw(raws, [m.jitter for m in models])
+    genes = [m.num_genes for m in models]
+    assert packed.size == sum(3 * g + 3 for g in genes)
+    # layout: every problem's d s b first, then every problem's l, obs_stddev, jitter
+    np.testing.assert_array_equal(packed[:4], raws[0]["true_d"])
+    assert packed[3 * sum(genes) + 2] == models[0].jitter
+    back = TR.unpack_raw(packed, genes)
+    for a, b in zip(back, raws):
+        for k in ("true_d", "true_s", "true_b"):
+            np.testing.assert_array_equal(a[k], b[k])
+        assert a["l"] == b["l"] and a["obs_stddev"] == b["obs_stddev"]
+    grads = farm.unpack_grads(packed, genes)
+    assert grads[3]["l"] == raws[3]["l"]
+
+
+class _FitLib:
+    """Stand-in for liblfm's batch entry points: records the arguments, moves every raw
+    parameter by +0.25 and writes a history."""
+
+    def __init__(self):
+        self.calls = []
+
+    def lfm_batch_create(self, handle, nprob, probs, out):
+        ctypes.cast(out, ctypes.POINTER(ctypes.c_void_p))[0] = 77
+        return 0
+
+    def lfm_batch_destroy(self, b):
+        return 0
+
+    def lfm_batch_fit_f64(self, handle, batch, opt, negative, step0, nsteps, raw, mu, nu, hist,
+                          status):
+        o = ctypes.cast(opt, ctypes.POINTER(_lib.LfmAdam))[0]
+        self.calls.append((o.learning_rate, o.num_steps_per_epoch, o.fix_params, negative, step0,
+                           nsteps))
+        n = sum(3 * 4 + 3 for _ in range(15))
+        r = np.ctypeslib.as_array(ctypes.cast(raw, ctypes.POINTER(ctypes.c_double)), (n,))
+        r[: 3 * 4 * 15] += 0.25
+        r[3 * 4 * 15:] += np.tile([0.25, 0.25, 0.0], 15)
+        h = np.ctypeslib.as_array(ctypes.cast(hist, ctypes.POINTER(ctypes.c_double)), (nsteps * 15,))
+        h[:] = np.arange(nsteps * 15)
+        return 0
+
+
+class _Ctx:
+    def __init__(self):
+        self.lib, self.handle = _FitLib(), None
+
+    def check(self, rc, allow_not_pd=False):
+        assert rc == 0
+        return rc
+
+
+def test_batch_trainer_host_logic():
+    from dis_project_amd.objectives import CustomConjMLL
+
+    models, datasets = farm.workload("c5")
+    ctx = _Ctx()
+    bt = TR.BatchTrainer(models, CustomConjMLL(negative=True), datasets, TR.adam(0.01),
+                         num_iters=3, ctx=ctx)
+    out, hist = bt.fit(fix_params=True, num_steps_per_epoch=7)
+    assert ctx.lib.calls == [(0.01, 7, 1, 1, 0, 3)]
+    assert hist.shape == (15, 3) and hist[1, 0] == 1.0  # [P, iters] from step-major
+    for m, r0 in zip(out, [TR.unconstrain(m) for m in models]):
+        want = TR.constrain({k: (np.asarray(v) + 0.25) for k, v in r0.items()}, m)
+        # after_epoch on the constrained model at the end (trainer.py:218-222): G = 4 > 3
+        assert m.true_s[3] == 1.0 and m.true_d[3] == 0.8
+        np.testing.assert_allclose(m.true_b, want.true_b, rtol=1e-15)
+        assert m.l == pytest.approx(want.l, rel=1e-15)
+        assert m.jitter == models[0].jitter
+    bt.close()
+
+
+def test_after_epoch_drops_out_of_bounds_like_jax():
+    p = {"true_s": np.array([1.5, 2.0]), "true_d": np.array([0.3, 0.4])}
+    q = TR.JaxTrainer.after_epoch(p, True)
+    np.testing.assert_array_equal(q["true_s"], p["true_s"])
+    np.testing.assert_array_equal(q["true_d"], p["true_d"])
+
+
+def test_cpu_port_gradient_matches_oracle():
+    g = load_golden("c1_p53_n35")
+    models, datasets = farm.workload("c5")
+    cases = [(g["x"], g["y"], g["D"], g["S"], g["B"], float(g["l"]), float(g["obs_stddev"]),
+              float(g["jitter"]))]
+    cases += [(d.X, d.y, m.true_d, m.true_s, m.true_b, m.l, m.obs_stddev, m.jitter)
+              for m, d in zip(models[:3], datasets[:3])]
+    x = cases[-1][0].copy()
+    x[[1, 5], 2] = 0.0  # latent rows: kernel_xf / kernel_ff terms
+    cases.append((x,) + cases[-1][1:])
+    for neg in (True, False):
+        for c in cases:
+            v, gr = lfm_cpu.mll_grad(*c, negative=neg)
+            ref = O.mll_grad(*c, negative=neg)
+            G = len(c[2])
+            want = np.concatenate([ref["d"], ref["s"], ref["b"], [ref["l"], ref["obs_stddev"]]])
+            scale = np.concatenate([ref["scale_d"], ref["scale_s"], ref["scale_b"],
+                                    [ref["scale_l"], ref["scale_obs_stddev"]]])
+            assert abs(v - ref["value"]) <= 1e-12 * abs(ref["value"])
+            assert np.all(np.abs(gr - want) <= 1e-12 * scale), (np.abs(gr - want) / scale).max()
+            assert gr.size == 3 * G + 2
+
+
+@pytest.mark.parametrize("case", ["fit_c5", "fit_c1_epoch"])
+def test_cpu_port_fit_matches_golden(case):
+    ref = load_golden(case)
+    from dis_project_amd import configs
+
+    if case == "fit_c5":
+        models, datasets = farm.workload("c5")
+    else:
+        c1 = configs.c1_p53()
+        models, datasets = [c1.model], [c1.data]
+    genes = [int(g) for g in ref["genes"]]
+    nvec = 3 * sum(genes)
+    raw0, off = ref["raw0"], 0
+    for p, (m, d) in enumerate(zip(models, datasets)):
+        G = genes[p]
+        r = np.concatenate([raw0[off:off + 3 * G], raw0[nvec + 3 * p: nvec + 3 * p + 3]])
+        off += 3 * G
+        h, bad = lfm_cpu.fit(d.X, d.y, G, r, int(ref["iters"]), spe=int(ref["spe"]),
+                             fix=bool(ref["fix_params"]))
+        assert bad == 0
+        np.testing.assert_allclose(h, ref["hist"][p], rtol=1e-11)
