@@ -621,13 +621,23 @@ def main(argv=None):
     else:
         models, datasets = farm.workload(a.workload, a.genes, a.timepoints, a.restarts)
         n = datasets[0].n
-        mine = len(farm.partition(len(models), world, rank))
-        workers = a.workers if a.workers > 0 else farm.choose_workers(mine)
-        evaluate, close = farm.gpu_evaluator(ctx, datasets, negative=False, workers=workers)
+        mine = farm.partition(len(models), world, rank)
+        workers = a.workers if a.workers > 0 else farm.choose_workers(len(mine))
         per_step = len(models)
+        if a.workload == "c5" and exchange == "rccl" and len(mine):
+            # the device-side round: this rank's block evaluated straight into its RCCL send
+            # slots, all-gathered on the device, published to the host (lfm_farm_batch_mll_f64)
+            my_models = [models[i] for i in mine]
+            fev = farm.BatchEvaluator(ctx, [datasets[i] for i in mine])
+            close = fev.close
 
-        def step():
-            return fm.run_problems(models, datasets, evaluate)
+            def step():
+                return fm.run_fused(len(models), lambda slots: fev.farm_round(my_models, slots))
+        else:
+            evaluate, close = farm.gpu_evaluator(ctx, datasets, negative=False, workers=workers)
+
+            def step():
+                return fm.run_problems(models, datasets, evaluate)
 
     results = []
 
@@ -695,6 +705,10 @@ def main(argv=None):
                              "gloo-fallback": "gloo all_gather (RCCL init failed)"}[exchange],
                       "bytes_per_rank": 8 * slots,
                       "latency_us_median": float(lt.item())}
+        if a.workload == "c5" and exchange == "rccl":
+            collective["in_step"] = ("chained on the device: batch kernel -> ncclAllGather -> "
+                                     "publish kernel, one bounded host wait "
+                                     "(lfm_farm_batch_mll_f64)")
     elif a.workload in ("c3", "c5"):
         # one GPU: the library's exchange path alone on a 1-rank RCCL communicator (staging
         # copies, enqueue, the bounded host wait; no xGMI transfer) — the floor the W > 1
@@ -714,6 +728,31 @@ def main(argv=None):
                                 "no xGMI transfer)",
                           "bytes_per_rank": 8 * slots,
                           "latency_us_median": float(np.median(lat[20:]))}
+            if a.workload == "c5":
+                # the whole device-side round on a 1-rank communicator: the batch kernel writing
+                # its send slots, ncclAllGather behind it, the publish kernel, one host wait —
+                # what a step costs per rank at W > 1 less the xGMI transfer itself
+                g1 = farm.RcclGather(ctx, 1, 0, farm.RcclGather.unique_id(ctx))
+                fev1 = farm.BatchEvaluator(ctx, datasets)
+                try:
+                    f1 = farm.Farm(1, 0, None)
+                    want = np.asarray(timed[0])
+                    rl = []
+                    for i in range(300):
+                        t1 = time.perf_counter()
+                        got = f1.run_fused(len(models), lambda s_: fev1.farm_round(models, s_))
+                        rl.append((time.perf_counter() - t1) * 1e6)
+                    if not np.array_equal(got, want):
+                        raise SystemExit("the device-side farm round disagrees with the step")
+                finally:
+                    fev1.close()
+                    g1.close()
+                collective["chained_round_us_median"] = float(np.median(rl[50:]))
+                collective["chained_round"] = ("batch kernel -> ncclAllGather (1 rank) -> "
+                                               "publish kernel, one host wait "
+                                               "(lfm_farm_batch_mll_f64)")
+        except SystemExit:
+            raise
         except Exception as e:  # noqa: BLE001
             collective = {"op": "ncclAllGather (RCCL, 1 rank)", "error": str(e)}
     # the timed region's results: all finite, every step the same values (same inputs)

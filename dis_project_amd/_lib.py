@@ -162,6 +162,7 @@ PRODUCT_SIGNATURES = [
     ("lfm_farm_unique_id", c_int, [_c_ctx, POINTER(ctypes.c_ubyte)]),
     ("lfm_farm_init", c_int, [_c_ctx, POINTER(ctypes.c_ubyte), c_int, c_int]),
     ("lfm_farm_allgather_f64", c_int, [_c_ctx, _dptr, c_int64, _dptr]),
+    ("lfm_farm_batch_mll_f64", c_int, [_c_ctx, c_void_p, _dptr, c_int, c_int64, _dptr, _dptr]),
     ("lfm_farm_destroy", c_int, [_c_ctx]),
 ]
 
@@ -284,6 +285,7 @@ class Context:
                                f"{n.value}. liblfm needs an MI355X (gfx950); there is no CPU fallback.")
         self.handle = h
         self.device = int(device)
+        self.farm_ranks = 1  # ranks of this context's farm communicator (farm.RcclGather)
 
     # -- error plumbing
     def check(self, rc: int, allow_not_pd: bool = False) -> int:

@@ -762,6 +762,7 @@ void lfm_ctx_destroy(lfm_ctx* ctx) {
     if (p) hipFree(p);
   if (ctx->hpin) hipHostFree(ctx->hpin);
   if (ctx->farm_h) hipHostFree(ctx->farm_h);
+  if (ctx->farm_pub) hipHostFree(ctx->farm_pub);
   for (auto& p : ctx->pending) {
     hipEventDestroy(p.a);
     hipEventDestroy(p.b);
@@ -1351,15 +1352,15 @@ int lfm_batch_destroy(lfm_batch* batch) {
   return LFM_OK;
 }
 
-int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative,
-                      double* out, int* status) {
-  if (!ctx) return LFM_E_ARG;
-  if (!batch || !hyp || !out) return set_err(ctx, LFM_E_ARG, "batch / hyp / out is NULL");
-  if (batch->device != ctx->device) return set_err(ctx, LFM_E_ARG, "batch of another device");
-  DeviceGuard g(ctx->device);
+}  // extern "C"
+
+namespace {
+// One launch of the batch's MLL kernel: results to `out` (the pinned buffer, or a device buffer
+// such as the farm's send slots), the status words (reset to -1 here, each written last by its
+// workgroup after a system-scope fence) to the pinned buffer.
+int batch_launch(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative, double* out) {
   const int64_t np = batch->nprob;
-  double* hres = batch->hbuf + batch->nhyp;
-  int* hst = reinterpret_cast<int*>(hres + np);
+  int* hst = reinterpret_cast<int*>(batch->hbuf + batch->nhyp + np);
   for (int64_t q = 0; q < np; ++q) hst[q] = -1;  // a problem's status word is written last
   int r;
   if (batch->use_args) {
@@ -1369,54 +1370,25 @@ int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int neg
     std::memcpy(a.hyp, hyp, (size_t)batch->nhyp * 8);
     std::memcpy(a.dsb_off, batch->dsb_off.data(), (size_t)np * sizeof(int));
     std::memcpy(a.sc_off, batch->sc_off.data(), (size_t)np * sizeof(int));
-    a.out = hres;
+    a.out = out;
     a.status = hst;
     a.negative = negative;
     r = launch_small_args(ctx, a, (int)np, batch->maxn, batch->maxg, batch->gridtab);
   } else {
     std::memcpy(batch->hbuf, hyp, (size_t)batch->nhyp * 8);
     r = launch_small_batch(ctx, batch->dprobs, (int)np, batch->maxn, batch->maxg,
-                           batch->gridtab, negative, hres, hst);
+                           batch->gridtab, negative, out, hst);
   }
   if (r) return r;
   hipEventRecord(batch->done, ctx->stream);
-  // Completion: every workgroup writes its result, a system-scope fence, then its status word
-  // (>= 0) into this pinned buffer, after it has read the hyperparameters, so the results are
-  // complete and the buffer free once no status word is -1: the host spins on them (~µs sooner
-  // than the kernel's end-of-dispatch signal behind hipStreamSynchronize). Past 20 ms, or when
-  // profiling (the events want the stream), it synchronises the stream instead, which also
-  // surfaces a kernel fault.
-  bool landed = false;
-  if (!ctx->prof) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (;;) {
-      landed = true;
-      for (int64_t q = 0; q < np && landed; ++q)
-        landed = __atomic_load_n(&hst[q], __ATOMIC_ACQUIRE) != -1;
-      if (landed || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
-      __builtin_ia32_pause();
-    }
-  }
-  if (!landed) {
-    r = finish(ctx);
-    if (r) return r;
-  }
-  int worst = LFM_OK;
-  for (int64_t q = 0; q < np; ++q) {
-    out[q] = hres[q];
-    const int s = hst[q] ? LFM_E_NOT_PD : LFM_OK;
-    if (status) status[q] = s;
-    if (s) worst = s;
-  }
-  if (worst) set_err(ctx, LFM_E_NOT_PD, "Cholesky failed: non-positive pivot in a batch problem");
-  return worst;
+  return LFM_OK;
 }
 
 // The host side of a call whose kernel writes results and status words into the batch's
 // pinned buffer: spin on the status words (each written last, after a system-scope fence, by
-// its workgroup), past 20 ms or while profiling synchronise the stream instead (which also
-// surfaces a kernel fault).
-namespace {
+// its workgroup; ~µs sooner than the kernel's end-of-dispatch signal behind
+// hipStreamSynchronize); past 20 ms, or while profiling (the events want the stream),
+// synchronise the stream instead, which also surfaces a kernel fault.
 int batch_wait(lfm_ctx* ctx, int64_t np, const int* hst) {
   bool landed = false;
   if (!ctx->prof) {
@@ -1431,7 +1403,38 @@ int batch_wait(lfm_ctx* ctx, int64_t np, const int* hst) {
   }
   return landed ? LFM_OK : finish(ctx);
 }
+
+// statuses of the batch's last call -> status[] (optional); LFM_E_NOT_PD if any problem failed
+int batch_status(lfm_ctx* ctx, const lfm_batch* batch, int* status) {
+  const int* hst = reinterpret_cast<const int*>(batch->hbuf + batch->nhyp + batch->nprob);
+  int worst = LFM_OK;
+  for (int64_t q = 0; q < batch->nprob; ++q) {
+    const int s = hst[q] ? LFM_E_NOT_PD : LFM_OK;
+    if (status) status[q] = s;
+    if (s) worst = s;
+  }
+  if (worst) set_err(ctx, LFM_E_NOT_PD, "Cholesky failed: non-positive pivot in a batch problem");
+  return worst;
+}
 }  // namespace
+
+extern "C" {
+
+int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative,
+                      double* out, int* status) {
+  if (!ctx) return LFM_E_ARG;
+  if (!batch || !hyp || !out) return set_err(ctx, LFM_E_ARG, "batch / hyp / out is NULL");
+  if (batch->device != ctx->device) return set_err(ctx, LFM_E_ARG, "batch of another device");
+  DeviceGuard g(ctx->device);
+  const int64_t np = batch->nprob;
+  double* hres = batch->hbuf + batch->nhyp;
+  int r = batch_launch(ctx, batch, hyp, negative, hres);
+  if (r) return r;
+  r = batch_wait(ctx, np, reinterpret_cast<const int*>(hres + np));
+  if (r) return r;
+  std::memcpy(out, hres, (size_t)np * 8);
+  return batch_status(ctx, batch, status);
+}
 
 int lfm_batch_mll_grad_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative,
                            double* value, double* grad, int* status) {
@@ -1690,6 +1693,19 @@ __global__ void stall_kernel(unsigned long long ticks) {
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
+// The end of a device-side farm round: the gathered slots to pinned host memory (system-scope
+// stores), a system-scope fence, then the round's sequence number — the host's completion signal
+// (it spins on that word instead of synchronising the stream: microseconds sooner).
+__global__ __launch_bounds__(256) void farm_publish_kernel(const double* __restrict__ src,
+                                                          int64_t count, double* __restrict__ dst,
+                                                          unsigned* seq_word, unsigned seq) {
+  for (int64_t i = threadIdx.x; i < count; i += 256) dst[i] = src[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0)
+    __hip_atomic_store(seq_word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct Rccl {
   void* h = nullptr;
   ncclResult_t (*getUniqueId)(ncclUniqueId*) = nullptr;
@@ -1756,6 +1772,10 @@ struct Backoff {
 
 // End a communicator after a failed or timed-out operation: ncclCommAbort (a non-blocking
 // communicator's pending kernels are released), and the context forgets it.
+// Work the aborted call left queued on the stream (its copies into the farm's pinned staging,
+// its publish kernel) may still run: farm_stale makes the next call drain it first (bounded), and
+// abandon the staging buffers if it does not drain (a bounded leak instead of a late write into
+// memory the next call is using).
 void rccl_drop(lfm_ctx* ctx) {
   if (!ctx->comm) return;
   if (g_rccl.commAbort) g_rccl.commAbort((ncclComm_t)ctx->comm);
@@ -1763,6 +1783,7 @@ void rccl_drop(lfm_ctx* ctx) {
   ctx->comm = nullptr;
   ctx->nranks = 0;
   ctx->rank = -1;
+  ctx->farm_stale = true;
 }
 
 // Poll a non-blocking communicator until its pending operation leaves ncclInProgress.
@@ -1851,10 +1872,144 @@ int lfm_farm_init(lfm_ctx* ctx, const unsigned char id[128], int nranks, int ran
   return LFM_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// Before a farm call writes its host staging: work a dropped (timed-out) call left queued is
+// drained, within the communicator's time bound; if it does not drain, the staging buffers it
+// could still write are abandoned (never freed, never reused) and fresh ones are made.
+int farm_drain_stale(lfm_ctx* ctx) {
+  if (!ctx->farm_stale) return LFM_OK;
+  const double end = mono_s() + std::min(rccl_timeout_s(ctx), 5.0);
+  const Backoff bo;
+  hipError_t e;
+  while ((e = hipStreamQuery(ctx->stream)) == hipErrorNotReady && mono_s() < end) bo.pause();
+  if (e == hipErrorNotReady) {
+    ctx->farm_h = nullptr;  // abandoned: a queued copy may still land in it
+    ctx->farm_h_bytes = 0;
+    ctx->farm_pub = nullptr;
+    ctx->farm_pub_bytes = 0;
+    ctx->farm_buf = nullptr;  // (device) the same for the queued collective's buffers
+    ctx->farm_bytes = 0;
+  } else if (e != hipSuccess) {
+    return hip_fail(ctx, e, "draining the aborted farm call");
+  }
+  ctx->farm_stale = false;
+  return LFM_OK;
+}
+
+// The device-side round's buffers: send [slots] | recv [nranks slots] on the device, the
+// publish target (recv's copy + a sequence word) in coherent pinned host memory.
+int farm_buffers(lfm_ctx* ctx, size_t slots) {
+  const size_t in = slots * 8, out = in * ctx->nranks;
+  int r = ensure(ctx, (void**)&ctx->farm_buf, &ctx->farm_bytes, in + out);
+  if (r) return r;
+  const size_t pub = out + 64;
+  if (!ctx->farm_pub || ctx->farm_pub_bytes < pub) {
+    if (ctx->farm_pub) {
+      hipStreamSynchronize(ctx->stream);
+      hipHostFree(ctx->farm_pub);
+      ctx->farm_pub = nullptr;
+    }
+    hipError_t e = hipHostMalloc((void**)&ctx->farm_pub, pub, hipHostMallocCoherent);
+    if (e != hipSuccess) return hip_fail(ctx, e, "farm publish buffer");
+    ctx->farm_pub_bytes = pub;
+  }
+  return LFM_OK;
+}
+
+// Enqueue the all-gather of `slots` doubles per rank (send -> recv, device) and the publish of
+// recv to the pinned host buffer, then wait (bounded) for the round's sequence word; on any error
+// or timeout the communicator is aborted (LFM_E_RCCL / LFM_E_HIP) and nothing is copied out.
+int farm_gather_publish(lfm_ctx* ctx, int64_t slots, double* recv) {
+  double* dsend = ctx->farm_buf;
+  double* drecv = ctx->farm_buf + slots;
+  const int64_t count = slots * ctx->nranks;
+  unsigned* seq_word = reinterpret_cast<unsigned*>(ctx->farm_pub + count);
+  // test instrument: a collective whose peers are late (LFM_DEBUG_FARM_STALL_MS)
+  if (const int stall = ctx->farm_stall_ms)
+    hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, ctx->stream,
+                       (unsigned long long)stall * 100000ull);
+  const ncclResult_t q = g_rccl.allGather(dsend, drecv, (size_t)slots, ncclFloat64,
+                                         (ncclComm_t)ctx->comm, ctx->stream);
+  int r = ctx->comm_nb && q == ncclInProgress ? rccl_poll(ctx, (ncclComm_t)ctx->comm, "ncclAllGather")
+                                               : rccl_fail(ctx, q, "ncclAllGather");
+  if (r) {
+    rccl_drop(ctx);
+    return r;
+  }
+  const unsigned seq = ++ctx->farm_seq;
+  hipLaunchKernelGGL(farm_publish_kernel, dim3(1), dim3(256), 0, ctx->stream, drecv, count,
+                     ctx->farm_pub, seq_word, seq);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    rccl_drop(ctx);
+    return hip_fail(ctx, e, "farm publish");
+  }
+  // one bounded wait for the whole chain (kernel, collective, publish): the sequence word, with
+  // the stream polled now and then so a fault surfaces instead of running out the bound
+  const double end = mono_s() + rccl_timeout_s(ctx);
+  const Backoff bo;
+  for (unsigned it = 0;; ++it) {
+    if (__atomic_load_n(seq_word, __ATOMIC_ACQUIRE) == seq) break;
+    if ((it & 1023) == 1023) {
+      e = hipStreamQuery(ctx->stream);
+      if (e != hipSuccess && e != hipErrorNotReady) {
+        rccl_drop(ctx);
+        return hip_fail(ctx, e, "farm round");
+      }
+      if (e == hipSuccess && __atomic_load_n(seq_word, __ATOMIC_ACQUIRE) != seq) {
+        rccl_drop(ctx);
+        return set_err(ctx, LFM_E_HIP, "farm round: the stream drained without publishing");
+      }
+      const double now = mono_s();
+      if (now > end) {
+        char waited[64];
+        std::snprintf(waited, sizeof(waited), " after %.2f s", now - bo.t0);
+        rccl_drop(ctx);
+        return set_err(ctx, LFM_E_RCCL, std::string("farm round: timed out") + waited +
+                                            " (a peer rank did not arrive)");
+      }
+      bo.pause();
+    }
+    __builtin_ia32_pause();
+  }
+  std::memcpy(recv, ctx->farm_pub, (size_t)count * 8);
+  return LFM_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int lfm_farm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative,
+                           int64_t slots, double* recv, int* status) {
+  if (!ctx) return LFM_E_ARG;
+  if (!batch || !hyp || !recv || slots < batch->nprob || slots < 1)
+    return set_err(ctx, LFM_E_ARG, "bad farm round arguments (slots >= nprob >= 1)");
+  if (batch->device != ctx->device) return set_err(ctx, LFM_E_ARG, "batch of another device");
+  if (!ctx->comm) return set_err(ctx, LFM_E_STATE, "farm not initialised");
+  DeviceGuard g(ctx->device);
+  int r = farm_drain_stale(ctx);
+  if (!r) r = farm_buffers(ctx, (size_t)slots);
+  if (r) return r;
+  // this rank's padding slots: NaN (all-ones bytes), then the kernel writes its nprob slots
+  if (slots > batch->nprob)
+    hipMemsetAsync(ctx->farm_buf + batch->nprob, 0xFF, (size_t)(slots - batch->nprob) * 8,
+                   ctx->stream);
+  r = batch_launch(ctx, batch, hyp, negative, ctx->farm_buf);
+  if (r) return r;
+  r = farm_gather_publish(ctx, slots, recv);
+  if (r) return r;
+  // the statuses landed before the kernel retired, and the kernel before the collective
+  return batch_status(ctx, batch, status);
+}
+
 int lfm_farm_allgather_f64(lfm_ctx* ctx, const double* send, int64_t count, double* recv) {
   if (!ctx || !send || !recv || count < 1) return LFM_E_ARG;
   if (!ctx->comm) return set_err(ctx, LFM_E_STATE, "farm not initialised");
   DeviceGuard g(ctx->device);
+  int rs = farm_drain_stale(ctx);
+  if (rs) return rs;
   const size_t in = (size_t)count * 8, out = in * ctx->nranks;
   int r = ensure(ctx, (void**)&ctx->farm_buf, &ctx->farm_bytes, in + out);
   if (r) return r;

@@ -122,6 +122,10 @@ struct lfm_ctx {
   double* farm_h = nullptr; size_t farm_h_bytes = 0;  // pinned host staging of the all-gather
                                                       // (its own: a copy left queued by a timed-
                                                       // out call can only ever write here)
+  double* farm_pub = nullptr; size_t farm_pub_bytes = 0;  // coherent pinned: the device-side
+                                                          // round's gathered slots + seq word
+  unsigned farm_seq = 0;    // device-side rounds published so far
+  bool farm_stale = false;  // an aborted farm call may have left work queued (drained first)
 };
 
 // ---------------------------------------------------------------- helpers

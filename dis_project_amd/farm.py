@@ -43,6 +43,7 @@ class RcclGather:
         self.ctx, self.world, self.rank = ctx, world, rank
         buf = (_lib.ctypes.c_ubyte * 128).from_buffer_copy(uid)
         ctx.check(ctx.lib.lfm_farm_init(ctx.handle, buf, world, rank))
+        ctx.farm_ranks = world  # the device-side rounds' receive size (BatchEvaluator.farm_round)
 
     @staticmethod
     def unique_id(ctx: _lib.Context) -> bytes:
@@ -218,6 +219,20 @@ class BatchEvaluator:
         self.ctx.check(rc, allow_not_pd=True)
         return self._out.copy()
 
+    def farm_round(self, models, slots: int) -> np.ndarray:
+        """One device-side farm round (``lfm_farm_batch_mll_f64``): this rank's problems
+        evaluated straight into its ``slots`` RCCL send slots (NaN-padded), all-gathered on the
+        device and published to the host in one chain; returns every rank's slots
+        [nranks * slots]. The context's communicator must be initialised (RcclGather)."""
+        self._pack(models)
+        nranks = max(1, int(getattr(self.ctx, "farm_ranks", 1)))
+        recv = np.empty(nranks * int(slots))
+        rc = self.ctx.lib.lfm_farm_batch_mll_f64(self.ctx.handle, self.batch, self._buf_ptr,
+                                                 int(self.negative), int(slots), _lib.dptr(recv),
+                                                 self._st_ptr)
+        self.ctx.check(rc, allow_not_pd=True)
+        return recv
+
     def value_and_grad(self, models):
         """Every problem's value and gradient (constrained parameters, as
         ``CustomConjMLL.value_and_grad``) in ONE launch (``lfm_batch_mll_grad_f64``; n <= 63 per
@@ -285,6 +300,19 @@ class Farm:
                 raise ValueError("evaluate returned the wrong number of values")
             send[: len(mine)] = vals
         recv = self.gather(send).reshape(self.world, -1)
+        out = np.empty(nprob)
+        for r in range(self.world):
+            rr = partition(nprob, self.world, r)
+            out[rr.start:rr.stop] = recv[r, : len(rr)]
+        return out
+
+    def run_fused(self, nprob: int, round_fn: Callable[[int], np.ndarray]) -> np.ndarray:
+        """One round whose evaluation and exchange are a single device-side chain:
+        ``round_fn(slots) -> recv`` evaluates this rank's block into its NaN-padded ``slots``
+        and returns every rank's slots, gathered (BatchEvaluator.farm_round over RCCL).
+        Returns every problem's value, in problem order."""
+        per = max(slots_per_rank(nprob, self.world), 1)
+        recv = np.asarray(round_fn(per), dtype=np.float64).reshape(self.world, -1)
         out = np.empty(nprob)
         for r in range(self.world):
             rr = partition(nprob, self.world, r)

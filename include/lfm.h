@@ -285,6 +285,17 @@ int lfm_farm_unique_id(lfm_ctx* ctx, unsigned char id[128]);
 int lfm_farm_init(lfm_ctx* ctx, const unsigned char id[128], int nranks, int rank);
 /* All-gather count fp64 per rank (host in, host out: recv holds nranks*count). */
 int lfm_farm_allgather_f64(lfm_ctx* ctx, const double* send, int64_t count, double* recv);
+/* One farm round of a resident batch — the replicate x ablation problems of
+ * src/notebook.py:33-75, each rank holding its block of them (lfm_batch_create) — with the
+ * exchange on the device: the batch's kernel writes every problem's MLL straight into this rank's
+ * `slots` send slots (NaN past nprob), ncclAllGather runs on the ctx's stream behind it, and a
+ * publish kernel copies the gathered nranks x slots values to pinned host memory and signals the
+ * host: one launch chain, one bounded wait (LFM_RCCL_TIMEOUT_S), recv[nranks * slots] filled.
+ * hyp / negative / status as lfm_batch_mll_f64 (status: this rank's problems). A failed or timed-
+ * out exchange aborts the communicator (LFM_E_RCCL; recv untouched; later calls LFM_E_STATE until
+ * lfm_farm_init). slots >= nprob, else LFM_E_ARG. */
+int lfm_farm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative,
+                           int64_t slots, double* recv, int* status);
 int lfm_farm_destroy(lfm_ctx* ctx);
 
 #ifdef __cplusplus

@@ -450,3 +450,97 @@ def test_resident_batch_memory_path_follows_changed_hyperparameters(monkeypatch,
     finally:
         ev.close()
         ctx.close()
+
+
+def test_run_fused_unpacks_the_gathered_slots():
+    """Farm.run_fused (host side of the device-side round): round_fn gets the NaN-padded slot
+    count, returns every rank's slots; the values come back in problem order."""
+    for world, nprob in ((1, 15), (2, 15), (4, 15), (8, 15), (3, 2)):
+        per = farm.slots_per_rank(nprob, world)
+
+        def round_fn(slots, world=world, nprob=nprob):
+            assert slots == max(per, 1)
+            recv = np.full((world, slots), np.nan)
+            for r in range(world):
+                rr = farm.partition(nprob, world, r)
+                recv[r, : len(rr)] = np.arange(rr.start, rr.stop) * 1.5
+            return recv.reshape(-1)
+
+        for rank in range(world):
+            out = farm.Farm(world, rank, None).run_fused(nprob, round_fn)
+            np.testing.assert_array_equal(out, np.arange(nprob) * 1.5)
+
+
+@pytest.mark.gpu
+def test_device_farm_round_one_rank():
+    """lfm_farm_batch_mll_f64 on a 1-rank communicator: the kernel writes the send slots, RCCL
+    gathers them on the device and the publish kernel signals the host — the values are the
+    resident batch's bit for bit, padding slots NaN, statuses as the batch's; repeated rounds with
+    changed hyperparameters follow them."""
+    from dis_project_amd import _lib
+
+    ctx = _lib.Context(0)
+    try:
+        g = farm.RcclGather(ctx, 1, 0, farm.RcclGather.unique_id(ctx))
+        models, datasets = farm.workload("c5")
+        ev = farm.BatchEvaluator(ctx, datasets)
+        try:
+            want = ev(models)
+            got = ev.farm_round(models, 15)
+            np.testing.assert_array_equal(got, want)
+            padded = ev.farm_round(models, 19)
+            np.testing.assert_array_equal(padded[:15], want)
+            assert np.all(np.isnan(padded[15:]))
+            for k in range(3):
+                moved = [m.replace(l=m.l * (1.0 + 0.1 * k)) for m in models]
+                np.testing.assert_array_equal(ev.farm_round(moved, 15), ev(moved))
+            bad = list(models)
+            bad[2] = models[2].replace(jitter=-50.0, obs_stddev=0.0)
+            out = ev.farm_round(bad, 15)
+            assert np.isnan(out[2]) and ev.status[2] != 0 and not np.any(ev.status[3:])
+            with pytest.raises(_lib.LfmError) as ei:
+                ev.farm_round(models, 14)  # fewer slots than problems
+            assert ei.value.code == _lib.LFM_E_ARG
+        finally:
+            ev.close()
+            g.close()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.gpu
+def test_device_farm_round_stalled_peer_is_bounded(monkeypatch):
+    """The device-side round with a collective whose peers never arrive (the stand-in stall
+    kernel ahead of the all-gather, LFM_DEBUG_FARM_STALL_MS, read at context creation): the
+    bounded wait gives up after LFM_RCCL_TIMEOUT_S with LFM_E_RCCL, the communicator is aborted
+    (next call LFM_E_STATE) and the caller's receive buffer is never written."""
+    import time
+
+    from dis_project_amd import _lib
+
+    monkeypatch.setenv("LFM_RCCL_TIMEOUT_S", "1")
+    monkeypatch.setenv("LFM_DEBUG_FARM_STALL_MS", "3000")
+    ctx = _lib.Context(0)
+    try:
+        farm.RcclGather(ctx, 1, 0, farm.RcclGather.unique_id(ctx))
+        models, datasets = farm.workload("c5")
+        ev = farm.BatchEvaluator(ctx, datasets)
+        try:
+            ev.registered([m.num_genes for m in models])
+            ev._pack(models)
+            recv = np.full(15, -7.0)
+            t0 = time.monotonic()
+            rc = ctx.lib.lfm_farm_batch_mll_f64(ctx.handle, ev.batch, ev._buf_ptr, 0, 15,
+                                                _lib.dptr(recv), None)
+            dt = time.monotonic() - t0
+            assert rc == _lib.LFM_E_RCCL, (rc, ctx.lib.lfm_last_error(ctx.handle))
+            assert b"did not arrive" in ctx.lib.lfm_last_error(ctx.handle)
+            assert dt < 8.0, dt
+            np.testing.assert_array_equal(recv, -7.0)
+            assert ctx.lib.lfm_farm_batch_mll_f64(ctx.handle, ev.batch, ev._buf_ptr, 0, 15,
+                                                  _lib.dptr(recv), None) == _lib.LFM_E_STATE
+            np.testing.assert_array_equal(recv, -7.0)
+        finally:
+            ev.close()
+    finally:
+        ctx.close()
