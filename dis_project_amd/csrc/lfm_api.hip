@@ -1699,7 +1699,7 @@ __global__ void stall_kernel(unsigned long long ticks) {
 __global__ __launch_bounds__(256) void farm_publish_kernel(const double* __restrict__ src,
                                                           int64_t count, double* __restrict__ dst,
                                                           unsigned* seq_word, unsigned seq) {
-  for (int64_t i = threadIdx.x; i < count; i += 256) dst[i] = src[i];
+  for (int64_t i = threadIdx.x; i < count; i += blockDim.x) dst[i] = src[i];
   __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0)
@@ -1939,40 +1939,41 @@ int farm_gather_publish(lfm_ctx* ctx, int64_t slots, double* recv) {
     return r;
   }
   const unsigned seq = ++ctx->farm_seq;
-  hipLaunchKernelGGL(farm_publish_kernel, dim3(1), dim3(256), 0, ctx->stream, drecv, count,
+  hipLaunchKernelGGL(farm_publish_kernel, dim3(1), dim3(64), 0, ctx->stream, drecv, count,
                      ctx->farm_pub, seq_word, seq);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     rccl_drop(ctx);
     return hip_fail(ctx, e, "farm publish");
   }
-  // one bounded wait for the whole chain (kernel, collective, publish): the sequence word, with
-  // the stream polled now and then so a fault surfaces instead of running out the bound
+  // one bounded wait for the whole chain (kernel, collective, publish): the sequence word — a
+  // tight spin for the first 2 ms (a round takes tens of microseconds), then the stream is
+  // polled between backed-off checks, so a fault surfaces instead of running out the bound
   const double end = mono_s() + rccl_timeout_s(ctx);
   const Backoff bo;
-  for (unsigned it = 0;; ++it) {
-    if (__atomic_load_n(seq_word, __ATOMIC_ACQUIRE) == seq) break;
-    if ((it & 1023) == 1023) {
-      e = hipStreamQuery(ctx->stream);
-      if (e != hipSuccess && e != hipErrorNotReady) {
-        rccl_drop(ctx);
-        return hip_fail(ctx, e, "farm round");
-      }
-      if (e == hipSuccess && __atomic_load_n(seq_word, __ATOMIC_ACQUIRE) != seq) {
-        rccl_drop(ctx);
-        return set_err(ctx, LFM_E_HIP, "farm round: the stream drained without publishing");
-      }
-      const double now = mono_s();
-      if (now > end) {
-        char waited[64];
-        std::snprintf(waited, sizeof(waited), " after %.2f s", now - bo.t0);
-        rccl_drop(ctx);
-        return set_err(ctx, LFM_E_RCCL, std::string("farm round: timed out") + waited +
-                                            " (a peer rank did not arrive)");
-      }
-      bo.pause();
-    }
+  const auto t_spin = std::chrono::steady_clock::now() + std::chrono::milliseconds(2);
+  while (__atomic_load_n(seq_word, __ATOMIC_ACQUIRE) != seq &&
+         std::chrono::steady_clock::now() < t_spin)
     __builtin_ia32_pause();
+  while (__atomic_load_n(seq_word, __ATOMIC_ACQUIRE) != seq) {
+    e = hipStreamQuery(ctx->stream);
+    if (e != hipSuccess && e != hipErrorNotReady) {
+      rccl_drop(ctx);
+      return hip_fail(ctx, e, "farm round");
+    }
+    if (e == hipSuccess && __atomic_load_n(seq_word, __ATOMIC_ACQUIRE) != seq) {
+      rccl_drop(ctx);
+      return set_err(ctx, LFM_E_HIP, "farm round: the stream drained without publishing");
+    }
+    const double now = mono_s();
+    if (now > end) {
+      char waited[64];
+      std::snprintf(waited, sizeof(waited), " after %.2f s", now - bo.t0);
+      rccl_drop(ctx);
+      return set_err(ctx, LFM_E_RCCL, std::string("farm round: timed out") + waited +
+                                          " (a peer rank did not arrive)");
+    }
+    bo.pause();
   }
   std::memcpy(recv, ctx->farm_pub, (size_t)count * 8);
   return LFM_OK;
