@@ -6,6 +6,8 @@
 ``C3``  C2 data x 32 random restarts (raw ~ N(0,1) -> Softplus / Sigmoid(0.5, 3.5)).
 ``C4``  256 genes x 256 timepoints, N = 65536, fp32 gram fill.
 ``C5``  3 replicates x 5 leave-one-gene-out ablations, N = 28 each (notebook.py:33-75).
+``notebook_pooled``  the notebook's own fit data: the 3 replicates pooled (replicate=None,
+        notebook.py:36), the 5 genes (N = 105) and their 5 leave-one-gene-out ablations (N = 84).
 
 Every config is generated with numpy's default_rng so the container and the GPU box
 rebuild bit-identical inputs from the seed alone.
@@ -97,4 +99,19 @@ def c5_ablations(seeds=(10, 11, 12)):
             x, y, _ = dataset_3d(data)
             out.append(Workload(f"rep{r}_minus_{drop}", ExactLFM(jitter=1e-4, num_genes=4),
                                 Dataset(x, y)))
+    return out
+
+
+def notebook_pooled(seed=10):
+    """notebook.py:32-75 with replicate=None: the three replicates pooled by dataset_3d
+    (15 blocks of 7 timepoints, genes repeating per replicate), the 5 Barenco genes (N = 105)
+    and each leave-one-gene-out gene set (N = 84); ExactLFM(jitter=1e-4, num_genes=len(genes))."""
+    out = []
+    for drop in [None] + list(BARENCO_GENES):
+        genes = list(BARENCO_GENES) if drop is None else [g for g in BARENCO_GENES if g != drop]
+        data = SyntheticP53Data(replicate=None, selected_genes=None if drop is None else genes,
+                                seed=seed)
+        x, y, _ = dataset_3d(data)
+        out.append(Workload("pooled" if drop is None else f"pooled_minus_{drop}",
+                            ExactLFM(jitter=1e-4, num_genes=len(genes)), Dataset(x, y)))
     return out

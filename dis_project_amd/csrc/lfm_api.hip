@@ -1305,11 +1305,13 @@ int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_
   b->use_args = ctx->small_kernarg && nprob <= SMALL_ARG_PROBS &&
                 nhyp <= SMALL_ARG_HYP;
   b->table = table;
-  // the gradient / fit kernels: every problem's augmented matrix on one wave (n + 1 <= 64) and
-  // its LDS map within a CU's 160 KB
+  // the gradient / fit kernels: every problem's augmented matrix on one or two waves
+  // (n + 1 <= 128) and its LDS map within a CU's 160 KB
   if (maxn <= SMALL_GRAD_MAX) {
     b->lds_grad = small_grad_lds(table.data(), (int)nprob, 0);
     b->lds_fit = small_grad_lds(table.data(), (int)nprob, 1);
+    if (b->lds_grad > 160 * 1024) b->lds_grad = 0;
+    if (b->lds_fit > 160 * 1024) b->lds_fit = 0;
   }
   std::vector<int> offs(b->dsb_off);
   offs.insert(offs.end(), b->sc_off.begin(), b->sc_off.end());
@@ -1443,8 +1445,8 @@ int lfm_batch_mll_grad_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, in
     return set_err(ctx, LFM_E_ARG, "batch / hyp / value / grad is NULL");
   if (batch->device != ctx->device) return set_err(ctx, LFM_E_ARG, "batch of another device");
   if (!batch->lds_grad)
-    return set_err(ctx, LFM_E_ARG, "lfm_batch_mll_grad_f64: every problem needs n <= 63 (one "
-                                   "wave per augmented matrix); use lfm_mll_grad_f64");
+    return set_err(ctx, LFM_E_ARG, "lfm_batch_mll_grad_f64: every problem needs n <= 127 and its "
+                                   "map within 160 KB of LDS; use lfm_mll_grad_f64");
   DeviceGuard g(ctx->device);
   const int64_t np = batch->nprob;
   double* hres = batch->hbuf + batch->nhyp;
@@ -1490,7 +1492,8 @@ int lfm_batch_fit_f64(lfm_ctx* ctx, lfm_batch* batch, const lfm_adam* opt, int n
     return set_err(ctx, LFM_E_ARG, "bad fit arguments");
   if (batch->device != ctx->device) return set_err(ctx, LFM_E_ARG, "batch of another device");
   if (!batch->lds_fit)
-    return set_err(ctx, LFM_E_ARG, "lfm_batch_fit_f64: every problem needs n <= 63");
+    return set_err(ctx, LFM_E_ARG, "lfm_batch_fit_f64: every problem needs n <= 127 and its map "
+                                   "within 160 KB of LDS");
   if (nsteps == 0) return LFM_OK;
   DeviceGuard g(ctx->device);
   const int64_t np = batch->nprob, nh = batch->nhyp;

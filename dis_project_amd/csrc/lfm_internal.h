@@ -198,7 +198,7 @@ inline int64_t small_grid_doubles(int64_t n) { return n + (n + 1) / 2; }
 // within a CU's 160 KB (launch_small_batch)
 constexpr int SMALL_GRID_TAB_MAX = 2048;
 constexpr int SMALL_MAX = 128;  // largest n handled by small_mll_kernel
-constexpr int SMALL_GRAD_MAX = 63;  // largest n of the batched gradient / fit (one wave per problem)
+constexpr int SMALL_GRAD_MAX = 127;  // largest n of the batched gradient / fit (two waves)
 
 // gram kernels (lfm_gram.hip)
 int launch_tables(lfm_ctx* ctx, const HypDev& h, const GridLayout& lay, const double* d_times,

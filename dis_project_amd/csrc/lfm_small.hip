@@ -114,18 +114,101 @@ __device__ __forceinline__ void small_factor_regs(double* __restrict__ sm, int l
   *bad_out = f.bad;
 }
 
+// The same factor for 64 < n + 1 <= 128: rows on two waves (thread r, r < 128, holds row r),
+// the window up to 128 columns wide (small_next_w2: 128 96 64 48 32 24 16 12 8). Column c's
+// entries and the next pivot's input (lane c + 1's d[1] - L[c + 1][c]^2, in slot 255) go through
+// one of two alternating LDS buffers with ONE workgroup barrier per column (a wave can be at most
+// one column ahead, so the buffer it writes is never the one another wave still reads); the
+// reads come back in chunks of 16 (the window and all its column values would not fit the
+// registers). Every thread of the workgroup calls it (waves 2 and 3 only keep the barrier count).
+template <int W>
+constexpr int small_next_w2() {
+  return W == 128 ? 96 : W == 96 ? 64 : small_next_w<W>();
+}
+template <int W, bool STORE>
+__device__ __forceinline__ void small_factor2_phase(double (&d)[W], int c, SmallFactor& f) {
+  constexpr int WN = small_next_w2<W>();
+  const int cend = W > 8 ? max(c, f.n - WN) : f.n;
+#pragma unroll 1
+  for (; c < cend; ++c) {
+    if (!(f.dc > 0.0) && f.bad == 0) f.bad = c + 1;
+    const double lc = f.r == c ? f.dc * f.y : d[0] * f.y;  // L[r][c]; lane c: the pivot
+    if (f.r == c) f.mp = lc;
+    double* buf = f.colbuf + (c & 1) * 256;
+    if (f.r < 128) buf[f.r] = (f.act && f.r > c) ? lc : 0.0;
+    if (f.r == c + 1) buf[255] = fma(-lc, lc, d[1]);  // the next pivot's input
+    if constexpr (STORE) {
+      if (f.act && f.r > c) f.A[f.r * f.ld + c] = lc;
+      if (f.r == c) {
+        f.piv[c] = lc;
+        f.iy[c] = f.y;
+      }
+    }
+    __syncthreads();
+    if (f.r == c) f.mz = buf[f.n];  // L[n][c] = z[c], from the residual row's lane
+    const double dn = buf[255];
+#pragma unroll
+    for (int q0 = 1; q0 < W; q0 += 16) {
+      double col[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (q0 + u < W) col[u] = buf[c + q0 + u];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (q0 + u < W) d[q0 + u - 1] = fma(-lc, col[u], d[q0 + u]);
+    }
+    d[W - 1] = 0.0;
+    f.dc = dn;
+    f.y = rsqrt_1nr(dn);
+  }
+  if constexpr (W > 8)
+    if (c < f.n) small_factor2_phase<WN, STORE>(*reinterpret_cast<double(*)[WN]>(&d[0]), c, f);
+}
+template <bool STORE = false>
+__device__ __forceinline__ void small_factor_regs2(double* __restrict__ sm, int ld, int n, int M,
+                                                   double* colbuf, double* piv_r, double* z_r,
+                                                   int* bad_out, double* piv = nullptr,
+                                                   double* iy = nullptr) {
+  SmallFactor f;
+  f.n = n;
+  f.r = threadIdx.x;
+  f.act = f.r < M;
+  f.colbuf = colbuf;
+  f.A = sm;
+  f.ld = ld;
+  f.piv = piv;
+  f.iy = iy;
+  // the buffers' tails past the rows read as zeros (window entries past the last column)
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    if (i >= 128) colbuf[i] = colbuf[256 + i] = 0.0;
+  }
+  double d[128];
+#pragma unroll
+  for (int q = 0; q < 128; ++q) d[q] = (f.act && q <= f.r && q < n) ? sm[f.r * ld + q] : 0.0;
+  f.dc = sm[0];
+  f.y = rsqrt_1nr(f.dc);
+  f.mp = f.mz = 0.0;
+  f.bad = 0;
+  __syncthreads();  // windows loaded (STORE overwrites rows from here on), buffer tails zero
+  small_factor2_phase<128, STORE>(d, 0, f);
+  *piv_r = f.mp;
+  *z_r = f.mz;
+  *bad_out = f.bad;
+}
+
 // LDS map of one problem (doubles from the dynamic shared memory base), shared by the MLL,
 // gradient and fit kernels:
 //   A      [M x ld]         Sigma's lower triangle and the residual row n (M = n + 1, ld = n + 2)
 //   red    [16]             reductions
 //   hyp    [3G + 3]         D S B, l, obs_stddev, jitter (the constrained parameters)
 //   ktab   [3G + n + nG]    KxxTab's per-gene / per-row factors (tabs: n + 1 <= 64 in the launch)
-//   colbuf [128]            the one-wave factor's column buffer
+//   colbuf [128 / 512]      the factor's column buffer(s): one wave 128; two waves (n + 1 > 64)
+//                           two of 256 (rows, a zero tail, the next pivot in slot 255)
 //   xs, ys [3n], [n]
 //   gt     [2GW + 3GT + G^2] the grid layout's gram tables (grid problems, W = 2T - 1)
 // the gradient and the fit (GRAD) add, past this problem's gram tables:
 //   gg     [6GW + 8GT]      the grid layout's derivative tables (grad_table_entry)
-//   piv, iy, al, wd [64 each]  L_cc, 1 / L_cc, alpha = Sigma^{-1} r, diag(W)
+//   piv, iy, al, wd [128 each] L_cc, 1 / L_cc, alpha = Sigma^{-1} r, diag(W)
 //   accw   [4][2G + 1]      the waves' partial sums of 1/2 tr(W dSigma / d{D, S, l})
 //   gout   [3G + 3]         the gradient in the packed layout (dD dS dB, dl, d obs_stddev, 0)
 // and the fit (FIT): raw, mu, nu [3G + 3 each] (the unconstrained parameters, Adam's moments).
@@ -152,16 +235,16 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
   q.red = take(16);
   q.hyp = take(3 * (size_t)G + 3);
   q.ktab = take(tabs ? 3 * (size_t)G + n + (size_t)n * G : 0);
-  q.colbuf = take(128);
+  q.colbuf = take(n + 1 > 64 ? 512 : 128);  // two waves: two 256-slot column buffers
   q.xs = take(3 * (size_t)n);
   q.ys = take((size_t)n);
   q.gt = take(T > 0 ? 2 * (size_t)G * W + 3 * (size_t)G * T + (size_t)G * G : 0);
   if (grad) {
     q.gg = take(T > 0 ? 6 * (size_t)G * W + 8 * (size_t)G * T : 0);
-    q.piv = take(64);
-    q.iy = take(64);
-    q.al = take(64);
-    q.wd = take(64);
+    q.piv = take(128);
+    q.iy = take(128);
+    q.al = take(128);
+    q.wd = take(128);
     q.accw = take(4 * (2 * (size_t)G + 1));
     q.gout = take(3 * (size_t)G + 3);
   }
@@ -184,6 +267,33 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
 #ifndef LFM_SMALL_STAMPS
 #define LFM_SMALL_STAMPS 0
 #endif
+// The MLL from a two-wave factor (every thread: pr / zr its row's pivot and z entry, rows < n):
+// per-wave sums, then wave 0's + wave 1's in that order; returned to every thread.
+__device__ __forceinline__ double small_mll_2wave(double pr, double zr, int bad, int n,
+                                                  int negative, double* red) {
+  const int tid = threadIdx.x;
+  double ldp = 0.0, qp = 0.0;
+  if (tid < n) {
+    ldp = log(pr);
+    qp = zr * zr;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    ldp += __shfl_xor(ldp, o);
+    qp += __shfl_xor(qp, o);
+  }
+  __syncthreads();  // every thread is past the factor's last reads of the column buffers
+  if (tid == 0 || tid == 64) {
+    red[tid >> 6] = ldp;
+    red[2 + (tid >> 6)] = qp;
+  }
+  __syncthreads();
+  const double two_pi = 6.283185307179586476925;
+  double mll = -0.5 * ((double)n * log(two_pi) + 2.0 * (red[0] + red[1]) + (red[2] + red[3]));
+  mll *= negative ? -1.0 : 1.0;
+  if (bad) mll = __builtin_nan("");
+  return mll;
+}
+
 // Sigma = (K + jitter I) + obs_stddev^2 I (objectives.py:66-73) in the lower triangle of A and
 // the residual r = y - m (model.py:124-149) in row n; every thread of the workgroup calls it (the
 // hyperparameters, x and y already in LDS; it ends without a barrier).
@@ -343,52 +453,15 @@ __device__ __forceinline__ void small_body(const SmallProb P, int negative,
     }
     return;
   }
-  for (int c = 0; c < n; ++c) {
-    const double d = sm[c * ld + c];
-    const double piv = sqrt(d);
-    const double inv = 1.0 / piv;
-    for (int r = c + 1 + tid; r < M; r += 256) sm[r * ld + c] *= inv;
-    if (tid == 0) {
-      sm[c * ld + c] = piv;
-      if (!(d > 0.0) && red[8] == 0.0) red[8] = (double)(c + 1);
-    }
-    __syncthreads();
-    const int w = M - c - 1;
-    for (int idx = tid; idx < w * w; idx += 256) {
-      const int r = c + 1 + idx / w, q = c + 1 + idx % w;
-      if (q <= r) sm[r * ld + q] -= sm[r * ld + c] * sm[q * ld + c];
-    }
-    __syncthreads();
-  }
-  double ldp = 0.0, qp = 0.0;
-  for (int c = tid; c < n; c += 256) {
-    ldp += log(sm[c * ld + c]);
-    const double z = sm[n * ld + c];
-    qp += z * z;
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    ldp += __shfl_xor(ldp, o);
-    qp += __shfl_xor(qp, o);
-  }
-  if ((tid & 63) == 0) {
-    red[tid >> 6] = ldp;
-    red[4 + (tid >> 6)] = qp;
-  }
-  __syncthreads();
+  // two waves (64 < n + 1 <= 128): the same right-looking register window, one barrier a column
+  double pr, zr;
+  int bad;
+  small_factor_regs2<false>(sm, ld, n, M, colbuf, &pr, &zr, &bad);
+  const double mll = small_mll_2wave(pr, zr, bad, n, negative, red);
   if (tid == 0) {
-    const double LD = 2.0 * (red[0] + red[1] + red[2] + red[3]);
-    const double Q = red[4] + red[5] + red[6] + red[7];
-    const double two_pi = 6.283185307179586476925;
-    double mll = -0.5 * ((double)n * log(two_pi) + LD + Q);
-    mll *= negative ? -1.0 : 1.0;
-    int st = 0;
-    if (red[8] != 0.0) {
-      mll = __builtin_nan("");
-      st = (int)red[8];  // 1-based failing pivot
-    }
     out[blockIdx.x] = mll;
     __threadfence_system();  // the result before the status word (lfm_batch_mll_f64)
-    if (status) status[blockIdx.x] = st;
+    if (status) status[blockIdx.x] = bad;
   }
 }
 
@@ -443,19 +516,33 @@ struct SmallInv {
 };
 template <int W>
 __device__ __forceinline__ void small_inv_phase(double (&e)[W], int c, const SmallInv& f) {
-  constexpr int WN = small_next_w<W>();
+  constexpr int WN = small_next_w2<W>();
   const int cend = W > 8 ? max(c, f.n - WN) : f.n;
 #pragma unroll 1
   for (; c < cend; ++c) {
     const double xc = e[0] * f.iy[c];
     if (f.j <= c) f.A[f.j * f.ld + c] = xc;  // XT[j][c]: A's upper triangle (L is strictly lower)
-    double col[W - 1];
-#pragma unroll
-    for (int q = 1; q < W; ++q) col[q - 1] = f.A[min(c + q, f.n - 1) * f.ld + c];
-    asm volatile("" ::: "memory");  // every read issued before the first use
     // rows past n - 1 are not L's (row n holds z): their window entries stay zero
+    if constexpr (W <= 64) {
+      double col[W - 1];
 #pragma unroll
-    for (int q = 1; q < W; ++q) e[q - 1] = c + q < f.n ? fma(-col[q - 1], xc, e[q]) : 0.0;
+      for (int q = 1; q < W; ++q) col[q - 1] = f.A[min(c + q, f.n - 1) * f.ld + c];
+      asm volatile("" ::: "memory");  // every read issued before the first use
+#pragma unroll
+      for (int q = 1; q < W; ++q) e[q - 1] = c + q < f.n ? fma(-col[q - 1], xc, e[q]) : 0.0;
+    } else {
+      // two waves' windows: the column in chunks of 16 (registers)
+#pragma unroll
+      for (int q0 = 1; q0 < W; q0 += 16) {
+        double col[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (q0 + u < W) col[u] = f.A[min(c + q0 + u, f.n - 1) * f.ld + c];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (q0 + u < W) e[q0 + u - 1] = c + q0 + u < f.n ? fma(-col[u], xc, e[q0 + u]) : 0.0;
+      }
+    }
     e[W - 1] = 0.0;
   }
   if constexpr (W > 8)
@@ -491,7 +578,24 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
   small_sigma(P, m, h, 1);
   for (int t = tid; t < 4 * nacc; t += 256) m.accw[t] = 0.0;
   __syncthreads();
-  if (wv == 0) {
+  if (M > 64) {
+    // two waves hold the rows (small_factor_regs2, one barrier a column); the derivative
+    // tables first, by every thread (waves 2 and 3 only keep the factor's barrier count)
+    if (P.T > 0) {
+      const int ngg = (int)grad_tables_doubles(G, P.T);
+      for (int q = tid; q < ngg; q += 256) m.gg[q] = grad_table_entry(h, P.T, P.dt, P.times, q);
+    }
+    double pr, zr;
+    int bad;
+    small_factor_regs2<true>(A, ld, n, M, m.colbuf, &pr, &zr, &bad, m.piv, m.iy);
+    const double mll = small_mll_2wave(pr, zr, bad, n, negative, m.red + 4);
+    if (tid == 0) {
+      m.red[0] = mll;
+      m.red[1] = (double)bad;
+    }
+    // X = L^{-1}: every L store landed before the factor's last barrier
+    if (tid < 128) small_inverse<128>(A, ld, n, m.iy);
+  } else if (wv == 0) {
     double pr, zr;
     int bad;
     m.colbuf[64 + lane] = 0.0;
@@ -889,14 +993,13 @@ int launch_small_fit(lfm_ctx* ctx, const SmallFitLaunch& f, size_t lds) {
 }
 
 static size_t small_lds(int maxn, int maxg, int gridtab, int* tabs_out) {
-  // tables (KxxTab) when every problem has n + 1 <= 64 rows: 3 G + n + n G doubles
+  // tables (KxxTab) when every problem has n + 1 <= 64 rows; every other part of a problem's map
+  // grows with n and G, so the largest n and G bound every problem's map (the grid tables apart:
+  // + gridtab, the largest of them)
   const int tabs = maxn + 1 <= 64;
-  const size_t tab = tabs ? 3 * (size_t)maxg + maxn + (size_t)maxn * maxg : 0;
   *tabs_out = tabs;
-  // + 128: the one-wave factor's column buffer (small_factor_regs); + 4 n: x and y; + gridtab:
-  // the grid-layout tables
-  return ((size_t)(maxn + 1) * (maxn + 2) + 16 + 3 * (size_t)maxg + 3 + tab + 128 +
-          4 * (size_t)maxn + (size_t)gridtab) * sizeof(double);
+  return (small_map(nullptr, maxn, maxg, 0, tabs, 0, 0, nullptr) + (size_t)gridtab) *
+         sizeof(double);
 }
 
 int launch_small_args(lfm_ctx* ctx, SmallArgs& a, int nprob, int maxn, int maxg, int gridtab) {

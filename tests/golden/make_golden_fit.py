@@ -4,7 +4,7 @@ oracle's value and gradient (oracle/lfm_oracle.py mll_grad: complex-step derivat
 reference kernel, explicit Sigma^{-1}), through the host restatement of the loop
 (dis_project_amd/trainer.py: bijectors, chain rule, optax.adam, after_epoch).
 
-    python tests/golden/make_golden_fit.py      # rewrites tests/golden/fit_*.npz (~40 s)
+    python tests/golden/make_golden_fit.py      # rewrites tests/golden/fit_*.npz (~2.5 min)
 
 Cases (the reference's own training configurations):
   fit_c5        the 15 replicate x leave-one-gene-out problems of configs[4] (N = 28), the
@@ -13,6 +13,9 @@ Cases (the reference's own training configurations):
                 steps, fix_params=True, num_steps_per_epoch=1000 (main.py:45-59)
   fit_c1_epoch  the same with num_steps_per_epoch=50: after_epoch's index-3 quirk on the
                 unconstrained leaves at steps 0, 50 and 100 (trainer.py:205-210)
+  fit_pooled    the notebook's own data (replicate=None: three replicates pooled, N = 105) and
+                its 5 leave-one-gene-out ablations (N = 84), adam(0.01), 150 steps,
+                fix_params=False (notebook.py:32-75)
 Each holds, per problem, the packed raw parameters before and after, the loss history
 [P, iters] and the final constrained parameters.
 """
@@ -67,6 +70,8 @@ def main():
     c1 = configs.c1_p53()
     run("fit_c1", [c1.model], [c1.data], 150, True, 1000)
     run("fit_c1_epoch", [c1.model], [c1.data], 150, True, 50)
+    ws = configs.notebook_pooled()
+    run("fit_pooled", [w.model for w in ws], [w.data for w in ws], 150, False, 1000)
 
 
 if __name__ == "__main__":

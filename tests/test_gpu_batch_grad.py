@@ -104,7 +104,7 @@ def test_batch_grad_layouts_vs_oracle(kind):
 def test_batch_grad_memory_path_and_not_pd(monkeypatch):
     """More than 16 problems (the problem table and hyperparameters read from memory, not the
     kernel arguments): the same bits as the argument path; a non-PD problem is NaN with its
-    status, the others unaffected; n = 64 is refused (n <= 63)."""
+    status, the others unaffected; n = 128 is refused (n <= 127)."""
     from dis_project_amd import _lib
     from dis_project_amd.dataset import Dataset, grid_inputs
 
@@ -131,7 +131,7 @@ def test_batch_grad_memory_path_and_not_pd(monkeypatch):
         np.testing.assert_array_equal(v[mask], v32[mask])
     finally:
         big.close()
-    wide = farm.BatchEvaluator(ctx, [Dataset(grid_inputs(4, 16), np.zeros(64))], negative=True)
+    wide = farm.BatchEvaluator(ctx, [Dataset(grid_inputs(4, 32), np.zeros(128))], negative=True)
     try:
         from dis_project_amd.model import ExactLFM
 
@@ -142,12 +142,44 @@ def test_batch_grad_memory_path_and_not_pd(monkeypatch):
         wide.close()
 
 
-@pytest.mark.parametrize("case", ["fit_c5", "fit_c1", "fit_c1_epoch"])
+def test_batch_grad_two_wave_problems_vs_oracle():
+    """Problems past one wave (64 < n + 1 <= 128: the two-wave factor and inverse, one barrier a
+    column): the notebook's pooled replicates (N = 105, 84), a shuffled-row N = 96 problem and
+    N = 127, in one launch with a small C5 problem; values bit-identical to lfm_batch_mll_f64's
+    (the same two-wave factor), gradients within 1e-8 of the oracle's summed terms."""
+    from dis_project_amd import _lib, configs
+    from dis_project_amd.dataset import Dataset, grid_inputs
+    from dis_project_amd.model import ExactLFM
+
+    ws = configs.notebook_pooled()
+    models, datasets = [w.model for w in ws[:3]], [w.data for w in ws[:3]]
+    rng = np.random.default_rng(96)
+    for G, T, shuffle in ((4, 24, True), (1, 127, True)):
+        D, S, B = rng.uniform(0.2, 1.0, G), rng.uniform(0.5, 1.5, G), rng.uniform(0.01, 0.1, G)
+        x = grid_inputs(G, T)
+        if shuffle:
+            x = x[rng.permutation(G * T)]
+        y = np.repeat(B / D, T) + 0.5 * rng.standard_normal(G * T)
+        models.append(ExactLFM(jitter=1e-4, num_genes=G, true_d=D, true_s=S, true_b=B, l=2.1))
+        datasets.append(Dataset(np.ascontiguousarray(x), y))
+    c5m, c5d = farm.workload("c5")
+    models.append(c5m[0])
+    datasets.append(c5d[0])
+    ev = farm.BatchEvaluator(_lib.get_context(), datasets, negative=True)
+    try:
+        vals, grads = ev.value_and_grad(models)
+        np.testing.assert_array_equal(vals, ev(models))
+        _check_grads(vals, grads, models, datasets, True)
+    finally:
+        ev.close()
+
+
+@pytest.mark.parametrize("case", ["fit_c5", "fit_c1", "fit_c1_epoch", "fit_pooled"])
 def test_batch_fit_matches_oracle_jaxtrainer(case, golden):
     """JaxTrainer.fit on the device (one launch: 150 Adam steps per problem inside the kernel)
     against the oracle-driven host JaxTrainer loops (tests/golden/make_golden_fit.py): the C5
-    notebook fit (15 problems, fix_params=False), main.py's C1 fit (fix_params=True) and the
-    same with after_epoch every 50 steps. Loss histories within 1e-9 relative, final
+    ablation fit (15 problems, fix_params=False), main.py's C1 fit (fix_params=True), the same
+    with after_epoch every 50 steps, and the notebook's pooled data (N = 105 and 84: two waves). Loss histories within 1e-9 relative, final
     unconstrained and constrained parameters within 1e-9 (relative, absolute below 1)."""
     from dis_project_amd import _lib, configs
     from dis_project_amd import trainer as TR
@@ -156,6 +188,9 @@ def test_batch_fit_matches_oracle_jaxtrainer(case, golden):
     ref = golden(case)
     if case == "fit_c5":
         models, datasets = farm.workload("c5")
+    elif case == "fit_pooled":
+        ws = configs.notebook_pooled()
+        models, datasets = [w.model for w in ws], [w.data for w in ws]
     else:
         c1 = configs.c1_p53()
         models, datasets = [c1.model], [c1.data]
