@@ -453,15 +453,67 @@ __device__ __forceinline__ void small_body(const SmallProb P, int negative,
     }
     return;
   }
-  // two waves (64 < n + 1 <= 128): the same right-looking register window, one barrier a column
-  double pr, zr;
-  int bad;
-  small_factor_regs2<false>(sm, ld, n, M, colbuf, &pr, &zr, &bad);
-  const double mll = small_mll_2wave(pr, zr, bad, n, negative, red);
+  if (M <= 128) {
+    // two waves (64 < n + 1 <= 128): the same right-looking register window, one barrier a
+    // column
+    double pr, zr;
+    int bad;
+    small_factor_regs2<false>(sm, ld, n, M, colbuf, &pr, &zr, &bad);
+    const double mll = small_mll_2wave(pr, zr, bad, n, negative, red);
+    if (tid == 0) {
+      out[blockIdx.x] = mll;
+      __threadfence_system();  // the result before the status word (lfm_batch_mll_f64)
+      if (status) status[blockIdx.x] = bad;
+    }
+    return;
+  }
+  // n = SMALL_MAX = 128 (129 rows with the residual): column by column in LDS, every thread
+  for (int c = 0; c < n; ++c) {
+    const double d = sm[c * ld + c];
+    const double piv = sqrt(d);
+    const double inv = 1.0 / piv;
+    for (int r = c + 1 + tid; r < M; r += 256) sm[r * ld + c] *= inv;
+    if (tid == 0) {
+      sm[c * ld + c] = piv;
+      if (!(d > 0.0) && red[8] == 0.0) red[8] = (double)(c + 1);
+    }
+    __syncthreads();
+    const int w = M - c - 1;
+    for (int idx = tid; idx < w * w; idx += 256) {
+      const int r = c + 1 + idx / w, q = c + 1 + idx % w;
+      if (q <= r) sm[r * ld + q] -= sm[r * ld + c] * sm[q * ld + c];
+    }
+    __syncthreads();
+  }
+  double ldp = 0.0, qp = 0.0;
+  for (int c = tid; c < n; c += 256) {
+    ldp += log(sm[c * ld + c]);
+    const double z = sm[n * ld + c];
+    qp += z * z;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    ldp += __shfl_xor(ldp, o);
+    qp += __shfl_xor(qp, o);
+  }
+  if ((tid & 63) == 0) {
+    red[tid >> 6] = ldp;
+    red[4 + (tid >> 6)] = qp;
+  }
+  __syncthreads();
   if (tid == 0) {
+    const double LD = 2.0 * (red[0] + red[1] + red[2] + red[3]);
+    const double Q = red[4] + red[5] + red[6] + red[7];
+    const double two_pi = 6.283185307179586476925;
+    double mll = -0.5 * ((double)n * log(two_pi) + LD + Q);
+    mll *= negative ? -1.0 : 1.0;
+    int st = 0;
+    if (red[8] != 0.0) {
+      mll = __builtin_nan("");
+      st = (int)red[8];  // 1-based failing pivot
+    }
     out[blockIdx.x] = mll;
     __threadfence_system();  // the result before the status word (lfm_batch_mll_f64)
-    if (status) status[blockIdx.x] = bad;
+    if (status) status[blockIdx.x] = st;
   }
 }
 
