@@ -206,6 +206,7 @@ __device__ __forceinline__ void small_factor_regs2(double* __restrict__ sm, int 
 //                           two of 256 (rows, a zero tail, the next pivot in slot 255)
 //   xs, ys [3n], [n]
 //   gt     [2GW + 3GT + G^2] the grid layout's gram tables (grid problems, W = 2T - 1)
+//   tms, bgs [T], [n / T]    the grid layout's times and block genes (grid problems)
 // the gradient and the fit (GRAD) add, past this problem's gram tables:
 //   gg     [6GW + 8GT]      the grid layout's derivative tables (grad_table_entry)
 //   piv, iy, al, wd [128 each] L_cc, 1 / L_cc, alpha = Sigma^{-1} r, diag(W)
@@ -214,7 +215,8 @@ __device__ __forceinline__ void small_factor_regs2(double* __restrict__ sm, int 
 // and the fit (FIT): raw, mu, nu [3G + 3 each] (the unconstrained parameters, Adam's moments).
 struct SmallMap {
   double *A, *red, *hyp, *ktab, *colbuf, *xs, *ys, *gt;
-  double *gg, *piv, *iy, *al, *wd, *accw, *gout, *raw, *mu, *nu;
+  double *gg, *piv, *iy, *al, *wd, *accw, *gout, *raw, *mu, *nu, *tms;
+  int* bgs;
   int n, ld, G;
 };
 // doubles of the map (sm = nullptr: the size only)
@@ -239,6 +241,9 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
   q.xs = take(3 * (size_t)n);
   q.ys = take((size_t)n);
   q.gt = take(T > 0 ? 2 * (size_t)G * W + 3 * (size_t)G * T + (size_t)G * G : 0);
+  // the grid layout's times and block genes, staged with x and y (read every element / step)
+  q.tms = take(T > 0 ? (size_t)T : 0);
+  q.bgs = reinterpret_cast<int*>(take(T > 0 ? ((size_t)n / T + 1) / 2 + 1 : 0));
   if (grad) {
     q.gg = take(T > 0 ? 6 * (size_t)G * W + 8 * (size_t)G * T : 0);
     q.piv = take(128);
@@ -294,6 +299,18 @@ __device__ __forceinline__ double small_mll_2wave(double pr, double zr, int bad,
   return mll;
 }
 
+// x, y and (grid problems) the times and block genes into the problem's LDS map; every thread
+// calls it, a barrier follows before use
+__device__ __forceinline__ void small_stage(const SmallProb& P, const SmallMap& m) {
+  const int tid = threadIdx.x, n = m.n;
+  for (int i = tid; i < 3 * n; i += 256) m.xs[i] = P.x[i];
+  for (int i = tid; i < n; i += 256) m.ys[i] = P.y[i];
+  if (P.T > 0) {
+    for (int i = tid; i < P.T; i += 256) m.tms[i] = P.times[i];
+    for (int i = tid; i < n / P.T; i += 256) m.bgs[i] = P.bg[i];
+  }
+}
+
 // Sigma = (K + jitter I) + obs_stddev^2 I (objectives.py:66-73) in the lower triangle of A and
 // the residual r = y - m (model.py:124-149) in row n; every thread of the workgroup calls it (the
 // hyperparameters, x and y already in LDS; it ends without a barrier).
@@ -312,7 +329,7 @@ __device__ __forceinline__ void small_sigma(const SmallProb& P, const SmallMap& 
     double* gt = m.gt;
     const int T = P.T, W = 2 * T - 1;
     const int nt = (int)(2 * (int64_t)G * W + 3 * (int64_t)G * T + (int64_t)G * G);
-    for (int q = tid; q < nt; q += 256) gt[q] = grid_table_entry(h, T, P.dt, P.times, q);
+    for (int q = tid; q < nt; q += 256) gt[q] = grid_table_entry(h, T, P.dt, m.tms, q);
     __syncthreads();
     const double* Wt = gt;
     const double* Xt = Wt + G * W;
@@ -326,8 +343,8 @@ __device__ __forceinline__ void small_sigma(const SmallProb& P, const SmallMap& 
       while (i * (i + 1) / 2 > q) --i;
       while ((i + 1) * (i + 2) / 2 <= q) ++i;
       const int c = q - i * (i + 1) / 2;
-      const int bi = i / T, tau = i - bi * T, j = P.bg[bi];
-      const int bc = c / T, tp = c - bc * T, k = P.bg[bc];
+      const int bi = i / T, tau = i - bi * T, j = m.bgs[bi];
+      const int bc = c / T, tp = c - bc * T, k = m.bgs[bc];
       const int d = tp - tau;
       double v = Wt[k * W + (T - 1) + d] + Wt[j * W + (T - 1) - d];
       v = fma(-Xt[k * W + (T - 1) + d], Pt[k * T + tau], v);
@@ -394,12 +411,9 @@ __device__ __forceinline__ void small_body(const SmallProb P, int negative,
   // y, so that no later phase waits on HBM
   double* hyp = m.hyp;
   double* colbuf = m.colbuf;
-  double* xs = m.xs;
-  double* ys = m.ys;
   for (int i = tid; i < 3 * G; i += 256) hyp[i] = LFM_SMALL_SKIP == 4 ? 0.5 : P.dsb[i];
   if (tid < 3) hyp[3 * G + tid] = LFM_SMALL_SKIP == 4 ? (tid == 0 ? 2.5 : 1.0) : P.sc[tid];
-  for (int i = tid; i < 3 * n; i += 256) xs[i] = P.x[i];
-  for (int i = tid; i < n; i += 256) ys[i] = P.y[i];
+  small_stage(P, m);
   __syncthreads();
   const unsigned long long st1 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
   const HypDev h{hyp, hyp + G, hyp + 2 * G, G, hyp[3 * G]};
@@ -547,8 +561,8 @@ __global__ __launch_bounds__(256) void small_mll_kernel_args(SmallArgs a) {
 //      X = L^{-1} by the same right-looking register window (lane j = column j of X, which it
 //      writes transposed into A's free upper triangle: XT[j][c] = X[c][j]); waves 1-3 meanwhile
 //      build the grid layout's derivative tables (grad_table_entry);
-//   3. alpha = X^T z and W's lower triangle (S^{-1} = X^T X as row dot products of XT), into A's
-//      strictly lower part (L is dead) and wd;
+//   3. W's lower triangle (S^{-1} = X^T X as row dot products of XT; alpha = X^T z accumulated
+//      by the inverse's sweep), into A's strictly lower part (L is dead) and wd;
 //   4. 1/2 tr(W dS/d{D, S, l}): grid problems one wave per gene-block pair (its rows share gene
 //      j, its columns gene k: the derivative tables as grad_grid_kernel reads them, the gene-pair
 //      constant applied to the wave's sums); other layouts one lane per pair with the dual-number
@@ -565,15 +579,17 @@ struct SmallInv {
   double* A;
   int ld, n, j;
   const double* iy;
+  double a;  // alpha_j = sum_{c >= j} X[c][j] z_c, accumulated as the sweep forms X[c][j]
 };
 template <int W>
-__device__ __forceinline__ void small_inv_phase(double (&e)[W], int c, const SmallInv& f) {
+__device__ __forceinline__ void small_inv_phase(double (&e)[W], int c, SmallInv& f) {
   constexpr int WN = small_next_w2<W>();
   const int cend = W > 8 ? max(c, f.n - WN) : f.n;
 #pragma unroll 1
   for (; c < cend; ++c) {
     const double xc = e[0] * f.iy[c];
     if (f.j <= c) f.A[f.j * f.ld + c] = xc;  // XT[j][c]: A's upper triangle (L is strictly lower)
+    if (f.j <= c) f.a = fma(xc, f.A[f.n * f.ld + c], f.a);  // z_c: row n (the residual)
     // rows past n - 1 are not L's (row n holds z): their window entries stay zero
     if constexpr (W <= 64) {
       double col[W - 1];
@@ -601,12 +617,14 @@ __device__ __forceinline__ void small_inv_phase(double (&e)[W], int c, const Sma
     if (c < f.n) small_inv_phase<WN>(*reinterpret_cast<double(*)[WN]>(&e[0]), c, f);
 }
 template <int MR>
-__device__ __forceinline__ void small_inverse(double* A, int ld, int n, const double* iy) {
-  SmallInv f{A, ld, n, (int)threadIdx.x, iy};
+__device__ __forceinline__ void small_inverse(double* A, int ld, int n, const double* iy,
+                                              double* al) {
+  SmallInv f{A, ld, n, (int)threadIdx.x, iy, 0.0};
   double e[MR];
 #pragma unroll
   for (int q = 0; q < MR; ++q) e[q] = q == f.j ? 1.0 : 0.0;
   small_inv_phase<MR>(e, 0, f);
+  if (f.j < n) al[f.j] = f.a;  // alpha = X^T z
 }
 
 // (i, c), c <= i, of lower-triangle element q (row by row)
@@ -635,7 +653,7 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
     // tables first, by every thread (waves 2 and 3 only keep the factor's barrier count)
     if (P.T > 0) {
       const int ngg = (int)grad_tables_doubles(G, P.T);
-      for (int q = tid; q < ngg; q += 256) m.gg[q] = grad_table_entry(h, P.T, P.dt, P.times, q);
+      for (int q = tid; q < ngg; q += 256) m.gg[q] = grad_table_entry(h, P.T, P.dt, m.tms, q);
     }
     double pr, zr;
     int bad;
@@ -646,7 +664,7 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
       m.red[1] = (double)bad;
     }
     // X = L^{-1}: every L store landed before the factor's last barrier
-    if (tid < 128) small_inverse<128>(A, ld, n, m.iy);
+    if (tid < 128) small_inverse<128>(A, ld, n, m.iy, m.al);
   } else if (wv == 0) {
     double pr, zr;
     int bad;
@@ -674,18 +692,11 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
       m.red[1] = (double)bad;
     }
     asm volatile("" ::: "memory");  // the wave's L stores precede its reads below (in order)
-    if (M <= 32) small_inverse<32>(A, ld, n, m.iy);
-    else small_inverse<64>(A, ld, n, m.iy);
+    if (M <= 32) small_inverse<32>(A, ld, n, m.iy, m.al);
+    else small_inverse<64>(A, ld, n, m.iy, m.al);
   } else if (P.T > 0) {
     const int ngg = (int)grad_tables_doubles(G, P.T);
-    for (int q = tid - 64; q < ngg; q += 192) m.gg[q] = grad_table_entry(h, P.T, P.dt, P.times, q);
-  }
-  __syncthreads();
-  // alpha = X^T z: alpha_i = sum_{k >= i} XT[i][k] z_k (z in row n)
-  for (int i = tid; i < n; i += 256) {
-    double a = 0.0;
-    for (int k = i; k < n; ++k) a = fma(A[i * ld + k], A[n * ld + k], a);
-    m.al[i] = a;
+    for (int q = tid - 64; q < ngg; q += 192) m.gg[q] = grad_table_entry(h, P.T, P.dt, m.tms, q);
   }
   __syncthreads();
   // W = alpha alpha^T - S^{-1}, S^{-1}_ic = sum_{k >= i} XT[i][k] XT[c][k] (c <= i)
@@ -710,7 +721,7 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
     for (int bp = wv; bp < nbp; bp += 4) {
       int bi, bc;
       tri_index(bp, &bi, &bc);
-      const int j = P.bg[bi], k = P.bg[bc];
+      const int j = m.bgs[bi], k = m.bgs[bc];
       double sV = 0.0, sVj = 0.0, sVk = 0.0, sVl = 0.0;
       for (int e = lane; e < T * T; e += 64) {
         const int tau = e / T, tp = e - tau * T;
@@ -819,16 +830,13 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
 // rebuilt from the dynamic LDS base), so the register windows of the factor and the inverse are
 // allocated without the loop's state beside them (inlined into the loop they spilled)
 __device__ __noinline__ double small_value_grad_step(int n, int G, int T, double dt,
-                                                     const double* times, const int* bg,
                                                      int negative, int* bad_out) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  SmallProb P{};
+  SmallProb P{};  // what small_value_grad reads of it: the sizes (x, y, times, genes are in LDS)
   P.n = n;
   P.G = G;
   P.T = T;
   P.dt = dt;
-  P.times = times;
-  P.bg = bg;
   SmallMap m;
   small_map(sm, n, G, T, 1, 1, 1, &m);
   return small_value_grad(P, m, negative, bad_out);
@@ -847,8 +855,7 @@ __device__ __forceinline__ void small_grad_one(const SmallProb& P, int negative,
   small_map(sm, n, G, P.T, 1, 1, 0, &m);
   for (int i = tid; i < 3 * G; i += 256) m.hyp[i] = P.dsb[i];
   if (tid < 3) m.hyp[3 * G + tid] = P.sc[tid];
-  for (int i = tid; i < 3 * n; i += 256) m.xs[i] = P.x[i];
-  for (int i = tid; i < n; i += 256) m.ys[i] = P.y[i];
+  small_stage(P, m);
   __syncthreads();
   int bad;
   const double v = small_value_grad(P, m, negative, &bad);
@@ -929,8 +936,7 @@ __global__ __launch_bounds__(256) void small_fit_kernel(FitArgs a) {
     m.mu[i] = a.mu[gi];
     m.nu[i] = a.nu[gi];
   }
-  for (int i = tid; i < 3 * n; i += 256) m.xs[i] = P.x[i];
-  for (int i = tid; i < n; i += 256) m.ys[i] = P.y[i];
+  small_stage(P, m);
   __syncthreads();
   int first_bad = 0;
   for (int64_t s = 0; s < a.nsteps; ++s) {
@@ -941,7 +947,7 @@ __global__ __launch_bounds__(256) void small_fit_kernel(FitArgs a) {
     }
     __syncthreads();
     int bad;
-    const double v = small_value_grad_step(n, G, P.T, P.dt, P.times, P.bg, a.negative, &bad);
+    const double v = small_value_grad_step(n, G, P.T, P.dt, a.negative, &bad);
     if (bad && !first_bad) first_bad = (int)s + 1;
     if (tid == 0) a.history[s * a.nprob + b] = v;
     if (tid < nh - 1) {
