@@ -503,7 +503,7 @@ int small_batch(lfm_ctx* ctx, int64_t np, const lfm_problem* probs, const int64_
     sp.n = (int)n;
     sp.G = (int)G;
     off += small_grid_pack(p.x, n, G, sp, hd + off, dd + off);
-    if (sp.T) gridtab = std::max<int>(gridtab, (int)tables_doubles((int)G, sp.T));
+    if (sp.T) gridtab = std::max<int>(gridtab, (int)small_grid_extra((int)n, (int)G, sp.T));
     hp[q] = sp;
   }
   const size_t up = round_up(bytes_d, 16) + bytes_p;
@@ -1298,7 +1298,7 @@ int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_
     sp.n = (int)n;
     sp.G = (int)G;
     off += small_grid_pack(p.x, n, G, sp, &hd[off], dd + off);
-    if (sp.T) b->gridtab = std::max<int>(b->gridtab, (int)tables_doubles((int)G, sp.T));
+    if (sp.T) b->gridtab = std::max<int>(b->gridtab, (int)small_grid_extra((int)n, (int)G, sp.T));
     b->dsb_off.push_back((int)(hv - 3 * G));
     b->sc_off.push_back((int)(nvec + hs - 3));
   }

@@ -284,7 +284,9 @@ struct SmallFitLaunch {
 };
 int launch_small_fit(lfm_ctx* ctx, const SmallFitLaunch& f, size_t lds);
 int launch_small_args(lfm_ctx* ctx, SmallArgs& a, int nprob, int maxn, int maxg, int gridtab);
-// gridtab: the largest grid table of the problems (doubles; 0: none on the grid path)
+// gridtab: the largest small_grid_extra of the problems (doubles; 0: none on the grid path)
+// LDS doubles a grid-layout problem adds to its map: the gram tables, the times, the block genes
+size_t small_grid_extra(int n, int G, int T);
 int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int maxn, int maxg,
                        int gridtab, int negative, double* d_out, int* d_status);
 

@@ -1050,10 +1050,14 @@ int launch_small_fit(lfm_ctx* ctx, const SmallFitLaunch& f, size_t lds) {
   return hip_fail(ctx, hipGetLastError(), "small_fit_kernel");
 }
 
+size_t small_grid_extra(int n, int G, int T) {
+  return small_map(nullptr, n, G, T, 0, 0, 0, nullptr) - small_map(nullptr, n, G, 0, 0, 0, 0, nullptr);
+}
+
 static size_t small_lds(int maxn, int maxg, int gridtab, int* tabs_out) {
   // tables (KxxTab) when every problem has n + 1 <= 64 rows; every other part of a problem's map
-  // grows with n and G, so the largest n and G bound every problem's map (the grid tables apart:
-  // + gridtab, the largest of them)
+  // grows with n and G, so the largest n and G bound every problem's map (the grid part apart:
+  // + gridtab, the largest small_grid_extra)
   const int tabs = maxn + 1 <= 64;
   *tabs_out = tabs;
   return (small_map(nullptr, maxn, maxg, 0, tabs, 0, 0, nullptr) + (size_t)gridtab) *

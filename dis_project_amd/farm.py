@@ -235,7 +235,7 @@ class BatchEvaluator:
 
     def value_and_grad(self, models):
         """Every problem's value and gradient (constrained parameters, as
-        ``CustomConjMLL.value_and_grad``) in ONE launch (``lfm_batch_mll_grad_f64``; n <= 63 per
+        ``CustomConjMLL.value_and_grad``) in ONE launch (``lfm_batch_mll_grad_f64``; n <= 127 per
         problem). Returns (values [P], [grads dict per problem]); NaN where not PD."""
         models = self._pack(models)
         grad = np.empty(self._buf.size)

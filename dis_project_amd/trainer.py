@@ -224,7 +224,7 @@ class BatchTrainer:
     """``JaxTrainer`` (trainer.py:36-228) over P independent (model, dataset) problems at once:
     ``fit`` runs every problem's ``num_iters`` training steps on the GPU in ONE launch
     (``lfm_batch_fit_f64``: one workgroup per problem, its Adam loop inside the kernel, no host
-    round trip between steps; n <= 63 per problem). Per problem the semantics are JaxTrainer's:
+    round trip between steps; n <= 127 per problem). Per problem the semantics are JaxTrainer's:
     training in the bijectors' unconstrained space (trainer.py:75), the objective's value and
     gradient at the constrained model (trainer.py:103, 126), ``optim`` (an ``adam``) on the
     unconstrained leaves (trainer.py:127-128), ``after_epoch`` on the unconstrained model every

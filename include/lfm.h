@@ -184,8 +184,9 @@ int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int neg
 /* Value and gradient of every problem's CustomConjMLL(negative).step in ONE launch, one
  * workgroup per problem — jax.value_and_grad(loss) at src/trainer.py:126 (before the
  * bijectors' chain rule, trainer.py:103), batched over the ablation problems of
- * src/notebook.py:33-75 / the p53 fit of src/main.py:59. Every problem needs n <= 63, else
- * LFM_E_ARG (lfm_mll_grad_f64 takes any n). hyp as lfm_batch_mll_f64; value[p] as its out[p] (the
+ * src/notebook.py:33-75 / the p53 fit of src/main.py:59. Every problem needs n <= 127 and its
+ * workgroup's LDS map (Sigma, x, y, and on the dataset_3d grid the gram and derivative tables)
+ * within 160 KB, else LFM_E_ARG (lfm_mll_grad_f64 takes any n). hyp as lfm_batch_mll_f64; value[p] as its out[p] (the
  * same bits); grad packed in hyp's layout: for each problem dD[G_p] dS[G_p] dB[G_p] in order,
  * then for each problem d l, d obs_stddev, 0 (jitter is static, model.py:64). Not PD: value and
  * that problem's gradient NaN, status[p] = LFM_E_NOT_PD, returns LFM_E_NOT_PD. Deterministic (no
@@ -215,7 +216,7 @@ typedef struct {
  *   status [nprob] optional: 0, or 1 + the first step whose Cholesky failed (its loss and the
  *          parameters are NaN from there on, as under JAX); returns LFM_E_NOT_PD if any did.
  * The final constrain and after_epoch on the constrained model (trainer.py:218-222) are the
- * caller's (dis_project_amd.trainer.BatchTrainer). n <= 63 per problem, else LFM_E_ARG. */
+ * caller's (dis_project_amd.trainer.BatchTrainer). Problem sizes as lfm_batch_mll_grad_f64. */
 int lfm_batch_fit_f64(lfm_ctx* ctx, lfm_batch* batch, const lfm_adam* opt, int negative,
                       int64_t step0, int64_t nsteps, double* raw, double* mu, double* nu,
                       double* history, int* status);
