@@ -10,6 +10,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <climits>
 #include <cstdio>
@@ -665,6 +666,8 @@ void release_partition(lfm_ctx* ctx) {
 //   LFM_DEBUG_FARM_STALL_MS  test stand-in for a late peer ahead of each all-gather
 //   LFM_SMALL_KERNARG    0: resident batches read their problem table / hyperparameters from
 //                        memory instead of the kernel arguments
+//   LFM_FARM_GRAPH       0: a device-side farm round is enqueued call by call instead of
+//                        replayed as one captured graph
 // Every knob is read here, once: a call never consults the environment.
 hipError_t create_streams(lfm_ctx* ctx) {
   ctx->sched = env_int_api("LFM_SCHED", 3) == 1 ? 1 : 3;
@@ -684,6 +687,7 @@ hipError_t create_streams(lfm_ctx* ctx) {
   }
   ctx->farm_stall_ms = std::max(0, env_int_api("LFM_DEBUG_FARM_STALL_MS", 0));
   ctx->small_kernarg = env_int_api("LFM_SMALL_KERNARG", 1) != 0;
+  ctx->farm_graph_on = env_int_api("LFM_FARM_GRAPH", 1) != 0;
   if (const char* ms = std::getenv("LFM_DEVICE_WAIT_MS")) {
     // 100 MHz ticks; at most ~42 s (the bound is a 32-bit tick count)
     const double t = std::min(std::max(std::atof(ms), 0.0), 42000.0);
@@ -1207,6 +1211,7 @@ int lfm_mll_batch_f64(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, int
 // words live in one pinned host buffer the kernel reads and writes directly, so an evaluation is
 // one memcpy into that buffer, ONE kernel launch and one stream synchronise — no copy commands.
 struct lfm_batch {
+  uint64_t id = 0;  // unique per process (never reused): keys the farm's captured graph
   int device = 0;
   int64_t nprob = 0, nhyp = 0;
   int maxn = 1, maxg = 1, gridtab = 0;
@@ -1254,6 +1259,8 @@ int lfm_batch_create(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, lfm_
   }
   DeviceGuard g(ctx->device);
   std::unique_ptr<lfm_batch> b(new lfm_batch);
+  static std::atomic<uint64_t> next_id{0};
+  b->id = ++next_id;
   b->device = ctx->device;
   b->nprob = nprob;
   b->nhyp = nhyp;
@@ -1696,14 +1703,16 @@ __global__ void stall_kernel(unsigned long long ticks) {
   while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
 }
 
-// The end of a device-side farm round: the gathered slots to pinned host memory (system-scope
-// stores), a system-scope fence, then the round's sequence number — the host's completion signal
-// (it spins on that word instead of synchronising the stream: microseconds sooner).
-__global__ __launch_bounds__(256) void farm_publish_kernel(const double* __restrict__ src,
-                                                          int64_t count, double* __restrict__ dst,
-                                                          unsigned* seq_word, unsigned seq) {
-  for (int64_t i = threadIdx.x; i < count; i += blockDim.x) dst[i] = src[i];
-  __threadfence_system();
+// The end of a device-side farm round: the gathered slots to pinned host memory, then the round's
+// sequence number — the host's completion signal (it spins on that word instead of synchronising
+// the stream: microseconds sooner). ONE wave (launched with 64 threads): the sequence word's
+// system-scope release store waits for every store the wave issued before it (s_waitcnt
+// vmcnt(0) is per wave) after the L2 write-back, so the slots land first; a per-thread
+// __threadfence_system before it would only repeat that write-back.
+__global__ __launch_bounds__(64) void farm_publish_kernel(const double* __restrict__ src,
+                                                         int64_t count, double* __restrict__ dst,
+                                                         unsigned* seq_word, unsigned seq) {
+  for (int64_t i = threadIdx.x; i < count; i += 64) dst[i] = src[i];
   __syncthreads();
   if (threadIdx.x == 0)
     __hip_atomic_store(seq_word, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1779,7 +1788,22 @@ struct Backoff {
 // its publish kernel) may still run: farm_stale makes the next call drain it first (bounded), and
 // abandon the staging buffers if it does not drain (a bounded leak instead of a late write into
 // memory the next call is using).
+// Forget the captured farm round (its buffers, batch or communicator are changing; nothing of it
+// is in flight).
+void farm_graph_reset(lfm_ctx* ctx) {
+  if (ctx->farm_exec) hipGraphExecDestroy(ctx->farm_exec);
+  ctx->farm_exec = nullptr;
+  ctx->farm_exec_batch = 0;
+}
+
 void rccl_drop(lfm_ctx* ctx) {
+  // a replay of the captured round may still be queued: the graph is set aside and destroyed
+  // only once the stream has drained (farm_drain_stale; a second abort before that leaks one)
+  if (ctx->farm_exec) {
+    ctx->farm_exec_old = ctx->farm_exec;
+    ctx->farm_exec = nullptr;
+    ctx->farm_exec_batch = 0;
+  }
   if (!ctx->comm) return;
   if (g_rccl.commAbort) g_rccl.commAbort((ncclComm_t)ctx->comm);
   else if (g_rccl.commDestroy) g_rccl.commDestroy((ncclComm_t)ctx->comm);
@@ -1872,6 +1896,7 @@ int lfm_farm_init(lfm_ctx* ctx, const unsigned char id[128], int nranks, int ran
   ctx->comm_nb = nb;
   ctx->nranks = nranks;
   ctx->rank = rank;
+  ++ctx->comm_gen;
   return LFM_OK;
 }
 
@@ -1888,6 +1913,7 @@ int farm_drain_stale(lfm_ctx* ctx) {
   hipError_t e;
   while ((e = hipStreamQuery(ctx->stream)) == hipErrorNotReady && mono_s() < end) bo.pause();
   if (e == hipErrorNotReady) {
+    farm_graph_reset(ctx);
     ctx->farm_h = nullptr;  // abandoned: a queued copy may still land in it
     ctx->farm_h_bytes = 0;
     ctx->farm_pub = nullptr;
@@ -1896,6 +1922,9 @@ int farm_drain_stale(lfm_ctx* ctx) {
     ctx->farm_bytes = 0;
   } else if (e != hipSuccess) {
     return hip_fail(ctx, e, "draining the aborted farm call");
+  } else if (ctx->farm_exec_old) {
+    hipGraphExecDestroy(ctx->farm_exec_old);
+    ctx->farm_exec_old = nullptr;
   }
   ctx->farm_stale = false;
   return LFM_OK;
@@ -1905,10 +1934,13 @@ int farm_drain_stale(lfm_ctx* ctx) {
 // publish target (recv's copy + a sequence word) in coherent pinned host memory.
 int farm_buffers(lfm_ctx* ctx, size_t slots) {
   const size_t in = slots * 8, out = in * ctx->nranks;
+  const double* before = ctx->farm_buf;
   int r = ensure(ctx, (void**)&ctx->farm_buf, &ctx->farm_bytes, in + out);
   if (r) return r;
+  if (ctx->farm_buf != before) farm_graph_reset(ctx);
   const size_t pub = out + 64;
   if (!ctx->farm_pub || ctx->farm_pub_bytes < pub) {
+    farm_graph_reset(ctx);
     if (ctx->farm_pub) {
       hipStreamSynchronize(ctx->stream);
       hipHostFree(ctx->farm_pub);
@@ -1920,6 +1952,8 @@ int farm_buffers(lfm_ctx* ctx, size_t slots) {
   }
   return LFM_OK;
 }
+
+int farm_wait(lfm_ctx* ctx, const unsigned* seq_word, unsigned seq, int64_t count, double* recv);
 
 // Enqueue the all-gather of `slots` doubles per rank (send -> recv, device) and the publish of
 // recv to the pinned host buffer, then wait (bounded) for the round's sequence word; on any error
@@ -1949,6 +1983,13 @@ int farm_gather_publish(lfm_ctx* ctx, int64_t slots, double* recv) {
     rccl_drop(ctx);
     return hip_fail(ctx, e, "farm publish");
   }
+  return farm_wait(ctx, seq_word, seq, count, recv);
+}
+
+// The host's side of a device-side round: wait (bounded) for the publish kernel's sequence word,
+// then copy the gathered slots out; on a fault or timeout the communicator is aborted.
+int farm_wait(lfm_ctx* ctx, const unsigned* seq_word, unsigned seq, int64_t count, double* recv) {
+  hipError_t e;
   // one bounded wait for the whole chain (kernel, collective, publish): the sequence word — a
   // tight spin for the first 2 ms (a round takes tens of microseconds), then the stream is
   // polled between backed-off checks, so a fault surfaces instead of running out the bound
@@ -1981,6 +2022,74 @@ int farm_gather_publish(lfm_ctx* ctx, int64_t slots, double* recv) {
   std::memcpy(recv, ctx->farm_pub, (size_t)count * 8);
   return LFM_OK;
 }
+
+// The round's publish value when it is replayed from the captured graph (a graph's kernel
+// arguments are fixed): the host clears the word before each replay. The enqueued path counts
+// from 1 and never reaches it.
+constexpr unsigned FARM_GRAPH_SEQ = 0xFFFFFFFFu;
+
+// Capture one device-side round — the padding memset (slots > nprob), the batch's MLL kernel
+// reading its hyperparameters from the batch's pinned buffer, ncclAllGather, the publish kernel —
+// as a graph, so a round costs one graph launch instead of three enqueues and RCCL's host-side
+// enqueue of the collective (which left the GPU idle between the kernel and the collective).
+// Returns LFM_OK with ctx->farm_exec set, or non-zero when capture is not possible (the caller
+// then enqueues; the graph stays off for this context).
+int farm_graph_build(lfm_ctx* ctx, lfm_batch* batch, int negative, int64_t slots) {
+  farm_graph_reset(ctx);
+  small_batch_attrs();
+  const int64_t np = batch->nprob;
+  double* dsend = ctx->farm_buf;
+  double* drecv = ctx->farm_buf + slots;
+  const int64_t count = slots * ctx->nranks;
+  unsigned* seq_word = reinterpret_cast<unsigned*>(ctx->farm_pub + count);
+  int* hst = reinterpret_cast<int*>(batch->hbuf + batch->nhyp + np);
+  hipError_t e = hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeRelaxed);
+  if (e != hipSuccess) return hip_fail(ctx, e, "farm graph: begin capture");
+  int r = LFM_OK;
+  if (slots > np)
+    e = hipMemsetAsync(dsend + np, 0xFF, (size_t)(slots - np) * 8, ctx->stream);
+  if (e == hipSuccess)
+    r = launch_small_batch(ctx, batch->dprobs, (int)np, batch->maxn, batch->maxg, batch->gridtab,
+                           negative, dsend, hst);
+  else
+    r = hip_fail(ctx, e, "farm graph: padding");
+  // test instrument: a collective whose peers are late (LFM_DEBUG_FARM_STALL_MS), captured too
+  if (!r && ctx->farm_stall_ms)
+    hipLaunchKernelGGL(stall_kernel, dim3(1), dim3(64), 0, ctx->stream,
+                       (unsigned long long)ctx->farm_stall_ms * 100000ull);
+  if (!r) {
+    const ncclResult_t q = g_rccl.allGather(dsend, drecv, (size_t)slots, ncclFloat64,
+                                           (ncclComm_t)ctx->comm, ctx->stream);
+    r = ctx->comm_nb && q == ncclInProgress ? rccl_poll(ctx, (ncclComm_t)ctx->comm, "ncclAllGather")
+                                            : rccl_fail(ctx, q, "ncclAllGather");
+  }
+  if (!r) {
+    hipLaunchKernelGGL(farm_publish_kernel, dim3(1), dim3(64), 0, ctx->stream, drecv, count,
+                       ctx->farm_pub, seq_word, FARM_GRAPH_SEQ);
+    r = hip_fail(ctx, hipGetLastError(), "farm graph: publish");
+  }
+  hipGraph_t graph = nullptr;
+  e = hipStreamEndCapture(ctx->stream, &graph);
+  if (!r && e != hipSuccess) r = hip_fail(ctx, e, "farm graph: end capture");
+  if (!r) {
+    e = hipGraphInstantiate(&ctx->farm_exec, graph, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+      ctx->farm_exec = nullptr;
+      r = hip_fail(ctx, e, "farm graph: instantiate");
+    }
+  }
+  if (graph) hipGraphDestroy(graph);
+  (void)hipGetLastError();
+  if (r) {
+    farm_graph_reset(ctx);
+    return r;
+  }
+  ctx->farm_exec_batch = batch->id;
+  ctx->farm_exec_slots = slots;
+  ctx->farm_exec_neg = negative;
+  ctx->farm_exec_gen = ctx->comm_gen;
+  return LFM_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -1996,6 +2105,32 @@ int lfm_farm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, in
   int r = farm_drain_stale(ctx);
   if (!r) r = farm_buffers(ctx, (size_t)slots);
   if (r) return r;
+  // replayed from the captured graph (not while profiling: its events want the enqueued launches)
+  if (ctx->farm_graph_on && !ctx->prof) {
+    if (!ctx->farm_exec || ctx->farm_exec_batch != batch->id || ctx->farm_exec_slots != slots ||
+        ctx->farm_exec_neg != negative || ctx->farm_exec_gen != ctx->comm_gen) {
+      // capture not possible here: enqueue from now on (an error of the collective itself
+      // surfaces again on the enqueued path below)
+      if (farm_graph_build(ctx, batch, negative, slots)) ctx->farm_graph_on = false;
+    }
+    if (ctx->farm_exec) {
+      const int64_t np = batch->nprob, count = slots * ctx->nranks;
+      std::memcpy(batch->hbuf, hyp, (size_t)batch->nhyp * 8);
+      int* hst = reinterpret_cast<int*>(batch->hbuf + batch->nhyp + np);
+      for (int64_t q = 0; q < np; ++q) hst[q] = -1;
+      unsigned* seq_word = reinterpret_cast<unsigned*>(ctx->farm_pub + count);
+      __atomic_store_n(seq_word, 0u, __ATOMIC_RELEASE);
+      hipError_t e = hipGraphLaunch(ctx->farm_exec, ctx->stream);
+      if (e != hipSuccess) {
+        rccl_drop(ctx);
+        return hip_fail(ctx, e, "farm graph launch");
+      }
+      hipEventRecord(batch->done, ctx->stream);
+      r = farm_wait(ctx, seq_word, FARM_GRAPH_SEQ, count, recv);
+      if (r) return r;
+      return batch_status(ctx, batch, status);
+    }
+  }
   // this rank's padding slots: NaN (all-ones bytes), then the kernel writes its nprob slots
   if (slots > batch->nprob)
     hipMemsetAsync(ctx->farm_buf + batch->nprob, 0xFF, (size_t)(slots - batch->nprob) * 8,
@@ -2065,6 +2200,11 @@ int lfm_farm_allgather_f64(lfm_ctx* ctx, const double* send, int64_t count, doub
 
 int lfm_farm_destroy(lfm_ctx* ctx) {
   if (!ctx) return LFM_E_ARG;
+  farm_graph_reset(ctx);
+  if (ctx->farm_exec_old && hipStreamQuery(ctx->stream) == hipSuccess) {
+    hipGraphExecDestroy(ctx->farm_exec_old);
+    ctx->farm_exec_old = nullptr;
+  }
   if (ctx->comm && g_rccl.commDestroy) g_rccl.commDestroy((ncclComm_t)ctx->comm);
   ctx->comm = nullptr;
   ctx->nranks = 0;

@@ -203,6 +203,8 @@ __global__ __launch_bounds__(256) void gram_grid_aligned_kernel(
 //   1: 128 threads, a lane owns columns 2 l, 2 l + 1 (one 2-element vector store per row)
 //   2: 256 threads, wave w sweeps rows w, w + 4, ...: four 256-B stores cover a row's 1 KB
 //   3: 128 threads, wave w sweeps rows w, w + 2, ...: two 2-element vector stores per row
+//   5: the baseline's tiles and stores with nothing computed or staged (the value is the row
+//      index): the floor of this store pattern (results invalid)
 //   4: the baseline's body in a persistent grid (LFM_GRAM_AB_WG workgroups, default 2048) that
 //      strides over the tiles, one barrier before each restage
 template <typename T, int MODE>
@@ -301,6 +303,33 @@ __global__ __launch_bounds__(MODE == 2 ? 256 : 128) void gram_ab_kernel(
         out[row * ldo + c] = elem(ii, x);
       }
     }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void gram_ab_store_kernel(int64_t n, int lower, T* __restrict__ out,
+                                                            int64_t ldo) {
+  constexpr int R = 64, C = 256;
+  int64_t c0, r0;
+  if (lower) {
+    const int64_t b = blockIdx.x;
+    int64_t q = (int64_t)((sqrt(2.0 * (double)b + 1.0) - 1.0) * 0.5);
+    while (2 * (q + 1) * (q + 2) <= b) ++q;
+    while (2 * q * (q + 1) > b) --q;
+    const int64_t off = b - 2 * q * (q + 1);
+    r0 = (4 * q + off / (q + 1)) * R;
+    c0 = (off % (q + 1)) * C;
+  } else {
+    c0 = (int64_t)blockIdx.x * C;
+    r0 = (int64_t)blockIdx.y * R;
+  }
+  const int64_t c = c0 + threadIdx.x;
+  T* op = out + r0 * ldo + c;
+#pragma unroll 4
+  for (int i = 0; i < R; ++i) {
+    const int64_t row = r0 + i;
+    if (lower && c > row) continue;
+    op[(int64_t)i * ldo] = (T)row;
   }
 }
 
@@ -416,6 +445,9 @@ int launch_gram_grid(lfm_ctx* ctx, const HypDev& h, const GridLayout& lay, const
     else if (mode == 3)
       hipLaunchKernelGGL((gram_ab_kernel<OutT, 3>), grid, dim3(128), 0, ctx->stream, tabT, h.G,
                          lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out, ldo);
+    else if (mode == 5)
+      hipLaunchKernelGGL((gram_ab_store_kernel<OutT>), grid, dim3(256), 0, ctx->stream, n, lower,
+                         out, ldo);
     else if (mode == 4) {
       const char* wg = getenv("LFM_GRAM_AB_WG");
       const int64_t nt = (int64_t)grid.x * grid.y;

@@ -126,6 +126,14 @@ struct lfm_ctx {
                                                           // round's gathered slots + seq word
   unsigned farm_seq = 0;    // device-side rounds published so far
   bool farm_stale = false;  // an aborted farm call may have left work queued (drained first)
+  // the device-side round captured as one graph (LFM_FARM_GRAPH, default 1; read at creation),
+  // replayed while its key (batch id, slots, sign, communicator generation) holds
+  bool farm_graph_on = true;
+  hipGraphExec_t farm_exec = nullptr;
+  hipGraphExec_t farm_exec_old = nullptr;  // dropped by an aborted round: destroyed once drained
+  uint64_t farm_exec_batch = 0, comm_gen = 0, farm_exec_gen = 0;
+  int64_t farm_exec_slots = 0;
+  int farm_exec_neg = -1;
 };
 
 // ---------------------------------------------------------------- helpers
@@ -284,6 +292,7 @@ struct SmallFitLaunch {
 };
 int launch_small_fit(lfm_ctx* ctx, const SmallFitLaunch& f, size_t lds);
 int launch_small_args(lfm_ctx* ctx, SmallArgs& a, int nprob, int maxn, int maxg, int gridtab);
+void small_batch_attrs();  // the MLL kernels' 160 KB LDS attribute (before launches / capture)
 // gridtab: the largest small_grid_extra of the problems (doubles; 0: none on the grid path)
 // LDS doubles a grid-layout problem adds to its map: the gram tables, the times, the block genes
 size_t small_grid_extra(int n, int G, int T);

@@ -9,6 +9,7 @@
 //   small_fit_kernel          JaxTrainer.fit (src/trainer.py:162-228): every problem's Adam steps
 //                             run inside the kernel, one workgroup per problem.
 #include "lfm_dual.h"
+#include <mutex>
 
 namespace lfm {
 
@@ -213,9 +214,12 @@ __device__ __forceinline__ void small_factor_regs2(double* __restrict__ sm, int 
 //   accw   [4][2G + 1]      the waves' partial sums of 1/2 tr(W dSigma / d{D, S, l})
 //   gout   [3G + 3]         the gradient in the packed layout (dD dS dB, dl, d obs_stddev, 0)
 // and the fit (FIT): raw, mu, nu [3G + 3 each] (the unconstrained parameters, Adam's moments).
+#ifndef LFM_FIT_STAMPS
+#define LFM_FIT_STAMPS 0
+#endif
 struct SmallMap {
   double *A, *red, *hyp, *ktab, *colbuf, *xs, *ys, *gt;
-  double *gg, *piv, *iy, *al, *wd, *accw, *gout, *raw, *mu, *nu, *tms;
+  double *gg, *piv, *iy, *al, *wd, *accw, *gout, *raw, *mu, *nu, *tms, *stp;
   int* bgs;
   int n, ld, G;
 };
@@ -257,6 +261,7 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
     q.raw = take(3 * (size_t)G + 3);
     q.mu = take(3 * (size_t)G + 3);
     q.nu = take(3 * (size_t)G + 3);
+    if (LFM_FIT_STAMPS) q.stp = take(17);
   }
   if (m) *m = q;
   return o;
@@ -272,6 +277,23 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
 #ifndef LFM_SMALL_STAMPS
 #define LFM_SMALL_STAMPS 0
 #endif
+// timing experiment (make EXTRA=-DLFM_FIT_STAMPS=1; results of problem 1 invalid): the fit
+// kernel's block 0 sums, over its steps, the time of each phase of a step (s_memrealtime ticks)
+// and writes the sums into problem 1's history (scripts/fit_stamps.py)
+// (the sums live in the fit map's stamp slots, m.stp: [0, 16) the phase sums, [16] the last stamp)
+#if LFM_FIT_STAMPS
+__device__ __forceinline__ void fit_stamp(const SmallMap& m, int k) {
+  if (m.stp && blockIdx.x == 0 && threadIdx.x == 0) {
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(m.stp);
+    const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+    st[k] += t - st[16];
+    st[16] = t;
+  }
+}
+#else
+__device__ __forceinline__ void fit_stamp(const SmallMap&, int) {}
+#endif
+
 // The MLL from a two-wave factor (every thread: pr / zr its row's pivot and z entry, rows < n):
 // per-wave sums, then wave 0's + wave 1's in that order; returned to every thread.
 __device__ __forceinline__ double small_mll_2wave(double pr, double zr, int bad, int n,
@@ -648,6 +670,7 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
   small_sigma(P, m, h, 1);
   for (int t = tid; t < 4 * nacc; t += 256) m.accw[t] = 0.0;
   __syncthreads();
+  fit_stamp(m, 1);
   if (M > 64) {
     // two waves hold the rows (small_factor_regs2, one barrier a column); the derivative
     // tables first, by every thread (waves 2 and 3 only keep the factor's barrier count)
@@ -699,6 +722,7 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
     for (int q = tid - 64; q < ngg; q += 192) m.gg[q] = grad_table_entry(h, P.T, P.dt, m.tms, q);
   }
   __syncthreads();
+  fit_stamp(m, 2);
   // W = alpha alpha^T - S^{-1}, S^{-1}_ic = sum_{k >= i} XT[i][k] XT[c][k] (c <= i)
   const int np = n * (n + 1) / 2;
   for (int q = tid; q < np; q += 256) {
@@ -711,6 +735,7 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
     else A[i * ld + c] = w;
   }
   __syncthreads();
+  fit_stamp(m, 3);
   double* aw = m.accw + wv * nacc;  // this wave's partial sums: [0,G) D  [G,2G) S  [2G] l
   if (P.T > 0) {
     const int T = P.T, Wd = 2 * T - 1, nblk = n / T;
@@ -795,6 +820,7 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
     }
   }
   __syncthreads();
+  fit_stamp(m, 4);
   const bool failed = m.red[1] != 0.0;
   const double nan = __builtin_nan("");
   if (tid < G) {
@@ -823,6 +849,7 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
   *bad_out = (int)m.red[1];
   const double v = m.red[0];
   __syncthreads();
+  fit_stamp(m, 5);
   return v;
 }
 
@@ -937,6 +964,10 @@ __global__ __launch_bounds__(256) void small_fit_kernel(FitArgs a) {
     m.nu[i] = a.nu[gi];
   }
   small_stage(P, m);
+#if LFM_FIT_STAMPS
+  if (tid < 16) reinterpret_cast<unsigned long long*>(m.stp)[tid] = 0;
+  if (tid == 16) reinterpret_cast<unsigned long long*>(m.stp)[16] = __builtin_amdgcn_s_memrealtime();
+#endif
   __syncthreads();
   int first_bad = 0;
   for (int64_t s = 0; s < a.nsteps; ++s) {
@@ -946,6 +977,7 @@ __global__ __launch_bounds__(256) void small_fit_kernel(FitArgs a) {
       m.hyp[i] = i == 3 * G ? 0.5 + 3.0 * sigmoid_d(x) : i == 3 * G + 2 ? x : softplus_d(x);
     }
     __syncthreads();
+    fit_stamp(m, 0);
     int bad;
     const double v = small_value_grad_step(n, G, P.T, P.dt, a.negative, &bad);
     if (bad && !first_bad) first_bad = (int)s + 1;
@@ -968,7 +1000,12 @@ __global__ __launch_bounds__(256) void small_fit_kernel(FitArgs a) {
       m.raw[3] = 0.8;      // true_d[3]
     }
     __syncthreads();
+    fit_stamp(m, 6);
   }
+#if LFM_FIT_STAMPS
+  if (b == 0 && tid < 7 && a.nprob > 1 && tid < a.nsteps)
+    a.history[tid * a.nprob + 1] = (double)reinterpret_cast<unsigned long long*>(m.stp)[tid];
+#endif
   for (int i = tid; i < nh; i += 256) {
     const int gi = i < 3 * G ? od + i : os + (i - 3 * G);
     a.raw[gi] = m.raw[i];
@@ -992,13 +1029,11 @@ static void small_attr(const void* f) {
 
 int launch_small_grad(lfm_ctx* ctx, SmallArgs* a, const SmallProb* d_probs, const int* d_offs,
                       int nprob, size_t lds, int negative, double* out, double* grad, int* status) {
-  static bool attr = false;
-  if (!attr) {
+  static std::once_flag once;
+  std::call_once(once, [] {
     small_attr(reinterpret_cast<const void*>(&small_grad_kernel));
     small_attr(reinterpret_cast<const void*>(&small_grad_kernel_args));
-    small_attr(reinterpret_cast<const void*>(&small_fit_kernel));
-    attr = true;
-  }
+  });
   if (lds > 160 * 1024) return set_err(ctx, LFM_E_ARG, "small gradient batch: LDS past 160 KB");
   hipEvent_t ev;
   prof_begin(ctx, K_SMALL_GRAD, &ev, ctx->stream);
@@ -1018,11 +1053,8 @@ int launch_small_grad(lfm_ctx* ctx, SmallArgs* a, const SmallProb* d_probs, cons
 
 int launch_small_fit(lfm_ctx* ctx, const SmallFitLaunch& f, size_t lds) {
   if (lds > 160 * 1024) return set_err(ctx, LFM_E_ARG, "small fit batch: LDS past 160 KB");
-  static bool attr = false;
-  if (!attr) {
-    small_attr(reinterpret_cast<const void*>(&small_fit_kernel));
-    attr = true;
-  }
+  static std::once_flag once;
+  std::call_once(once, [] { small_attr(reinterpret_cast<const void*>(&small_fit_kernel)); });
   FitArgs a{};
   a.probs = f.probs;
   a.offs = f.offs;
@@ -1064,18 +1096,23 @@ static size_t small_lds(int maxn, int maxg, int gridtab, int* tabs_out) {
          sizeof(double);
 }
 
+// the MLL kernels' LDS limit raised to a CU's 160 KB, once per process (before any launch or
+// stream capture that uses them)
+void small_batch_attrs() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    small_attr(reinterpret_cast<const void*>(&small_mll_kernel));
+    small_attr(reinterpret_cast<const void*>(&small_mll_kernel_args));
+  });
+}
+
 int launch_small_args(lfm_ctx* ctx, SmallArgs& a, int nprob, int maxn, int maxg, int gridtab) {
   int tabs;
   const size_t lds = small_lds(maxn, maxg, gridtab, &tabs);
   if (lds > 160 * 1024 || nprob > SMALL_ARG_PROBS)
     return set_err(ctx, LFM_E_ARG, "small batch (kernel arguments): past its limits");
   a.tabs = tabs;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&small_mll_kernel_args),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  small_batch_attrs();
   hipEvent_t ev;
   prof_begin(ctx, K_SMALL, &ev, ctx->stream);
   hipLaunchKernelGGL(small_mll_kernel_args, dim3(nprob), dim3(256), lds, ctx->stream, a);
@@ -1090,12 +1127,7 @@ int launch_small_batch(lfm_ctx* ctx, const SmallProb* d_probs, int nprob, int ma
   if (lds > 160 * 1024)
     return set_err(ctx, LFM_E_ARG, "small batch: LDS past 160 KB (n <= 128, grid tables <= "
                                    "SMALL_GRID_TAB_MAX)");
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&small_mll_kernel),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  small_batch_attrs();
   hipEvent_t ev;
   prof_begin(ctx, K_SMALL, &ev, ctx->stream);
   hipLaunchKernelGGL(small_mll_kernel, dim3(nprob), dim3(256), lds, ctx->stream,

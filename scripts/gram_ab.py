@@ -4,6 +4,7 @@ profile, fp64 at N = 16384 (C2) and fp32 at N = 65536 (C4), lower triangle, devi
 PAD=<elements> is the script's own: the fill's leading dimension becomes N + PAD. ISO=<us>
 (also the script's own): each timed fill follows a device sync and a host sleep of that many
 microseconds, as bench.py's steps do (fill, 4-byte read-back, Python) instead of back to back.
+MEMSET=1 times lfm_memset_dev over the fill's byte count instead (contiguous; wall time).
 LFM_GRAM_AB=<mode> selects a store-shape variant in a library built with -DLFM_GRAM_AB.
 Round 3 A/B-ed its rows-per-tile / nontemporal / 16-B store variants this way (profiles/
 r03_ab_gram_*); those knobs were removed with the variants, so the gram has no per-call knob now."""
@@ -35,6 +36,8 @@ for vi, v in enumerate(variants):
     for k in {kk for vv in variants for kk in vv}:
         os.environ.pop(k, None)
     os.environ.update(v)
+    if v.get("MEMSET"):
+        continue
     for name, n, esz, fn, dx, dk, hp in cases:
         ld = n + int(v.get("PAD", 0))
         ctx.check(lib.lfm_memset_dev(h, dk, 0, n * ld * esz))
@@ -63,6 +66,17 @@ for rnd in range(4):
         os.environ.update(v)
         for name, n, esz, fn, dx, dk, hp in cases:
             ld = n + int(v.get("PAD", 0))
+            if v.get("MEMSET"):
+                # the runtime's fill of the same byte count, contiguous (wall time of 5, synced)
+                nb = esz * n * (n + 1) // 2
+                ctx.check(lib.lfm_memset_dev(h, dk, 0, nb))
+                ctx.check(lib.lfm_ctx_synchronize(h))
+                t0 = time.perf_counter()
+                for _ in range(5):
+                    ctx.check(lib.lfm_memset_dev(h, dk, 0, nb))
+                ctx.check(lib.lfm_ctx_synchronize(h))
+                res.setdefault((vi, name), []).append((time.perf_counter() - t0) / 5 * 1e3)
+                continue
             ctx.check(fn(h, dx, n, hp.ref, 0.0, _lib.LFM_UPLO_LOWER, dk, ld))
             ctx.profile(True, classes=["gram_grid"])
             ctx.profile_reset()

@@ -472,13 +472,17 @@ def test_run_fused_unpacks_the_gathered_slots():
 
 
 @pytest.mark.gpu
-def test_device_farm_round_one_rank():
+@pytest.mark.parametrize("graph", ["1", "0"])
+def test_device_farm_round_one_rank(monkeypatch, graph):
     """lfm_farm_batch_mll_f64 on a 1-rank communicator: the kernel writes the send slots, RCCL
     gathers them on the device and the publish kernel signals the host — the values are the
     resident batch's bit for bit, padding slots NaN, statuses as the batch's; repeated rounds with
-    changed hyperparameters follow them."""
+    changed hyperparameters follow them. Replayed from the captured graph (LFM_FARM_GRAPH=1, the
+    default; re-captured when the slots, the batch or the sign change) and enqueued call by call
+    (0)."""
     from dis_project_amd import _lib
 
+    monkeypatch.setenv("LFM_FARM_GRAPH", graph)
     ctx = _lib.Context(0)
     try:
         g = farm.RcclGather(ctx, 1, 0, farm.RcclGather.unique_id(ctx))
@@ -501,6 +505,18 @@ def test_device_farm_round_one_rank():
             with pytest.raises(_lib.LfmError) as ei:
                 ev.farm_round(models, 14)  # fewer slots than problems
             assert ei.value.code == _lib.LFM_E_ARG
+            # another batch (7 of the problems, the negated MLL) on the same communicator, then
+            # the first batch again
+            ev2 = farm.BatchEvaluator(ctx, datasets[:7], negative=True)
+            try:
+                for _ in range(2):
+                    got2 = ev2.farm_round(models[:7], 8)
+                    np.testing.assert_array_equal(got2[:7], ev2(models[:7]))
+                    np.testing.assert_array_equal(got2[:7], -want[:7])
+                    assert np.isnan(got2[7])
+            finally:
+                ev2.close()
+            np.testing.assert_array_equal(ev.farm_round(models, 15), want)
         finally:
             ev.close()
             g.close()
