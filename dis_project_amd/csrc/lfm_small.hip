@@ -277,9 +277,9 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
 #ifndef LFM_SMALL_STAMPS
 #define LFM_SMALL_STAMPS 0
 #endif
-// timing experiment (make EXTRA=-DLFM_FIT_STAMPS=1; results of problem 1 invalid): the fit
-// kernel's block 0 sums, over its steps, the time of each phase of a step (s_memrealtime ticks)
-// and writes the sums into problem 1's history (scripts/fit_stamps.py)
+// timing experiment (make EXTRA=-DLFM_FIT_STAMPS=1; problem 0's first history entries invalid):
+// the fit kernel's block 0 sums, over its steps, the time of each phase of a step (s_memrealtime
+// ticks) and writes the sums over its own first seven history entries (scripts/fit_stamps.py)
 // (the sums live in the fit map's stamp slots, m.stp: [0, 16) the phase sums, [16] the last stamp)
 #if LFM_FIT_STAMPS
 __device__ __forceinline__ void fit_stamp(const SmallMap& m, int k) {
@@ -1003,8 +1003,9 @@ __global__ __launch_bounds__(256) void small_fit_kernel(FitArgs a) {
     fit_stamp(m, 6);
   }
 #if LFM_FIT_STAMPS
-  if (b == 0 && tid < 7 && a.nprob > 1 && tid < a.nsteps)
-    a.history[tid * a.nprob + 1] = (double)reinterpret_cast<unsigned long long*>(m.stp)[tid];
+  __syncthreads();  // block 0's own history entries of steps 0-6 are done: overwrite them
+  if (b == 0 && tid < 7 && tid < a.nsteps)
+    a.history[tid * a.nprob] = (double)reinterpret_cast<unsigned long long*>(m.stp)[tid];
 #endif
   for (int i = tid; i < nh; i += 256) {
     const int gi = i < 3 * G ? od + i : os + (i - 3 * G);

@@ -1,6 +1,6 @@
 """Per-step phase times of small_fit_kernel's block 0 (problem 0) on the C5 batch, from a
 library built with make EXTRA=-DLFM_FIT_STAMPS=1 (loaded with LFM_LIBRARY=; that build
-overwrites problem 1's first seven history entries with the phase sums).
+overwrites problem 0's first seven history entries with the phase sums).
     LFM_LIBRARY=ablibs/fitst/liblfm.so python scripts/fit_stamps.py [iters]"""
 import os
 import sys
@@ -23,7 +23,8 @@ for rep in range(5):
     t0 = time.perf_counter()
     bt.fit()
     wall = time.perf_counter() - t0
-    res.append(bt.history[1, :7] * 0.01 / iters)  # ticks of 10 ns -> us per step
+    print('raw', bt.history[0, :8])
+    res.append(bt.history[0, :7] * 0.01 / iters)  # ticks of 10 ns -> us per step
     bt.close()
 r = np.median(np.array(res), axis=0)
 for nm, v in zip(names, r):
