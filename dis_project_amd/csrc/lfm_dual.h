@@ -133,6 +133,27 @@ __device__ __forceinline__ double wave_sum(double v) {
   return v;
 }
 
+// The same sum without LDS round trips (the small kernels' reductions are latency-bound): an
+// inclusive scan by DPP row shifts (1, 2, 4, 8) within each 16-lane row, row_bcast15 /
+// row_bcast31 across the rows, then lane 63's total read back to every lane. 32-bit DPP moves on
+// the two halves; lanes without a source read 0. Another summation order than wave_sum's.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_step(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROW_MASK, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROW_MASK, 0xf, true);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_step<0x111, 0xf>(v);  // row_shr:1
+  v += dpp_step<0x112, 0xf>(v);  // row_shr:2
+  v += dpp_step<0x114, 0xf>(v);  // row_shr:4
+  v += dpp_step<0x118, 0xf>(v);  // row_shr:8
+  v += dpp_step<0x142, 0xa>(v);  // row_bcast:15 into rows 1 and 3
+  v += dpp_step<0x143, 0xc>(v);  // row_bcast:31 into rows 2 and 3
+  return rdl(v, 63);
+}
+
 // ------------------------------------------------------- grid (table) path
 // On the dataset_3d grid every transcendental of kernel_xx and of its derivatives in
 // (D_j, D_k, l) separates per (gene, tau) or per (gene, d = tau' - tau), as in the gram's

@@ -73,12 +73,21 @@ __device__ __forceinline__ void small_factor_phase(double (&d)[W], int c, SmallF
     }
     // the wave's LDS operations complete in order: the reads see every lane's store
     asm volatile("" ::: "memory");
-    double col[W - 1];
+    // the column comes back in chunks of at most 32, every read of a chunk issued before its
+    // first use (sched_barrier: the scheduler would otherwise sink the reads to their uses and
+    // expose the LDS latency two or three reads at a time)
+    constexpr int CH = W > 32 ? 32 : W;
 #pragma unroll
-    for (int q = 1; q < W; ++q) col[q - 1] = f.colbuf[c + q];
-    asm volatile("" ::: "memory");  // every read issued before the first use
+    for (int q0 = 1; q0 < W; q0 += CH) {
+      double col[CH];
 #pragma unroll
-    for (int q = 1; q < W; ++q) d[q - 1] = fma(-lc, col[q - 1], d[q]);
+      for (int u = 0; u < CH; ++u)
+        if (q0 + u < W) col[u] = f.colbuf[c + q0 + u];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int u = 0; u < CH; ++u)
+        if (q0 + u < W) d[q0 + u - 1] = fma(-lc, col[u], d[q0 + u]);
+    }
     d[W - 1] = 0.0;
     f.dc = dn;
     f.y = yn;
@@ -154,6 +163,7 @@ __device__ __forceinline__ void small_factor2_phase(double (&d)[W], int c, Small
 #pragma unroll
       for (int u = 0; u < 16; ++u)
         if (q0 + u < W) col[u] = buf[c + q0 + u];
+      __builtin_amdgcn_sched_barrier(0);  // the chunk's reads issued before its first use
 #pragma unroll
       for (int u = 0; u < 16; ++u)
         if (q0 + u < W) d[q0 + u - 1] = fma(-lc, col[u], d[q0 + u]);
@@ -241,7 +251,10 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
   q.red = take(16);
   q.hyp = take(3 * (size_t)G + 3);
   q.ktab = take(tabs ? 3 * (size_t)G + n + (size_t)n * G : 0);
-  q.colbuf = take(n + 1 > 64 ? 512 : 128);  // two waves: two 256-slot column buffers
+  o = (o + 1) & ~(size_t)1;  // 16-B aligned: the sweep reads its row buffers 16 B at a time
+  // one wave: the factor's 128 or the sweep's two row buffers (2 x 64 and its copy shifted by
+  // one, 2 x 64 + 2); two waves: two 256-slot column buffers
+  q.colbuf = take(n + 1 > 64 ? 512 : 264);
   q.xs = take(3 * (size_t)n);
   q.ys = take((size_t)n);
   q.gt = take(T > 0 ? 2 * (size_t)G * W + 3 * (size_t)G * T + (size_t)G * G : 0);
@@ -279,7 +292,7 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
 #endif
 // timing experiment (make EXTRA=-DLFM_FIT_STAMPS=1; problem 0's first history entries invalid):
 // the fit kernel's block 0 sums, over its steps, the time of each phase of a step (s_memrealtime
-// ticks) and writes the sums over its own first seven history entries (scripts/fit_stamps.py)
+// ticks) and writes the sums over its own first ten history entries (scripts/fit_stamps.py)
 // (the sums live in the fit map's stamp slots, m.stp: [0, 16) the phase sums, [16] the last stamp)
 #if LFM_FIT_STAMPS
 __device__ __forceinline__ void fit_stamp(const SmallMap& m, int k) {
@@ -290,8 +303,16 @@ __device__ __forceinline__ void fit_stamp(const SmallMap& m, int k) {
     st[16] = t;
   }
 }
+// a thread's own time since the last stamp into slot k (the last stamp unchanged)
+__device__ __forceinline__ void fit_peek(const SmallMap& m, int k, int thread) {
+  if (m.stp && blockIdx.x == 0 && threadIdx.x == thread) {
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(m.stp);
+    st[k] += __builtin_amdgcn_s_memrealtime() - st[16];
+  }
+}
 #else
 __device__ __forceinline__ void fit_stamp(const SmallMap&, int) {}
+__device__ __forceinline__ void fit_peek(const SmallMap&, int, int) {}
 #endif
 
 // The MLL from a two-wave factor (every thread: pr / zr its row's pivot and z entry, rows < n):
@@ -617,7 +638,7 @@ __device__ __forceinline__ void small_inv_phase(double (&e)[W], int c, SmallInv&
       double col[W - 1];
 #pragma unroll
       for (int q = 1; q < W; ++q) col[q - 1] = f.A[min(c + q, f.n - 1) * f.ld + c];
-      asm volatile("" ::: "memory");  // every read issued before the first use
+      __builtin_amdgcn_sched_barrier(0);  // every read issued before the first use
 #pragma unroll
       for (int q = 1; q < W; ++q) e[q - 1] = c + q < f.n ? fma(-col[q - 1], xc, e[q]) : 0.0;
     } else {
@@ -628,6 +649,7 @@ __device__ __forceinline__ void small_inv_phase(double (&e)[W], int c, SmallInv&
 #pragma unroll
         for (int u = 0; u < 16; ++u)
           if (q0 + u < W) col[u] = f.A[min(c + q0 + u, f.n - 1) * f.ld + c];
+        __builtin_amdgcn_sched_barrier(0);  // the chunk's reads issued before its first use
 #pragma unroll
         for (int u = 0; u < 16; ++u)
           if (q0 + u < W) e[q0 + u - 1] = c + q0 + u < f.n ? fma(-col[u], xc, e[q0 + u]) : 0.0;
@@ -647,6 +669,121 @@ __device__ __forceinline__ void small_inverse(double* A, int ld, int n, const do
   for (int q = 0; q < MR; ++q) e[q] = q == f.j ? 1.0 : 0.0;
   small_inv_phase<MR>(e, 0, f);
   if (f.j < n) al[f.j] = f.a;  // alpha = X^T z
+}
+
+// The gradient's factorisation for n + 1 <= 64 (one wave): the sweep operator (Goodnight 1979;
+// Gauss-Jordan elimination of a symmetric matrix without pivoting, stable for SPD input) on the
+// augmented [[Sigma, r], [r^T, 0]], swept on its first n indices, leaves [[-Sigma^{-1}, alpha],
+// [alpha^T, -r^T Sigma^{-1} r]] with alpha = Sigma^{-1} r, and its pivots are the factor's
+// (L_kk^2, the Schur complements), so logdet = sum log d_k. One sweep replaces the factor, the
+// triangular inverse and the X^T X products (round 5: 10 + 14 + 2.2 us a step at n = 28).
+// Lane i holds row i, ROTATED so that the column being swept is always slot 0: after step k,
+// slot q holds column (q + k + 1) mod MR, and the swept column enters at slot MR - 1. Step k:
+// every lane puts its slot 0 (A[i][k] = A[k][i]) into buf[i] and buf[i + MR]; row k comes back
+// as buf[k + q]; then
+//   lane i != k: g = A[i][k] / d,  A[i][j] -= g A[k][j],  A[i][k] = g
+//   lane k:      A[k][j] /= d,                             A[k][k] = -1 / d.
+// On return slot q holds column (q + n) mod MR: alpha_i = a[0], column j < n sits at slot
+// j + MR - n. buf: >= 4 MR + 2 doubles of LDS, 16-B aligned.
+template <int MR>
+__device__ __forceinline__ void small_sweep_regs(const double* __restrict__ A, int ld, int n,
+                                                 double* buf, double (&a)[MR], double* logdet,
+                                                 int* bad_out) {
+  using dbl2 = double __attribute__((ext_vector_type(2)));
+  // the row comes back in chunks: the whole row at MR = 32, 16 at a time at MR = 64 (registers),
+  // 16 B a read: from buf when it starts at an even index, else from bufS (buf shifted by one)
+  constexpr int CH = MR == 32 ? 32 : 16;
+  double* bufS = buf + 2 * MR;
+  const int i = threadIdx.x;  // wave 0
+  const int M = n + 1;
+#pragma unroll
+  for (int q = 0; q < MR; ++q) {
+    double v = 0.0;
+    if (i < M && q < M && !(i == n && q == n)) v = q <= i ? A[i * ld + q] : A[q * ld + i];
+    a[q] = v;
+  }
+  double mypiv = 1.0;  // lane k keeps d_k (its log is taken once, after the sweep)
+  int bad = 0;
+  asm volatile("" ::: "memory");  // the rows are loaded before the buffers are written
+#pragma unroll 1
+  for (int k = 0; k < n; ++k) {
+    if (i < MR) {
+      buf[i] = a[0];
+      buf[i + MR] = a[0];
+      bufS[i + 1] = a[0];
+      bufS[i + 1 + MR] = a[0];
+    }
+    // the wave's LDS operations complete in order: the reads see every lane's store
+    asm volatile("" ::: "memory");
+    const int s0 = k + 1;  // row k's entries buf[s0 + q - 1], q = 1 .. MR - 1
+    const double* src = (s0 & 1) ? bufS + 1 : buf;  // src[s0 + 2 p] is 16-B aligned
+    const double d = buf[k];
+    double row[CH];
+#pragma unroll
+    for (int u = 0; u < CH; u += 2) {
+      const dbl2 v = *reinterpret_cast<const dbl2*>(src + s0 + u);
+      row[u] = v.x;
+      row[u + 1] = v.y;
+    }
+    // every read issued here, before the pivot's arithmetic (the scheduler would otherwise sink
+    // them to their uses and expose the LDS latency two reads at a time)
+    __builtin_amdgcn_sched_barrier(0);
+    if (!(d > 0.0) && bad == 0) bad = k + 1;
+    const bool piv = i == k;
+    if (piv) mypiv = d;
+    // 1 / d: v_rcp_f64 and two Newton steps
+    double invd = __builtin_amdgcn_rcp(d);
+    invd = fma(invd, fma(-d, invd, 1.0), invd);
+    invd = fma(invd, fma(-d, invd, 1.0), invd);
+    const double g = piv ? -invd : a[0] * invd;  // lane k: -g = 1 / d scales its row
+    const double keep = piv ? 0.0 : 1.0;
+#pragma unroll
+    for (int q0 = 1; q0 < MR; q0 += CH) {
+      if (q0 > 1) {
+#pragma unroll
+        for (int u = 0; u < CH; u += 2) {
+          const dbl2 v = *reinterpret_cast<const dbl2*>(src + s0 + (q0 - 1) + u);
+          row[u] = v.x;
+          row[u + 1] = v.y;
+        }
+        __builtin_amdgcn_sched_barrier(0);  // the chunk's reads issued before the first use
+      }
+#pragma unroll
+      for (int u = 0; u < CH; ++u)
+        if (q0 + u < MR) a[q0 + u - 1] = fma(-g, row[u], a[q0 + u] * keep);
+    }
+    a[MR - 1] = g;
+  }
+  // logdet = sum_k log d_k, one log per lane, then the wave's sum
+  double lp = i < n ? log(mypiv) : 0.0;
+  for (int o = 32; o > 0; o >>= 1) lp += __shfl_xor(lp, o);
+  *logdet = lp;
+  *bad_out = bad;
+}
+
+// W = alpha alpha^T - Sigma^{-1} from the sweep's rows (lane i: row i of -Sigma^{-1} and alpha_i):
+// alpha into al, W's strictly lower part into A (its Sigma is dead), diag(W) into wd.
+template <int MR>
+__device__ __forceinline__ void small_sweep_w(const double (&a)[MR], int n, double* A, int ld,
+                                              double* al, double* wd) {
+  const int i = threadIdx.x;  // wave 0
+  if (i < n) al[i] = a[0];
+  asm volatile("" ::: "memory");  // alpha in LDS before it is read back (in order)
+  const double ai = a[0];
+  // every alpha_j read before the first store (the stores into A could alias al otherwise)
+  double alj[MR];
+#pragma unroll
+  for (int q = 1; q < MR; ++q) alj[q] = al[max(q - (MR - n), 0)];
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int q = 1; q < MR; ++q) {
+    const int j = q - (MR - n);  // the column slot q holds (j < 0: none)
+    if (i < n && j >= 0 && j <= i) {
+      const double w = fma(ai, alj[q], a[q]);
+      if (j == i) wd[i] = w;
+      else A[i * ld + j] = w;
+    }
+  }
 }
 
 // (i, c), c <= i, of lower-triangle element q (row by row)
@@ -689,43 +826,43 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
     // X = L^{-1}: every L store landed before the factor's last barrier
     if (tid < 128) small_inverse<128>(A, ld, n, m.iy, m.al);
   } else if (wv == 0) {
-    double pr, zr;
-    int bad;
-    m.colbuf[64 + lane] = 0.0;
-    if (M <= 32)
-      small_factor_regs<32, true>(A, ld, n, M, m.colbuf, &pr, &zr, &bad, m.piv, m.iy);
-    else
-      small_factor_regs<64, true>(A, ld, n, M, m.colbuf, &pr, &zr, &bad, m.piv, m.iy);
-    // the MLL kernel's reduction, term for term (the same value to the bit)
-    double ldp = 0.0, qp = 0.0;
-    if (lane < n) {
-      ldp = log(pr);
-      qp = zr * zr;
+    // one wave: the sweep (small_sweep_regs) gives the MLL's logdet and quadratic form, alpha
+    // and -Sigma^{-1} at once; W is written straight from its rows
+    auto sweep = [&](auto& a) {
+      double logdet;
+      int bad;
+      small_sweep_regs(A, ld, n, m.colbuf, a, &logdet, &bad);
+      const double quad = -__shfl(a[0], n);  // lane n: -r^T Sigma^{-1} r
+      fit_peek(m, 7, 0);
+      small_sweep_w(a, n, A, ld, m.al, m.wd);
+      if (lane == 0) {
+        const double two_pi = 6.283185307179586476925;
+        double mll = -0.5 * ((double)n * log(two_pi) + logdet + quad);
+        mll *= negative ? -1.0 : 1.0;
+        if (bad) mll = __builtin_nan("");
+        m.red[0] = mll;
+        m.red[1] = (double)bad;
+      }
+      fit_peek(m, 8, 0);
+    };
+    if (M <= 32) {
+      double a[32];
+      sweep(a);
+    } else {
+      double a[64];
+      sweep(a);
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      ldp += __shfl_xor(ldp, o);
-      qp += __shfl_xor(qp, o);
-    }
-    if (lane == 0) {
-      const double two_pi = 6.283185307179586476925;
-      double mll = -0.5 * ((double)n * log(two_pi) + 2.0 * ldp + qp);
-      mll *= negative ? -1.0 : 1.0;
-      if (bad) mll = __builtin_nan("");
-      m.red[0] = mll;
-      m.red[1] = (double)bad;
-    }
-    asm volatile("" ::: "memory");  // the wave's L stores precede its reads below (in order)
-    if (M <= 32) small_inverse<32>(A, ld, n, m.iy, m.al);
-    else small_inverse<64>(A, ld, n, m.iy, m.al);
   } else if (P.T > 0) {
     const int ngg = (int)grad_tables_doubles(G, P.T);
     for (int q = tid - 64; q < ngg; q += 192) m.gg[q] = grad_table_entry(h, P.T, P.dt, m.tms, q);
+    fit_peek(m, 9, 64);
   }
   __syncthreads();
   fit_stamp(m, 2);
-  // W = alpha alpha^T - S^{-1}, S^{-1}_ic = sum_{k >= i} XT[i][k] XT[c][k] (c <= i)
+  // two waves: W = alpha alpha^T - S^{-1}, S^{-1}_ic = sum_{k >= i} XT[i][k] XT[c][k] (c <= i)
+  // (one wave: the sweep wrote W already)
   const int np = n * (n + 1) / 2;
-  for (int q = tid; q < np; q += 256) {
+  for (int q = M > 64 ? tid : np; q < np; q += 256) {
     int i, c;
     tri_index(q, &i, &c);
     double s = 0.0;
@@ -777,10 +914,10 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
         sVk += w * Vk;
         sVl += w * Vl;
       }
-      sV = wave_sum(sV);
-      sVj = wave_sum(sVj);
-      sVk = wave_sum(sVk);
-      sVl = wave_sum(sVl);
+      sV = wave_sum_dpp(sV);
+      sVj = wave_sum_dpp(sVj);
+      sVk = wave_sum_dpp(sVk);
+      sVl = wave_sum_dpp(sVl);
       if (lane == 0) {
         const double l = h.l, iDD = 1.0 / (h.D[j] + h.D[k]);
         const double Cm = h.S[j] * h.S[k] * l * kSqrtPi * 0.5 * iDD;
@@ -808,14 +945,14 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
         kc = gene_index(xb[1], G);
       }
       for (int g = 0; g < G; ++g) {
-        const double sD = wave_sum((jr == g ? o.dDr : 0.0) + (kc == g ? o.dDc : 0.0));
-        const double sS = wave_sum((jr == g ? o.dSr : 0.0) + (kc == g ? o.dSc : 0.0));
+        const double sD = wave_sum_dpp((jr == g ? o.dDr : 0.0) + (kc == g ? o.dDc : 0.0));
+        const double sS = wave_sum_dpp((jr == g ? o.dSr : 0.0) + (kc == g ? o.dSc : 0.0));
         if (lane == 0) {
           aw[g] += sD;
           aw[G + g] += sS;
         }
       }
-      const double sl = wave_sum(o.dl);
+      const double sl = wave_sum_dpp(o.dl);
       if (lane == 0) aw[2 * G] += sl;
     }
   }
@@ -837,14 +974,18 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
     m.gout[G + g] = failed ? nan : sign * aS;
     m.gout[2 * G + g] = failed ? nan : sign * (af / D);
   }
-  if (tid == 255) {
-    const double* acc = m.accw;
-    const double al_ = ((acc[2 * G] + acc[nacc + 2 * G]) + acc[2 * nacc + 2 * G]) + acc[3 * nacc + 2 * G];
-    double tr = 0.0;
-    for (int i = 0; i < n; ++i) tr += m.wd[i];
-    m.gout[3 * G] = failed ? nan : sign * al_;
-    m.gout[3 * G + 1] = failed ? nan : sign * sd * tr;
-    m.gout[3 * G + 2] = 0.0;  // jitter: a static field (model.py:64), no gradient
+  if (wv == 3) {
+    // tr W by the last wave (n <= 127: two entries a lane), summed across it by DPP
+    double tr = (lane < n ? m.wd[lane] : 0.0) + (lane + 64 < n ? m.wd[lane + 64] : 0.0);
+    tr = wave_sum_dpp(tr);
+    if (lane == 63) {
+      const double* acc = m.accw;
+      const double al_ =
+          ((acc[2 * G] + acc[nacc + 2 * G]) + acc[2 * nacc + 2 * G]) + acc[3 * nacc + 2 * G];
+      m.gout[3 * G] = failed ? nan : sign * al_;
+      m.gout[3 * G + 1] = failed ? nan : sign * sd * tr;
+      m.gout[3 * G + 2] = 0.0;  // jitter: a static field (model.py:64), no gradient
+    }
   }
   *bad_out = (int)m.red[1];
   const double v = m.red[0];
@@ -1004,7 +1145,7 @@ __global__ __launch_bounds__(256) void small_fit_kernel(FitArgs a) {
   }
 #if LFM_FIT_STAMPS
   __syncthreads();  // block 0's own history entries of steps 0-6 are done: overwrite them
-  if (b == 0 && tid < 7 && tid < a.nsteps)
+  if (b == 0 && tid < 10 && tid < a.nsteps)
     a.history[tid * a.nprob] = (double)reinterpret_cast<unsigned long long*>(m.stp)[tid];
 #endif
   for (int i = tid; i < nh; i += 256) {

@@ -63,9 +63,10 @@ def _problems(kind, seed=21):
 
 @pytest.mark.parametrize("negative", [True, False])
 def test_batch_grad_c5_and_c1_vs_oracle(negative):
-    """The C5 problems and C1 in one launch: every value within 1e-9 of the oracle and bit-
-    identical to lfm_batch_mll_f64's (the same Sigma and factor arithmetic), every gradient
-    component within 1e-8 of its summed terms' magnitude; a second call gives the same bits."""
+    """The C5 problems and C1 in one launch: every value within 1e-9 of the oracle and within
+    1e-12 of lfm_batch_mll_f64's (the same Sigma; the gradient's one-wave path factors by the
+    sweep operator, the MLL kernel by Cholesky), every gradient component within 1e-8 of its
+    summed terms' magnitude; a second call gives the same bits."""
     from dis_project_amd import _lib, configs
 
     models, datasets = farm.workload("c5")
@@ -74,7 +75,7 @@ def test_batch_grad_c5_and_c1_vs_oracle(negative):
     ev = farm.BatchEvaluator(_lib.get_context(), datasets, negative=negative)
     try:
         vals, grads = ev.value_and_grad(models)
-        np.testing.assert_array_equal(vals, ev(models))
+        np.testing.assert_allclose(vals, ev(models), rtol=1e-12, atol=0)
         _check_grads(vals, grads, models, datasets, negative)
         vals2, grads2 = ev.value_and_grad(models)
         np.testing.assert_array_equal(vals2, vals)
@@ -145,8 +146,9 @@ def test_batch_grad_memory_path_and_not_pd(monkeypatch):
 def test_batch_grad_two_wave_problems_vs_oracle():
     """Problems past one wave (64 < n + 1 <= 128: the two-wave factor and inverse, one barrier a
     column): the notebook's pooled replicates (N = 105, 84), a shuffled-row N = 96 problem and
-    N = 127, in one launch with a small C5 problem; values bit-identical to lfm_batch_mll_f64's
-    (the same two-wave factor), gradients within 1e-8 of the oracle's summed terms."""
+    N = 127, in one launch with a small C5 problem; the two-wave values bit-identical to
+    lfm_batch_mll_f64's (the same two-wave factor), the one-wave problem's within 1e-12 (the
+    sweep), gradients within 1e-8 of the oracle's summed terms."""
     from dis_project_amd import _lib, configs
     from dis_project_amd.dataset import Dataset, grid_inputs
     from dis_project_amd.model import ExactLFM
@@ -168,7 +170,9 @@ def test_batch_grad_two_wave_problems_vs_oracle():
     ev = farm.BatchEvaluator(_lib.get_context(), datasets, negative=True)
     try:
         vals, grads = ev.value_and_grad(models)
-        np.testing.assert_array_equal(vals, ev(models))
+        ref = ev(models)
+        np.testing.assert_array_equal(vals[:-1], ref[:-1])
+        np.testing.assert_allclose(vals[-1], ref[-1], rtol=1e-12, atol=0)
         _check_grads(vals, grads, models, datasets, True)
     finally:
         ev.close()
