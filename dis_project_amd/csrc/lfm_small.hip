@@ -786,6 +786,9 @@ __device__ __forceinline__ void small_sweep_w(const double (&a)[MR], int n, doub
   }
 }
 
+// genes up to which the gradient's grid reduction keeps per-thread, per-gene sums
+constexpr int SMALL_RED_G = 8;
+
 // (i, c), c <= i, of lower-triangle element q (row by row)
 __device__ __forceinline__ void tri_index(int q, int* i_out, int* c_out) {
   int i = (int)((sqrt(8.0 * q + 1.0) - 1.0) * 0.5);
@@ -879,53 +882,102 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
     const int nW = G * Wd, nT = G * T;
     const double* Tt = m.gg;           // six Toeplitz tables, table w at Tt + w nW
     const double* Pt = m.gg + 6 * nW;  // eight time tables, table w at Pt + w nT
-    const int nbp = nblk * (nblk + 1) / 2;
-    for (int bp = wv; bp < nbp; bp += 4) {
-      int bi, bc;
-      tri_index(bp, &bi, &bc);
-      const int j = m.bgs[bi], k = m.bgs[bc];
-      double sV = 0.0, sVj = 0.0, sVk = 0.0, sVl = 0.0;
-      for (int e = lane; e < T * T; e += 64) {
-        const int tau = e / T, tp = e - tau * T;
-        const int i = bi * T + tau, c = bc * T + tp;
-        if (c > i) continue;
-        const int d = tp - tau;
-        const int kd = k * Wd + (T - 1) + d, jd = j * Wd + (T - 1) - d;
-        const double Wk = Tt[kd], Xk = Tt[nW + kd], WkD = Tt[2 * nW + kd], XkD = Tt[3 * nW + kd];
-        const double Wkl = Tt[4 * nW + kd], Xkl = Tt[5 * nW + kd];
-        const double Wj = Tt[jd], Xj = Tt[nW + jd], WjD = Tt[2 * nW + jd], XjD = Tt[3 * nW + jd];
-        const double Wjl = Tt[4 * nW + jd], Xjl = Tt[5 * nW + jd];
-        const int kr = k * T + tau, jr = j * T + tau, jc = j * T + tp, kc = k * T + tp;
-        const double Pk = Pt[kr], PkD = Pt[nT + kr], Pkl = Pt[2 * nT + kr];
-        const double Ej = Pt[3 * nT + jr], EjD = Pt[4 * nT + jr];
-        const double Qj = Pt[5 * nT + jr], QjD = Pt[6 * nT + jr], Qjl = Pt[7 * nT + jr];
-        const double Pj = Pt[jc], PjD = Pt[nT + jc], Pjl = Pt[2 * nT + jc];
-        const double Ek = Pt[3 * nT + kc], EkD = Pt[4 * nT + kc];
-        const double Qk = Pt[5 * nT + kc], QkD = Pt[6 * nT + kc], Qkl = Pt[7 * nT + kc];
-        const double EE = Ek * Ej, QQ = Qk + Qj;
-        const double V = Wk + Wj - Xk * Pk - Xj * Pj - EE * QQ;
-        const double Vk = WkD - XkD * Pk - Xk * PkD - EkD * Ej * QQ - EE * QkD;
-        const double Vj = WjD - XjD * Pj - Xj * PjD - Ek * EjD * QQ - EE * QjD;
-        const double Vl =
-            Wkl - Xkl * Pk - Xk * Pkl + Wjl - Xjl * Pj - Xj * Pjl - EE * (Qkl + Qjl);
+    // element (i, c), c <= i, of gene block pair (bi, bc): the bracket V of kxx / (D_j + D_k) and
+    // its derivatives in D_j, D_k, l, from the derivative tables (grad_grid_kernel's reads)
+    auto elem = [&](int bi, int bc, int tau, int tp, int j, int k, double& V, double& Vj,
+                    double& Vk, double& Vl) {
+      const int d = tp - tau;
+      const int kd = k * Wd + (T - 1) + d, jd = j * Wd + (T - 1) - d;
+      const double Wk = Tt[kd], Xk = Tt[nW + kd], WkD = Tt[2 * nW + kd], XkD = Tt[3 * nW + kd];
+      const double Wkl = Tt[4 * nW + kd], Xkl = Tt[5 * nW + kd];
+      const double Wj = Tt[jd], Xj = Tt[nW + jd], WjD = Tt[2 * nW + jd], XjD = Tt[3 * nW + jd];
+      const double Wjl = Tt[4 * nW + jd], Xjl = Tt[5 * nW + jd];
+      const int kr = k * T + tau, jr = j * T + tau, jc = j * T + tp, kc = k * T + tp;
+      const double Pk = Pt[kr], PkD = Pt[nT + kr], Pkl = Pt[2 * nT + kr];
+      const double Ej = Pt[3 * nT + jr], EjD = Pt[4 * nT + jr];
+      const double Qj = Pt[5 * nT + jr], QjD = Pt[6 * nT + jr], Qjl = Pt[7 * nT + jr];
+      const double Pj = Pt[jc], PjD = Pt[nT + jc], Pjl = Pt[2 * nT + jc];
+      const double Ek = Pt[3 * nT + kc], EkD = Pt[4 * nT + kc];
+      const double Qk = Pt[5 * nT + kc], QkD = Pt[6 * nT + kc], Qkl = Pt[7 * nT + kc];
+      const double EE = Ek * Ej, QQ = Qk + Qj;
+      V = Wk + Wj - Xk * Pk - Xj * Pj - EE * QQ;
+      Vk = WkD - XkD * Pk - Xk * PkD - EkD * Ej * QQ - EE * QkD;
+      Vj = WjD - XjD * Pj - Xj * PjD - Ek * EjD * QQ - EE * QjD;
+      Vl = Wkl - Xkl * Pk - Xk * Pkl + Wjl - Xjl * Pj - Xj * Pjl - EE * (Qkl + Qjl);
+    };
+    if (G <= SMALL_RED_G) {
+      // every lower element by one thread (np / 256 rounds, no idle lanes), its contributions
+      // to the 2G + 1 sums scaled by its gene pair's constants and kept per thread and gene
+      // (predicated: the genes are run-time), then one DPP sum per accumulator and wave
+      double accD[SMALL_RED_G], accS[SMALL_RED_G], accl = 0.0;
+#pragma unroll
+      for (int g = 0; g < SMALL_RED_G; ++g) accD[g] = accS[g] = 0.0;
+      const double l = h.l;
+      for (int q = tid; q < np; q += 256) {
+        int i, c;
+        tri_index(q, &i, &c);
+        const int bi = i / T, bc = c / T;
+        const int tau = i - bi * T, tp = c - bc * T;
+        const int j = m.bgs[bi], k = m.bgs[bc];
+        double V, Vj, Vk, Vl;
+        elem(bi, bc, tau, tp, j, k, V, Vj, Vk, Vl);
         const double w = i == c ? 0.5 * m.wd[i] : A[i * ld + c];
-        sV += w * V;
-        sVj += w * Vj;
-        sVk += w * Vk;
-        sVl += w * Vl;
-      }
-      sV = wave_sum_dpp(sV);
-      sVj = wave_sum_dpp(sVj);
-      sVk = wave_sum_dpp(sVk);
-      sVl = wave_sum_dpp(sVl);
-      if (lane == 0) {
-        const double l = h.l, iDD = 1.0 / (h.D[j] + h.D[k]);
+        const double iDD = 1.0 / (h.D[j] + h.D[k]);
         const double Cm = h.S[j] * h.S[k] * l * kSqrtPi * 0.5 * iDD;
-        aw[j] += Cm * (sVj - sV * iDD);
-        aw[k] += Cm * (sVk - sV * iDD);
-        aw[G + j] += Cm * sV / h.S[j];
-        aw[G + k] += Cm * sV / h.S[k];
-        aw[2 * G] += Cm * (sV / l + sVl);
+        const double cV = Cm * (w * V);
+        const double dj = Cm * (w * Vj) - cV * iDD, dk = Cm * (w * Vk) - cV * iDD;
+        const double sj = cV / h.S[j], sk = cV / h.S[k];
+        accl += cV / l + Cm * (w * Vl);
+#pragma unroll
+        for (int g = 0; g < SMALL_RED_G; ++g) {
+          accD[g] += (j == g ? dj : 0.0) + (k == g ? dk : 0.0);
+          accS[g] += (j == g ? sj : 0.0) + (k == g ? sk : 0.0);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < SMALL_RED_G; ++g) {
+        if (g < G) {
+          const double sD = wave_sum_dpp(accD[g]), sS = wave_sum_dpp(accS[g]);
+          if (lane == 63) {
+            aw[g] = sD;
+            aw[G + g] = sS;
+          }
+        }
+      }
+      const double sl = wave_sum_dpp(accl);
+      if (lane == 63) aw[2 * G] = sl;
+    } else {
+      const int nbp = nblk * (nblk + 1) / 2;
+      for (int bp = wv; bp < nbp; bp += 4) {
+        int bi, bc;
+        tri_index(bp, &bi, &bc);
+        const int j = m.bgs[bi], k = m.bgs[bc];
+        double sV = 0.0, sVj = 0.0, sVk = 0.0, sVl = 0.0;
+        for (int e = lane; e < T * T; e += 64) {
+          const int tau = e / T, tp = e - tau * T;
+          const int i = bi * T + tau, c = bc * T + tp;
+          if (c > i) continue;
+          double V, Vj, Vk, Vl;
+          elem(bi, bc, tau, tp, j, k, V, Vj, Vk, Vl);
+          const double w = i == c ? 0.5 * m.wd[i] : A[i * ld + c];
+          sV += w * V;
+          sVj += w * Vj;
+          sVk += w * Vk;
+          sVl += w * Vl;
+        }
+        sV = wave_sum_dpp(sV);
+        sVj = wave_sum_dpp(sVj);
+        sVk = wave_sum_dpp(sVk);
+        sVl = wave_sum_dpp(sVl);
+        if (lane == 0) {
+          const double l = h.l, iDD = 1.0 / (h.D[j] + h.D[k]);
+          const double Cm = h.S[j] * h.S[k] * l * kSqrtPi * 0.5 * iDD;
+          aw[j] += Cm * (sVj - sV * iDD);
+          aw[k] += Cm * (sVk - sV * iDD);
+          aw[G + j] += Cm * sV / h.S[j];
+          aw[G + k] += Cm * sV / h.S[k];
+          aw[2 * G] += Cm * (sV / l + sVl);
+        }
       }
     }
   } else {
