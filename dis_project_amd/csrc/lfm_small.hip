@@ -209,7 +209,9 @@ __device__ __forceinline__ void small_factor_regs2(double* __restrict__ sm, int 
 
 // LDS map of one problem (doubles from the dynamic shared memory base), shared by the MLL,
 // gradient and fit kernels:
-//   A      [M x ld]         Sigma's lower triangle and the residual row n (M = n + 1, ld = n + 2)
+//   A      [M x ld]         Sigma's lower triangle and the residual row n (M = n + 1; ld the odd
+//                           one of n + 2, n + 3: a wave's accesses down a column, lane r at row r,
+//                           are then free of LDS bank conflicts)
 //   red    [16]             reductions
 //   hyp    [3G + 3]         D S B, l, obs_stddev, jitter (the constrained parameters)
 //   ktab   [3G + n + nG]    KxxTab's per-gene / per-row factors (tabs: n + 1 <= 64 in the launch)
@@ -222,6 +224,7 @@ __device__ __forceinline__ void small_factor_regs2(double* __restrict__ sm, int 
 //   gg     [6GW + 8GT]      the grid layout's derivative tables (grad_table_entry)
 //   piv, iy, al, wd [128 each] L_cc, 1 / L_cc, alpha = Sigma^{-1} r, diag(W)
 //   accw   [4][2G + 1]      the waves' partial sums of 1/2 tr(W dSigma / d{D, S, l})
+//   wb     [(n + 1) x ldw]  one wave: W's rows as the sweep leaves them (small_sweep_w)
 //   gout   [3G + 3]         the gradient in the packed layout (dD dS dB, dl, d obs_stddev, 0)
 // and the fit (FIT): raw, mu, nu [3G + 3 each] (the unconstrained parameters, Adam's moments).
 #ifndef LFM_FIT_STAMPS
@@ -229,10 +232,14 @@ __device__ __forceinline__ void small_factor_regs2(double* __restrict__ sm, int 
 #endif
 struct SmallMap {
   double *A, *red, *hyp, *ktab, *colbuf, *xs, *ys, *gt;
-  double *gg, *piv, *iy, *al, *wd, *accw, *gout, *raw, *mu, *nu, *tms, *stp;
+  double *gg, *piv, *iy, *al, *wd, *accw, *gout, *raw, *mu, *nu, *tms, *stp, *wb;
   int* bgs;
   int n, ld, G;
 };
+// the sweep's register width for n + 1 rows (one wave), and the row stride of its W buffer:
+// slot q of lane i's row lands at wb[i ldw + q - 1] (compile-time offsets, odd stride)
+__host__ __device__ constexpr int small_sweep_mr(int n) { return n + 1 <= 32 ? 32 : 64; }
+__host__ __device__ constexpr int small_wb_ld(int n) { return small_sweep_mr(n) | 1; }
 // doubles of the map (sm = nullptr: the size only)
 __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int tabs, int grad,
                                             int fit, SmallMap* m) {
@@ -245,9 +252,9 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
   const size_t W = T > 0 ? 2 * (size_t)T - 1 : 0;
   SmallMap q{};
   q.n = n;
-  q.ld = n + 2;
+  q.ld = (n + 2) | 1;
   q.G = G;
-  q.A = take((size_t)(n + 1) * (n + 2));
+  q.A = take((size_t)(n + 1) * q.ld);
   q.red = take(16);
   q.hyp = take(3 * (size_t)G + 3);
   q.ktab = take(tabs ? 3 * (size_t)G + n + (size_t)n * G : 0);
@@ -267,6 +274,8 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
     q.iy = take(128);
     q.al = take(128);
     q.wd = take(128);
+    // one wave (n + 1 <= 64): W's rows as the sweep leaves them, row stride ldw (small_wb_ld)
+    q.wb = take(n + 1 <= 64 ? (size_t)(n + 1) * small_wb_ld(n) : 0);
     q.accw = take(4 * (2 * (size_t)G + 1));
     q.gout = take(3 * (size_t)G + 3);
   }
@@ -292,7 +301,7 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
 #endif
 // timing experiment (make EXTRA=-DLFM_FIT_STAMPS=1; problem 0's first history entries invalid):
 // the fit kernel's block 0 sums, over its steps, the time of each phase of a step (s_memrealtime
-// ticks) and writes the sums over its own first ten history entries (scripts/fit_stamps.py)
+// ticks) and writes the sums over its own first twelve history entries (scripts/fit_stamps.py)
 // (the sums live in the fit map's stamp slots, m.stp: [0, 16) the phase sums, [16] the last stamp)
 #if LFM_FIT_STAMPS
 __device__ __forceinline__ void fit_stamp(const SmallMap& m, int k) {
@@ -374,6 +383,7 @@ __device__ __forceinline__ void small_sigma(const SmallProb& P, const SmallMap& 
     const int nt = (int)(2 * (int64_t)G * W + 3 * (int64_t)G * T + (int64_t)G * G);
     for (int q = tid; q < nt; q += 256) gt[q] = grid_table_entry(h, T, P.dt, m.tms, q);
     __syncthreads();
+    fit_peek(m, 10, 0);
     const double* Wt = gt;
     const double* Xt = Wt + G * W;
     const double* Pt = Xt + G * W;
@@ -397,6 +407,7 @@ __device__ __forceinline__ void small_sigma(const SmallProb& P, const SmallMap& 
       if (i == c) v = (v + jitter) + noise;
       sm[i * ld + c] = v;
     }
+    fit_peek(m, 11, 0);
   } else if (tabs) {
     // n <= 63 (the launch's LDS holds the tables): gene-gene pairs from KxxTab, the same bits
     // as kernel_ref with a third of its transcendentals; pairs with a latent row direct
@@ -445,10 +456,11 @@ __device__ __forceinline__ void small_body(const SmallProb P, int negative,
                                            double* __restrict__ out, int* __restrict__ status,
                                            int tabs, unsigned long long st0) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int n = P.n, M = n + 1, ld = n + 2, G = P.G;
+  const int n = P.n, M = n + 1, G = P.G;
   const int tid = threadIdx.x;
   SmallMap m;
   small_map(sm, n, G, P.T, tabs, 0, 0, &m);
+  const int ld = m.ld;
   double* red = m.red;  // [8] reduction scratch + [1] flag
   // hyperparameters staged in LDS (they may live in pinned host memory: read once), with x and
   // y, so that no later phase waits on HBM
@@ -715,19 +727,19 @@ __device__ __forceinline__ void small_sweep_regs(const double* __restrict__ A, i
     }
     // the wave's LDS operations complete in order: the reads see every lane's store
     asm volatile("" ::: "memory");
-    const int s0 = k + 1;  // row k's entries buf[s0 + q - 1], q = 1 .. MR - 1
-    const double* src = (s0 & 1) ? bufS + 1 : buf;  // src[s0 + 2 p] is 16-B aligned
-    const double d = buf[k];
+    // row k from its pivot on: r[u] = buf[k + u] (r[0] = d), 16 B a read from buf when k is
+    // even, else from bufS (buf shifted by one); the pivot's read is the oldest, so its
+    // arithmetic starts while the rest of the row is in flight
+    const double* src = (k & 1) ? bufS + 1 : buf;  // src[k + 2 p] is 16-B aligned
     double row[CH];
 #pragma unroll
     for (int u = 0; u < CH; u += 2) {
-      const dbl2 v = *reinterpret_cast<const dbl2*>(src + s0 + u);
+      const dbl2 v = *reinterpret_cast<const dbl2*>(src + k + u);
       row[u] = v.x;
       row[u + 1] = v.y;
     }
-    // every read issued here, before the pivot's arithmetic (the scheduler would otherwise sink
-    // them to their uses and expose the LDS latency two reads at a time)
     __builtin_amdgcn_sched_barrier(0);
+    const double d = row[0];
     if (!(d > 0.0) && bad == 0) bad = k + 1;
     const bool piv = i == k;
     if (piv) mypiv = d;
@@ -737,20 +749,21 @@ __device__ __forceinline__ void small_sweep_regs(const double* __restrict__ A, i
     invd = fma(invd, fma(-d, invd, 1.0), invd);
     const double g = piv ? -invd : a[0] * invd;  // lane k: -g = 1 / d scales its row
     const double keep = piv ? 0.0 : 1.0;
+    // slot q takes row entry q (r index q within the chunk starting at q0)
 #pragma unroll
-    for (int q0 = 1; q0 < MR; q0 += CH) {
-      if (q0 > 1) {
+    for (int q0 = 0; q0 < MR; q0 += CH) {
+      if (q0 > 0) {
 #pragma unroll
         for (int u = 0; u < CH; u += 2) {
-          const dbl2 v = *reinterpret_cast<const dbl2*>(src + s0 + (q0 - 1) + u);
+          const dbl2 v = *reinterpret_cast<const dbl2*>(src + k + q0 + u);
           row[u] = v.x;
           row[u + 1] = v.y;
         }
-        __builtin_amdgcn_sched_barrier(0);  // the chunk's reads issued before the first use
+        __builtin_amdgcn_sched_barrier(0);  // the chunk's reads issued before its first use
       }
 #pragma unroll
       for (int u = 0; u < CH; ++u)
-        if (q0 + u < MR) a[q0 + u - 1] = fma(-g, row[u], a[q0 + u] * keep);
+        if (q0 + u >= 1) a[q0 + u - 1] = fma(-g, row[u], a[q0 + u] * keep);
     }
     a[MR - 1] = g;
   }
@@ -762,28 +775,32 @@ __device__ __forceinline__ void small_sweep_regs(const double* __restrict__ A, i
 }
 
 // W = alpha alpha^T - Sigma^{-1} from the sweep's rows (lane i: row i of -Sigma^{-1} and alpha_i):
-// alpha into al, W's strictly lower part into A (its Sigma is dead), diag(W) into wd.
+// alpha into al, W's rows into A (its Sigma is dead; the reduction reads the strictly lower
+// part), diag(W) into wd.
 template <int MR>
-__device__ __forceinline__ void small_sweep_w(const double (&a)[MR], int n, double* A, int ld,
-                                              double* al, double* wd) {
+__device__ __forceinline__ void small_sweep_w(const double (&a)[MR], int n, double* wb,
+                                              double* alS, double* al, double* wd) {
+  constexpr int LDW = MR | 1;
   const int i = threadIdx.x;  // wave 0
-  if (i < n) al[i] = a[0];
+  // alpha at alS[MR - n + j] (slot q of every row holds column j = q - (MR - n)), so that
+  // every read and store below has a compile-time offset; alpha also into al
+  if (i < n) {
+    al[i] = a[0];
+    alS[MR - n + i] = a[0];
+  }
   asm volatile("" ::: "memory");  // alpha in LDS before it is read back (in order)
-  const double ai = a[0];
-  // every alpha_j read before the first store (the stores into A could alias al otherwise)
   double alj[MR];
 #pragma unroll
-  for (int q = 1; q < MR; ++q) alj[q] = al[max(q - (MR - n), 0)];
-  asm volatile("" ::: "memory");
+  for (int q = 1; q < MR; ++q) alj[q] = alS[q];
+  __builtin_amdgcn_sched_barrier(0);
+  // lane i's row (lanes past row n - 1 write the dead row n); the slots before column 0 hold
+  // the padding columns' products, never read
+  const double ai = a[0];
+  double* row = wb + min(i, n) * LDW - 1;
 #pragma unroll
-  for (int q = 1; q < MR; ++q) {
-    const int j = q - (MR - n);  // the column slot q holds (j < 0: none)
-    if (i < n && j >= 0 && j <= i) {
-      const double w = fma(ai, alj[q], a[q]);
-      if (j == i) wd[i] = w;
-      else A[i * ld + j] = w;
-    }
-  }
+  for (int q = 1; q < MR; ++q) row[q] = fma(ai, alj[q], a[q]);
+  asm volatile("" ::: "memory");  // the row stored before its diagonal is read back
+  if (i < n) wd[i] = row[MR - n + i];
 }
 
 // genes up to which the gradient's grid reduction keeps per-thread, per-gene sums
@@ -837,7 +854,7 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
       small_sweep_regs(A, ld, n, m.colbuf, a, &logdet, &bad);
       const double quad = -__shfl(a[0], n);  // lane n: -r^T Sigma^{-1} r
       fit_peek(m, 7, 0);
-      small_sweep_w(a, n, A, ld, m.al, m.wd);
+      small_sweep_w(a, n, m.wb, m.colbuf, m.al, m.wd);
       if (lane == 0) {
         const double two_pi = 6.283185307179586476925;
         double mll = -0.5 * ((double)n * log(two_pi) + logdet + quad);
@@ -877,6 +894,10 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
   __syncthreads();
   fit_stamp(m, 3);
   double* aw = m.accw + wv * nacc;  // this wave's partial sums: [0,G) D  [G,2G) S  [2G] l
+  // W's strictly lower part: W[i][c] = Wrow[i ldw + c] (one wave: the sweep's row buffer; two
+  // waves: A's lower triangle)
+  const int ldw = M <= 64 ? small_wb_ld(n) : ld;
+  const double* Wrow = M <= 64 ? m.wb + (small_sweep_mr(n) - n - 1) : A;
   if (P.T > 0) {
     const int T = P.T, Wd = 2 * T - 1, nblk = n / T;
     const int nW = G * Wd, nT = G * T;
@@ -912,7 +933,7 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
       double accD[SMALL_RED_G], accS[SMALL_RED_G], accl = 0.0;
 #pragma unroll
       for (int g = 0; g < SMALL_RED_G; ++g) accD[g] = accS[g] = 0.0;
-      const double l = h.l;
+
       for (int q = tid; q < np; q += 256) {
         int i, c;
         tri_index(q, &i, &c);
@@ -921,13 +942,13 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
         const int j = m.bgs[bi], k = m.bgs[bc];
         double V, Vj, Vk, Vl;
         elem(bi, bc, tau, tp, j, k, V, Vj, Vk, Vl);
-        const double w = i == c ? 0.5 * m.wd[i] : A[i * ld + c];
+        const double w = i == c ? 0.5 * m.wd[i] : Wrow[i * ldw + c];
         const double iDD = 1.0 / (h.D[j] + h.D[k]);
-        const double Cm = h.S[j] * h.S[k] * l * kSqrtPi * 0.5 * iDD;
+        const double Cm = h.S[j] * h.S[k] * h.l * kSqrtPi * 0.5 * iDD;
         const double cV = Cm * (w * V);
         const double dj = Cm * (w * Vj) - cV * iDD, dk = Cm * (w * Vk) - cV * iDD;
         const double sj = cV / h.S[j], sk = cV / h.S[k];
-        accl += cV / l + Cm * (w * Vl);
+        accl += cV / h.l + Cm * (w * Vl);
 #pragma unroll
         for (int g = 0; g < SMALL_RED_G; ++g) {
           accD[g] += (j == g ? dj : 0.0) + (k == g ? dk : 0.0);
@@ -959,7 +980,7 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
           if (c > i) continue;
           double V, Vj, Vk, Vl;
           elem(bi, bc, tau, tp, j, k, V, Vj, Vk, Vl);
-          const double w = i == c ? 0.5 * m.wd[i] : A[i * ld + c];
+          const double w = i == c ? 0.5 * m.wd[i] : Wrow[i * ldw + c];
           sV += w * V;
           sVj += w * Vj;
           sVk += w * Vk;
@@ -989,7 +1010,7 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
       if (q < np) {
         int i, c;
         tri_index(q, &i, &c);
-        const double w = i == c ? 0.5 * m.wd[i] : A[i * ld + c];
+        const double w = i == c ? 0.5 * m.wd[i] : Wrow[i * ldw + c];
         const double* xa = xs + 3 * i;
         const double* xb = xs + 3 * c;
         kernel_grad(h, xa[0], xa[1], xa[2], xb[0], xb[1], xb[2], w, o);
@@ -1162,19 +1183,22 @@ __global__ __launch_bounds__(256) void small_fit_kernel(FitArgs a) {
   if (tid == 16) reinterpret_cast<unsigned long long*>(m.stp)[16] = __builtin_amdgcn_s_memrealtime();
 #endif
   __syncthreads();
+  // model.constrain() (trainer.py:103): D, S, B, obs_stddev = softplus, l = 0.5 + 3 sigmoid; the
+  // jitter slot holds the static jitter itself
+  auto constrain = [&](int i, double x) {
+    return i == 3 * G ? 0.5 + 3.0 * sigmoid_d(x) : i == 3 * G + 2 ? x : softplus_d(x);
+  };
+  for (int i = tid; i < nh; i += 256) m.hyp[i] = constrain(i, m.raw[i]);
+  __syncthreads();
   int first_bad = 0;
   for (int64_t s = 0; s < a.nsteps; ++s) {
-    // model.constrain() (trainer.py:103)
-    for (int i = tid; i < nh; i += 256) {
-      const double x = m.raw[i];
-      m.hyp[i] = i == 3 * G ? 0.5 + 3.0 * sigmoid_d(x) : i == 3 * G + 2 ? x : softplus_d(x);
-    }
-    __syncthreads();
     fit_stamp(m, 0);
     int bad;
     const double v = small_value_grad_step(n, G, P.T, P.dt, a.negative, &bad);
     if (bad && !first_bad) first_bad = (int)s + 1;
     if (tid == 0) a.history[s * a.nprob + b] = v;
+    // the update, after_epoch on the unconstrained leaves, and the next step's constrained model,
+    // each parameter by its own thread (one barrier a step)
     if (tid < nh - 1) {
       const double x = m.raw[tid], g = m.gout[tid];
       const double sg = sigmoid_d(x);
@@ -1185,19 +1209,20 @@ __global__ __launch_bounds__(256) void small_fit_kernel(FitArgs a) {
       const double upd = -a.lr * (mu / c1) / (sqrt(nu / c2 + a.eps_root) + a.eps);
       m.mu[tid] = mu;
       m.nu[tid] = nu;
-      m.raw[tid] = x + upd;
-    }
-    __syncthreads();
-    if (a.fix && (a.step0 + s) % a.spe == 0 && G > 3 && tid == 0) {
-      m.raw[G + 3] = 1.0;  // true_s[3]
-      m.raw[3] = 0.8;      // true_d[3]
+      double xn = x + upd;
+      if (a.fix && (a.step0 + s) % a.spe == 0 && G > 3) {
+        if (tid == G + 3) xn = 1.0;  // true_s[3]
+        if (tid == 3) xn = 0.8;      // true_d[3]
+      }
+      m.raw[tid] = xn;
+      m.hyp[tid] = constrain(tid, xn);
     }
     __syncthreads();
     fit_stamp(m, 6);
   }
 #if LFM_FIT_STAMPS
   __syncthreads();  // block 0's own history entries of steps 0-6 are done: overwrite them
-  if (b == 0 && tid < 10 && tid < a.nsteps)
+  if (b == 0 && tid < 12 && tid < a.nsteps)
     a.history[tid * a.nprob] = (double)reinterpret_cast<unsigned long long*>(m.stp)[tid];
 #endif
   for (int i = tid; i < nh; i += 256) {

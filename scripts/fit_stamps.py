@@ -1,6 +1,6 @@
 """Per-step phase times of small_fit_kernel's block 0 (problem 0) on the C5 batch, from a
 library built with make EXTRA=-DLFM_FIT_STAMPS=1 (loaded with LFM_LIBRARY=; that build
-overwrites problem 0's first ten history entries with the phase sums).
+overwrites problem 0's first twelve history entries with the phase sums).
     LFM_LIBRARY=ablibs/fitst/liblfm.so python scripts/fit_stamps.py [iters]"""
 import os
 import sys
@@ -13,10 +13,11 @@ from dis_project_amd import _lib, configs, objectives, trainer  # noqa: E402
 
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 150
 ws = configs.c5_ablations()
-names = ["constrain", "gram (+ tables)", "factor | grad tables", "W (two waves)",
-         "tr(W dK) reduction", "gradient out", "Adam + after_epoch",
+names = ["(loop top)", "gram (+ tables)", "factor | grad tables", "W (two waves)",
+         "tr(W dK) reduction", "gradient out", "Adam + after_epoch + constrain",
          "  (inside phase 2) wave 0: factor done", "  (inside phase 2) wave 0: W written",
-         "  (inside phase 2) wave 1: grad tables done"]
+         "  (inside phase 2) wave 1: grad tables done",
+         "  (inside phase 1) thread 0: gram tables + barrier", "  (inside phase 1) thread 0: gram elements"]
 ctx = _lib.get_context(0)
 res = []
 for rep in range(5):
@@ -25,8 +26,8 @@ for rep in range(5):
     t0 = time.perf_counter()
     bt.fit()
     wall = time.perf_counter() - t0
-    print('raw', bt.history[0, :11])
-    res.append(bt.history[0, :10] * 0.01 / iters)  # ticks of 10 ns -> us per step
+    print('raw', bt.history[0, :12])
+    res.append(bt.history[0, :12] * 0.01 / iters)  # ticks of 10 ns -> us per step
     bt.close()
 r = np.median(np.array(res), axis=0)
 for nm, v in zip(names, r):
