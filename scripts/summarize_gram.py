@@ -6,7 +6,7 @@
                              lower fill of N = 16384 as its own kernel)
   gpurun_out/prof_unfused_write/  --pmc WRITE_SIZE of that run
 
-writes profiles/<round>_gram.json and profiles/<round>_gram.md: per fill, the rocprof average
+writes profiles/<round>_gram.json and profiles/<round>_gram_trace.md: per fill, the rocprof average
 duration of gram_grid_aligned_kernel, the algorithmic bytes (elem bytes x N (N + 1) / 2, the
 lower triangle with its diagonal), achieved GB/s and the fraction of the 8 TB/s spec, the
 WRITE_SIZE bytes per launch (exact for streaming stores, MI355X_MICROARCH.md §HBM), and the
@@ -104,7 +104,7 @@ def main():
     lines += ["", "Algorithmic bytes: the lower triangle with its diagonal, elem x N (N + 1) / 2 "
               "(the fill writes nothing above the diagonal: tests/test_gpu_regimes.py checks a "
               "0xFF sentinel there)."]
-    open(os.path.join(PROF, f"{rnd}_gram.md"), "w").write("\n".join(lines) + "\n")
+    open(os.path.join(PROF, f"{rnd}_gram_trace.md"), "w").write("\n".join(lines) + "\n")
     print("\n".join(lines))
 
 
