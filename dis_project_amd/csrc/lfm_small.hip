@@ -803,6 +803,107 @@ __device__ __forceinline__ void small_sweep_w(const double (&a)[MR], int n, doub
   if (i < n) wd[i] = row[MR - n + i];
 }
 
+// The sweep for n + 1 <= 32 with each row on TWO lanes (half the fused multiply-adds a step):
+// lane i holds slots 0..15 of row i, lane i + 32 slots 16..31 of row i, rotated as in
+// small_sweep_regs. Step k: the low lanes put their slot 0 (A[i][k]) into the buffers; each half
+// reads its 16 row entries (16 B a read) and A[i][k], d from the buffer; the high lane also forms
+// the new value of slot 16, which moves to the low lane's slot 15 (v_permlane32_swap), and takes
+// the swept column into slot 31. On return slot q holds column (q + n) mod 32, as before.
+__device__ __forceinline__ double swap_halves(double v) {
+  // lane i < 32 gets lane i + 32's value and lane i + 32 lane i's (v_permlane32_swap_b32)
+  const long long b = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false,
+                                                   false);
+  const bool low = (threadIdx.x & 32) == 0;
+  const unsigned l = low ? lo[1] : lo[0], h = low ? hi[1] : hi[0];
+  return __longlong_as_double(((long long)h << 32) | l);
+}
+
+__device__ __forceinline__ void small_sweep_half(const double* __restrict__ A, int ld, int n,
+                                                 double* buf, double (&a)[16], double* logdet,
+                                                 int* bad_out) {
+  using dbl2 = double __attribute__((ext_vector_type(2)));
+  constexpr int MR = 32;
+  double* bufS = buf + 2 * MR;
+  const int lane = threadIdx.x;  // wave 0
+  const int i = lane & 31, hi = lane >> 5;
+  const int M = n + 1;
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int q = hi * 16 + u;
+    double v = 0.0;
+    if (i < M && q < M && !(i == n && q == n)) v = q <= i ? A[i * ld + q] : A[q * ld + i];
+    a[u] = v;
+  }
+  double mypiv = 1.0;
+  int bad = 0;
+  asm volatile("" ::: "memory");  // the rows are loaded before the buffers are written
+#pragma unroll 1
+  for (int k = 0; k < n; ++k) {
+    if (hi == 0) {
+      buf[i] = a[0];
+      buf[i + MR] = a[0];
+      bufS[i + 1] = a[0];
+      bufS[i + 1 + MR] = a[0];
+    }
+    asm volatile("" ::: "memory");  // in-order LDS: the reads see every lane's store
+    const int s0 = k + hi * 16;  // this half's row entries buf[s0 + u], u = 0..15
+    const double* src = (s0 & 1) ? bufS + 1 : buf;
+    const double d = buf[k];
+    const double aik = buf[i];  // A[i][k]: the low lane's slot 0, for both halves
+    double row[16];
+#pragma unroll
+    for (int u = 0; u < 16; u += 2) {
+      const dbl2 v = *reinterpret_cast<const dbl2*>(src + s0 + u);
+      row[u] = v.x;
+      row[u + 1] = v.y;
+    }
+    __builtin_amdgcn_sched_barrier(0);  // every read issued before the pivot's arithmetic
+    if (!(d > 0.0) && bad == 0) bad = k + 1;
+    const bool piv = i == k;
+    if (piv) mypiv = d;
+    double invd = __builtin_amdgcn_rcp(d);
+    invd = fma(invd, fma(-d, invd, 1.0), invd);
+    invd = fma(invd, fma(-d, invd, 1.0), invd);
+    const double g = piv ? -invd : aik * invd;
+    const double keep = piv ? 0.0 : 1.0;
+    // the high lane's old slot 16 -> the low lane's new slot 15
+    const double t = swap_halves(fma(-g, row[0], a[0] * keep));
+#pragma unroll
+    for (int u = 1; u < 16; ++u) a[u - 1] = fma(-g, row[u], a[u] * keep);
+    a[15] = hi ? g : t;
+  }
+  double lp = (hi == 0 && i < n) ? log(mypiv) : 0.0;
+  for (int o = 32; o > 0; o >>= 1) lp += __shfl_xor(lp, o);
+  *logdet = lp;
+  *bad_out = bad;
+}
+
+// small_sweep_w for the two-lane rows of small_sweep_half.
+__device__ __forceinline__ void small_sweep_w_half(const double (&a)[16], int n, double* wb,
+                                                   double* alS, double* al, double* wd) {
+  constexpr int MR = 32, LDW = MR | 1;
+  const int lane = threadIdx.x;
+  const int i = lane & 31, hi = lane >> 5;
+  if (hi == 0 && i < n) {
+    al[i] = a[0];
+    alS[MR - n + i] = a[0];
+  }
+  asm volatile("" ::: "memory");  // alpha in LDS before it is read back (in order)
+  const double ai = al[min(i, max(n - 1, 0))];
+  double alj[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) alj[u] = alS[hi * 16 + u];
+  __builtin_amdgcn_sched_barrier(0);
+  double* row = wb + min(i, n) * LDW - 1 + hi * 16;
+#pragma unroll
+  for (int u = 0; u < 16; ++u)
+    if (hi || u > 0) row[u] = fma(ai, alj[u], a[u]);
+  asm volatile("" ::: "memory");  // both halves' stores before the diagonal is read back
+  if (hi == 0 && i < n) wd[i] = wb[i * LDW - 1 + MR - n + i];
+}
+
 // genes up to which the gradient's grid reduction keeps per-thread, per-gene sums
 constexpr int SMALL_RED_G = 8;
 
@@ -866,8 +967,23 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
       fit_peek(m, 8, 0);
     };
     if (M <= 32) {
-      double a[32];
-      sweep(a);
+      // each row on two lanes (small_sweep_half)
+      double a[16];
+      double logdet;
+      int bad;
+      small_sweep_half(A, ld, n, m.colbuf, a, &logdet, &bad);
+      const double quad = -__shfl(a[0], n);  // lane n: -r^T Sigma^{-1} r
+      fit_peek(m, 7, 0);
+      small_sweep_w_half(a, n, m.wb, m.colbuf, m.al, m.wd);
+      if (lane == 0) {
+        const double two_pi = 6.283185307179586476925;
+        double mll = -0.5 * ((double)n * log(two_pi) + logdet + quad);
+        mll *= negative ? -1.0 : 1.0;
+        if (bad) mll = __builtin_nan("");
+        m.red[0] = mll;
+        m.red[1] = (double)bad;
+      }
+      fit_peek(m, 8, 0);
     } else {
       double a[64];
       sweep(a);
