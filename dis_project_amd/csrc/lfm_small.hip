@@ -37,18 +37,13 @@ struct SmallFactor {
   double dc, y;      // the current column's pivot input and 1 / sqrt of it
   double mp, mz;     // this lane's pivot and z entry
   int bad;
-  // STORE (the gradient): L's strictly lower part and the residual row z into A (row stride
-  // ld), the pivots L_cc and their multipliers 1 / L_cc (y) into piv / iy
-  double* A;
-  int ld;
-  double *piv, *iy;
 };
 // window widths of the phases: 64 48 32 24 16 12 8
 template <int W>
 constexpr int small_next_w() {
   return W == 64 ? 48 : W == 48 ? 32 : W == 32 ? 24 : W == 24 ? 16 : W == 16 ? 12 : 8;
 }
-template <int W, bool STORE>
+template <int W>
 __device__ __forceinline__ void small_factor_phase(double (&d)[W], int c, SmallFactor& f) {
   // phase W: the columns while more than the next width of them remain (the last phase: all)
   constexpr int WN = small_next_w<W>();
@@ -64,13 +59,6 @@ __device__ __forceinline__ void small_factor_phase(double (&d)[W], int c, SmallF
     const double dn = rdl(fma(-lc, lc, d[1]), c + 1);
     const double yn = rsqrt_1nr(dn);
     f.colbuf[f.r] = (f.act && f.r > c) ? lc : 0.0;
-    if constexpr (STORE) {
-      if (f.act && f.r > c) f.A[f.r * f.ld + c] = lc;
-      if (f.r == c) {
-        f.piv[c] = lc;
-        f.iy[c] = f.y;
-      }
-    }
     // the wave's LDS operations complete in order: the reads see every lane's store
     asm volatile("" ::: "memory");
     // the column comes back in chunks of at most 32, every read of a chunk issued before its
@@ -93,22 +81,17 @@ __device__ __forceinline__ void small_factor_phase(double (&d)[W], int c, SmallF
     f.y = yn;
   }
   if constexpr (W > 8)
-    if (c < f.n) small_factor_phase<WN, STORE>(*reinterpret_cast<double(*)[WN]>(&d[0]), c, f);
+    if (c < f.n) small_factor_phase<WN>(*reinterpret_cast<double(*)[WN]>(&d[0]), c, f);
 }
-template <int MR, bool STORE = false>
-__device__ __forceinline__ void small_factor_regs(double* __restrict__ sm, int ld, int n, int M,
-                                                  double* colbuf, double* piv_r, double* z_r,
-                                                  int* bad_out, double* piv = nullptr,
-                                                  double* iy = nullptr) {
+template <int MR>
+__device__ __forceinline__ void small_factor_regs(const double* __restrict__ sm, int ld, int n,
+                                                  int M, double* colbuf, double* piv_r,
+                                                  double* z_r, int* bad_out) {
   SmallFactor f;
   f.n = n;
   f.r = threadIdx.x;  // wave 0
   f.act = f.r < M;
   f.colbuf = colbuf;
-  f.A = sm;
-  f.ld = ld;
-  f.piv = piv;
-  f.iy = iy;
   double d[MR];
 #pragma unroll
   for (int q = 0; q < MR; ++q) d[q] = (f.act && q <= f.r && q < n) ? sm[f.r * ld + q] : 0.0;
@@ -116,9 +99,7 @@ __device__ __forceinline__ void small_factor_regs(double* __restrict__ sm, int l
   f.y = rsqrt_1nr(f.dc);
   f.mp = f.mz = 0.0;
   f.bad = 0;
-  // the window is loaded: STORE may overwrite the rows' entries from here on
-  asm volatile("" ::: "memory");
-  small_factor_phase<MR, STORE>(d, 0, f);
+  small_factor_phase<MR>(d, 0, f);
   *piv_r = f.mp;
   *z_r = f.mz;
   *bad_out = f.bad;
@@ -135,7 +116,7 @@ template <int W>
 constexpr int small_next_w2() {
   return W == 128 ? 96 : W == 96 ? 64 : small_next_w<W>();
 }
-template <int W, bool STORE>
+template <int W>
 __device__ __forceinline__ void small_factor2_phase(double (&d)[W], int c, SmallFactor& f) {
   constexpr int WN = small_next_w2<W>();
   const int cend = W > 8 ? max(c, f.n - WN) : f.n;
@@ -147,13 +128,6 @@ __device__ __forceinline__ void small_factor2_phase(double (&d)[W], int c, Small
     double* buf = f.colbuf + (c & 1) * 256;
     if (f.r < 128) buf[f.r] = (f.act && f.r > c) ? lc : 0.0;
     if (f.r == c + 1) buf[255] = fma(-lc, lc, d[1]);  // the next pivot's input
-    if constexpr (STORE) {
-      if (f.act && f.r > c) f.A[f.r * f.ld + c] = lc;
-      if (f.r == c) {
-        f.piv[c] = lc;
-        f.iy[c] = f.y;
-      }
-    }
     __syncthreads();
     if (f.r == c) f.mz = buf[f.n];  // L[n][c] = z[c], from the residual row's lane
     const double dn = buf[255];
@@ -173,22 +147,16 @@ __device__ __forceinline__ void small_factor2_phase(double (&d)[W], int c, Small
     f.y = rsqrt_1nr(dn);
   }
   if constexpr (W > 8)
-    if (c < f.n) small_factor2_phase<WN, STORE>(*reinterpret_cast<double(*)[WN]>(&d[0]), c, f);
+    if (c < f.n) small_factor2_phase<WN>(*reinterpret_cast<double(*)[WN]>(&d[0]), c, f);
 }
-template <bool STORE = false>
-__device__ __forceinline__ void small_factor_regs2(double* __restrict__ sm, int ld, int n, int M,
-                                                   double* colbuf, double* piv_r, double* z_r,
-                                                   int* bad_out, double* piv = nullptr,
-                                                   double* iy = nullptr) {
+__device__ __forceinline__ void small_factor_regs2(const double* __restrict__ sm, int ld, int n,
+                                                   int M, double* colbuf, double* piv_r,
+                                                   double* z_r, int* bad_out) {
   SmallFactor f;
   f.n = n;
   f.r = threadIdx.x;
   f.act = f.r < M;
   f.colbuf = colbuf;
-  f.A = sm;
-  f.ld = ld;
-  f.piv = piv;
-  f.iy = iy;
   // the buffers' tails past the rows read as zeros (window entries past the last column)
   for (int i = threadIdx.x; i < 256; i += blockDim.x) {
     if (i >= 128) colbuf[i] = colbuf[256 + i] = 0.0;
@@ -200,8 +168,8 @@ __device__ __forceinline__ void small_factor_regs2(double* __restrict__ sm, int 
   f.y = rsqrt_1nr(f.dc);
   f.mp = f.mz = 0.0;
   f.bad = 0;
-  __syncthreads();  // windows loaded (STORE overwrites rows from here on), buffer tails zero
-  small_factor2_phase<128, STORE>(d, 0, f);
+  __syncthreads();  // windows loaded, buffer tails zero
+  small_factor2_phase<128>(d, 0, f);
   *piv_r = f.mp;
   *z_r = f.mz;
   *bad_out = f.bad;
@@ -222,7 +190,7 @@ __device__ __forceinline__ void small_factor_regs2(double* __restrict__ sm, int 
 //   tms, bgs [T], [n / T]    the grid layout's times and block genes (grid problems)
 // the gradient and the fit (GRAD) add, past this problem's gram tables:
 //   gg     [6GW + 8GT]      the grid layout's derivative tables (grad_table_entry)
-//   piv, iy, al, wd [128 each] L_cc, 1 / L_cc, alpha = Sigma^{-1} r, diag(W)
+//   al, wd [128 each]       alpha = Sigma^{-1} r, diag(W)
 //   accw   [4][2G + 1]      the waves' partial sums of 1/2 tr(W dSigma / d{D, S, l})
 //   wb     [(n + 1) x ldw]  one wave: W's rows as the sweep leaves them (small_sweep_w)
 //   gout   [3G + 3]         the gradient in the packed layout (dD dS dB, dl, d obs_stddev, 0)
@@ -232,10 +200,13 @@ __device__ __forceinline__ void small_factor_regs2(double* __restrict__ sm, int 
 #endif
 struct SmallMap {
   double *A, *red, *hyp, *ktab, *colbuf, *xs, *ys, *gt;
-  double *gg, *piv, *iy, *al, *wd, *accw, *gout, *raw, *mu, *nu, *tms, *stp, *wb;
+  double *gg, *al, *wd, *accw, *gout, *raw, *mu, *nu, *tms, *stp, *wb;
   int* bgs;
   int n, ld, G;
 };
+// the four-wave sweep's buffers (small_sweep4): per step parity a row buffer (256) and its
+// copy shifted by one (258), then per parity the crossing slots (128), then two wave sums
+constexpr int SWEEP4_LDS = 2 * 520 + 2 * 128 + 8;
 // the sweep's register width for n + 1 rows (one wave), and the row stride of its W buffer:
 // slot q of lane i's row lands at wb[i ldw + q - 1] (compile-time offsets, odd stride)
 __host__ __device__ constexpr int small_sweep_mr(int n) { return n + 1 <= 32 ? 32 : 64; }
@@ -261,7 +232,7 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
   o = (o + 1) & ~(size_t)1;  // 16-B aligned: the sweep reads its row buffers 16 B at a time
   // one wave: the factor's 128 or the sweep's two row buffers (2 x 64 and its copy shifted by
   // one, 2 x 64 + 2); two waves: two 256-slot column buffers
-  q.colbuf = take(n + 1 > 64 ? 512 : 264);
+  q.colbuf = take(n + 1 > 64 ? (grad ? SWEEP4_LDS : 512) : 264);
   q.xs = take(3 * (size_t)n);
   q.ys = take((size_t)n);
   q.gt = take(T > 0 ? 2 * (size_t)G * W + 3 * (size_t)G * T + (size_t)G * G : 0);
@@ -270,8 +241,6 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
   q.bgs = reinterpret_cast<int*>(take(T > 0 ? ((size_t)n / T + 1) / 2 + 1 : 0));
   if (grad) {
     q.gg = take(T > 0 ? 6 * (size_t)G * W + 8 * (size_t)G * T : 0);
-    q.piv = take(128);
-    q.iy = take(128);
     q.al = take(128);
     q.wd = take(128);
     // one wave (n + 1 <= 64): W's rows as the sweep leaves them, row stride ldw (small_wb_ld)
@@ -527,7 +496,7 @@ __device__ __forceinline__ void small_body(const SmallProb P, int negative,
     // column
     double pr, zr;
     int bad;
-    small_factor_regs2<false>(sm, ld, n, M, colbuf, &pr, &zr, &bad);
+    small_factor_regs2(sm, ld, n, M, colbuf, &pr, &zr, &bad);
     const double mll = small_mll_2wave(pr, zr, bad, n, negative, red);
     if (tid == 0) {
       out[blockIdx.x] = mll;
@@ -609,15 +578,14 @@ __global__ __launch_bounds__(256) void small_mll_kernel_args(SmallArgs a) {
 // before the bijectors' chain rule (the large-N path's algebra, lfm_grad.hip):
 //     d log N(y; m, S) / d theta = 1/2 tr(W dS/dtheta) + alpha^T dm/dtheta,
 //     alpha = S^{-1} r,  W = alpha alpha^T - S^{-1},
-// for n <= 63 (n + 1 <= 64: one wave holds the augmented matrix, small_factor_regs):
-//   1. Sigma and r in LDS (small_sigma: the MLL kernel's arithmetic, so the value is the MLL
-//      kernel's to the bit);
-//   2. wave 0: the factor, storing L (strictly lower), its pivots and z = L^{-1} r into LDS, then
-//      X = L^{-1} by the same right-looking register window (lane j = column j of X, which it
-//      writes transposed into A's free upper triangle: XT[j][c] = X[c][j]); waves 1-3 meanwhile
-//      build the grid layout's derivative tables (grad_table_entry);
-//   3. W's lower triangle (S^{-1} = X^T X as row dot products of XT; alpha = X^T z accumulated
-//      by the inverse's sweep), into A's strictly lower part (L is dead) and wd;
+// for n <= 127 (n + 1 <= 128 rows of the augmented matrix in registers):
+//   1. Sigma and r in LDS (small_sigma: the MLL kernel's arithmetic);
+//   2. the sweep operator on [[Sigma, r], [r^T, 0]] (below): -Sigma^{-1}, alpha and the pivots
+//      (logdet) in one pass — on half a wave (n + 1 <= 32, two lanes a row), one wave
+//      (n + 1 <= 64; waves 1-3 meanwhile build the grid layout's derivative tables,
+//      grad_table_entry) or four waves (n + 1 <= 128, one barrier a step);
+//   3. W = alpha alpha^T - Sigma^{-1} written by the sweep's last pass (small_sweep_w*): into wb
+//      (one wave) or A's lower triangle (four waves), diag(W) into wd;
 //   4. 1/2 tr(W dS/d{D, S, l}): grid problems one wave per gene-block pair (its rows share gene
 //      j, its columns gene k: the derivative tables as grad_grid_kernel reads them, the gene-pair
 //      constant applied to the wave's sums); other layouts one lane per pair with the dual-number
@@ -627,61 +595,6 @@ __global__ __launch_bounds__(256) void small_mll_kernel_args(SmallArgs a) {
 //      flag_i (model.py:124-149), the sign of CustomConjMLL(negative); NaN on a failed factor.
 // Every thread calls it, with the hyperparameters (hyp), x and y in LDS; on return (after a
 // barrier) m.gout holds the gradient and the MLL is returned to every thread.
-
-// X = L^{-1}, lane j: e[q] = B[c + q][j] over the rows from c on (B = I initially), right-looking
-// as small_factor_phase: X[c][j] = e[0] / L_cc, e[q - 1] = e[q] - L[c + q][c] X[c][j].
-struct SmallInv {
-  double* A;
-  int ld, n, j;
-  const double* iy;
-  double a;  // alpha_j = sum_{c >= j} X[c][j] z_c, accumulated as the sweep forms X[c][j]
-};
-template <int W>
-__device__ __forceinline__ void small_inv_phase(double (&e)[W], int c, SmallInv& f) {
-  constexpr int WN = small_next_w2<W>();
-  const int cend = W > 8 ? max(c, f.n - WN) : f.n;
-#pragma unroll 1
-  for (; c < cend; ++c) {
-    const double xc = e[0] * f.iy[c];
-    if (f.j <= c) f.A[f.j * f.ld + c] = xc;  // XT[j][c]: A's upper triangle (L is strictly lower)
-    if (f.j <= c) f.a = fma(xc, f.A[f.n * f.ld + c], f.a);  // z_c: row n (the residual)
-    // rows past n - 1 are not L's (row n holds z): their window entries stay zero
-    if constexpr (W <= 64) {
-      double col[W - 1];
-#pragma unroll
-      for (int q = 1; q < W; ++q) col[q - 1] = f.A[min(c + q, f.n - 1) * f.ld + c];
-      __builtin_amdgcn_sched_barrier(0);  // every read issued before the first use
-#pragma unroll
-      for (int q = 1; q < W; ++q) e[q - 1] = c + q < f.n ? fma(-col[q - 1], xc, e[q]) : 0.0;
-    } else {
-      // two waves' windows: the column in chunks of 16 (registers)
-#pragma unroll
-      for (int q0 = 1; q0 < W; q0 += 16) {
-        double col[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-          if (q0 + u < W) col[u] = f.A[min(c + q0 + u, f.n - 1) * f.ld + c];
-        __builtin_amdgcn_sched_barrier(0);  // the chunk's reads issued before its first use
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-          if (q0 + u < W) e[q0 + u - 1] = c + q0 + u < f.n ? fma(-col[u], xc, e[q0 + u]) : 0.0;
-      }
-    }
-    e[W - 1] = 0.0;
-  }
-  if constexpr (W > 8)
-    if (c < f.n) small_inv_phase<WN>(*reinterpret_cast<double(*)[WN]>(&e[0]), c, f);
-}
-template <int MR>
-__device__ __forceinline__ void small_inverse(double* A, int ld, int n, const double* iy,
-                                              double* al) {
-  SmallInv f{A, ld, n, (int)threadIdx.x, iy, 0.0};
-  double e[MR];
-#pragma unroll
-  for (int q = 0; q < MR; ++q) e[q] = q == f.j ? 1.0 : 0.0;
-  small_inv_phase<MR>(e, 0, f);
-  if (f.j < n) al[f.j] = f.a;  // alpha = X^T z
-}
 
 // The gradient's factorisation for n + 1 <= 64 (one wave): the sweep operator (Goodnight 1979;
 // Gauss-Jordan elimination of a symmetric matrix without pivoting, stable for SPD input) on the
@@ -904,6 +817,116 @@ __device__ __forceinline__ void small_sweep_w_half(const double (&a)[16], int n,
   if (hi == 0 && i < n) wd[i] = wb[i * LDW - 1 + MR - n + i];
 }
 
+// The sweep for 64 < n + 1 <= 128 on the four waves: row r = (wave & 1) 64 + lane, the
+// wave's column half h = wave >> 1 holding slots 64 h .. 64 h + 63 of that row, rotated as in
+// small_sweep_regs (slot q holds column (q + k) mod 128 before step k). One workgroup barrier a
+// step: the h = 0 lanes put their slot 0 (A[r][k]) into the step parity's row buffer, then every
+// lane reads d, A[r][k] and its 64 row entries; the h = 1 lane's old slot 64 becomes the h = 0
+// lane's new slot 63 through the parity's crossing buffer, read after the next step's barrier
+// (double-buffered by step parity: a wave is never more than one step ahead). Every thread of
+// the workgroup calls it. On return slot q holds column (q + n) mod 128, slot 63 included.
+__device__ __forceinline__ void small_sweep4(const double* __restrict__ A, int ld, int n,
+                                             double* buf, double (&a)[64], double* logdet,
+                                             int* bad_out) {
+  using dbl2 = double __attribute__((ext_vector_type(2)));
+  constexpr int MR = 128;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = (wv & 1) * 64 + lane, h = wv >> 1;
+  const int M = n + 1;
+  double* cross = buf + 2 * 520;  // [parity][128]
+  double* wsum = cross + 2 * 128;
+#pragma unroll
+  for (int u = 0; u < 64; ++u) {
+    const int q = h * 64 + u;
+    double v = 0.0;
+    if (r < M && q < M && !(r == n && q == n)) v = q <= r ? A[r * ld + q] : A[q * ld + r];
+    a[u] = v;
+  }
+  double mypiv = 1.0;
+  int bad = 0;
+#pragma unroll 1
+  for (int k = 0; k < n; ++k) {
+    double* B = buf + (k & 1) * 520;
+    double* BS = B + 2 * MR;
+    if (h == 0) {
+      B[r] = a[0];
+      B[r + MR] = a[0];
+      BS[r + 1] = a[0];
+      BS[r + 1 + MR] = a[0];
+    }
+    __syncthreads();
+    if (h == 0 && k > 0) a[63] = cross[((k - 1) & 1) * 128 + r];
+    const int s0 = k + h * 64;  // this half's row entries B[s0 + u], u = 0..63
+    const double* src = (s0 & 1) ? BS + 1 : B;
+    const double d = B[k];
+    const double aik = B[r];
+    double row[16];
+#pragma unroll
+    for (int u = 0; u < 16; u += 2) {
+      const dbl2 v = *reinterpret_cast<const dbl2*>(src + s0 + u);
+      row[u] = v.x;
+      row[u + 1] = v.y;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (!(d > 0.0) && bad == 0) bad = k + 1;
+    const bool piv = r == k;
+    if (piv && h == 0) mypiv = d;
+    double invd = __builtin_amdgcn_rcp(d);
+    invd = fma(invd, fma(-d, invd, 1.0), invd);
+    invd = fma(invd, fma(-d, invd, 1.0), invd);
+    const double g = piv ? -invd : aik * invd;
+    const double keep = piv ? 0.0 : 1.0;
+    // the h = 1 lane's old slot 64: the h = 0 lane's new slot 63
+    if (h == 1) cross[(k & 1) * 128 + r] = fma(-g, row[0], a[0] * keep);
+#pragma unroll
+    for (int q0 = 0; q0 < 64; q0 += 16) {
+      if (q0 > 0) {
+#pragma unroll
+        for (int u = 0; u < 16; u += 2) {
+          const dbl2 v = *reinterpret_cast<const dbl2*>(src + s0 + q0 + u);
+          row[u] = v.x;
+          row[u + 1] = v.y;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        if (q0 + u >= 1) a[q0 + u - 1] = fma(-g, row[u], a[q0 + u] * keep);
+    }
+    a[63] = h ? g : 0.0;  // h = 0: fetched after the next barrier
+  }
+  __syncthreads();
+  if (h == 0) a[63] = cross[((n - 1) & 1) * 128 + r];
+  // logdet = sum_k log d_k: the h = 0 waves' sums, wave 0's then wave 1's
+  double lp = (h == 0 && r < n) ? log(mypiv) : 0.0;
+  for (int o = 32; o > 0; o >>= 1) lp += __shfl_xor(lp, o);
+  if (lane == 0 && h == 0) wsum[wv] = lp;
+  __syncthreads();
+  *logdet = wsum[0] + wsum[1];
+  *bad_out = bad;
+}
+
+// W = alpha alpha^T - Sigma^{-1} from small_sweep4's rows: alpha into al, W's strictly lower
+// part into A (its Sigma is dead since the sweep's loads), diag(W) into wd. Every thread calls it.
+__device__ __forceinline__ void small_sweep4_w(const double (&a)[64], int n, double* A, int ld,
+                                               double* al, double* wd) {
+  constexpr int MR = 128;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = (wv & 1) * 64 + lane, h = wv >> 1;
+  if (h == 0 && r < n) al[r] = a[0];
+  __syncthreads();
+  const double ar = al[min(r, n - 1)];
+#pragma unroll
+  for (int u = 0; u < 64; ++u) {
+    const int j = h * 64 + u - (MR - n);  // the column slot h 64 + u holds (j < 0: none)
+    if (j >= 0 && j <= r && r < n) {
+      const double w = fma(ar, al[j], a[u]);
+      if (j == r) wd[r] = w;
+      else A[r * ld + j] = w;
+    }
+  }
+}
+
 // genes up to which the gradient's grid reduction keeps per-thread, per-gene sums
 constexpr int SMALL_RED_G = 8;
 
@@ -936,16 +959,23 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
       const int ngg = (int)grad_tables_doubles(G, P.T);
       for (int q = tid; q < ngg; q += 256) m.gg[q] = grad_table_entry(h, P.T, P.dt, m.tms, q);
     }
-    double pr, zr;
+    __syncthreads();  // Sigma and r are read by every wave
+    // the four-wave sweep: logdet, the quadratic form, alpha and -Sigma^{-1}; W from its rows
+    double a[64];
+    double logdet;
     int bad;
-    small_factor_regs2<true>(A, ld, n, M, m.colbuf, &pr, &zr, &bad, m.piv, m.iy);
-    const double mll = small_mll_2wave(pr, zr, bad, n, negative, m.red + 4);
+    small_sweep4(A, ld, n, m.colbuf, a, &logdet, &bad);
+    // -r^T Sigma^{-1} r: row n's slot 0 (thread n: the h = 0 threads are rows 0..127)
+    if (tid == n) m.red[2] = -a[0];
+    small_sweep4_w(a, n, A, ld, m.al, m.wd);
     if (tid == 0) {
+      const double two_pi = 6.283185307179586476925;
+      double mll = -0.5 * ((double)n * log(two_pi) + logdet + m.red[2]);
+      mll *= negative ? -1.0 : 1.0;
+      if (bad) mll = __builtin_nan("");
       m.red[0] = mll;
       m.red[1] = (double)bad;
     }
-    // X = L^{-1}: every L store landed before the factor's last barrier
-    if (tid < 128) small_inverse<128>(A, ld, n, m.iy, m.al);
   } else if (wv == 0) {
     // one wave: the sweep (small_sweep_regs) gives the MLL's logdet and quadratic form, alpha
     // and -Sigma^{-1} at once; W is written straight from its rows
@@ -995,18 +1025,8 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
   }
   __syncthreads();
   fit_stamp(m, 2);
-  // two waves: W = alpha alpha^T - S^{-1}, S^{-1}_ic = sum_{k >= i} XT[i][k] XT[c][k] (c <= i)
-  // (one wave: the sweep wrote W already)
+  // (W was written by the sweep: small_sweep_w / _half on one wave, small_sweep4_w on four)
   const int np = n * (n + 1) / 2;
-  for (int q = M > 64 ? tid : np; q < np; q += 256) {
-    int i, c;
-    tri_index(q, &i, &c);
-    double s = 0.0;
-    for (int k = i; k < n; ++k) s = fma(A[i * ld + k], A[c * ld + k], s);
-    const double w = m.al[i] * m.al[c] - s;
-    if (i == c) m.wd[i] = w;
-    else A[i * ld + c] = w;
-  }
   __syncthreads();
   fit_stamp(m, 3);
   double* aw = m.accw + wv * nacc;  // this wave's partial sums: [0,G) D  [G,2G) S  [2G] l
@@ -1184,8 +1204,8 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
 }
 
 // small_value_grad for the fit's step loop, a call of its own: scalar arguments only (the map is
-// rebuilt from the dynamic LDS base), so the register windows of the factor and the inverse are
-// allocated without the loop's state beside them (inlined into the loop they spilled)
+// rebuilt from the dynamic LDS base), so the sweep's register rows are allocated without the
+// loop's state beside them (inlined into the loop they spilled)
 __device__ __noinline__ double small_value_grad_step(int n, int G, int T, double dt,
                                                      int negative, int* bad_out) {
   extern __shared__ __attribute__((aligned(16))) double sm[];

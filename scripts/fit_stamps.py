@@ -1,7 +1,8 @@
 """Per-step phase times of small_fit_kernel's block 0 (problem 0) on the C5 batch, from a
 library built with make EXTRA=-DLFM_FIT_STAMPS=1 (loaded with LFM_LIBRARY=; that build
 overwrites problem 0's first twelve history entries with the phase sums).
-    LFM_LIBRARY=ablibs/fitst/liblfm.so python scripts/fit_stamps.py [iters]"""
+    LFM_LIBRARY=ablibs/fitst/liblfm.so python scripts/fit_stamps.py [iters] [c5|pooled]
+(pooled: configs.notebook_pooled, block 0 = the N = 105 problem on the two-wave path)"""
 import os
 import sys
 import time
@@ -12,7 +13,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from dis_project_amd import _lib, configs, objectives, trainer  # noqa: E402
 
 iters = int(sys.argv[1]) if len(sys.argv) > 1 else 150
-ws = configs.c5_ablations()
+which = sys.argv[2] if len(sys.argv) > 2 else "c5"
+ws = configs.c5_ablations() if which == "c5" else configs.notebook_pooled()
 names = ["(loop top)", "gram (+ tables)", "factor | grad tables", "W (two waves)",
          "tr(W dK) reduction", "gradient out", "Adam + after_epoch + constrain",
          "  (inside phase 2) wave 0: factor done", "  (inside phase 2) wave 0: W written",

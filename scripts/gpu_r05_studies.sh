@@ -49,6 +49,7 @@ for study in "$@"; do
       ;;
     small)
       LFM_LIBRARY=ablibs/fitst/liblfm.so $S fit_stamps 120 python -u scripts/fit_stamps.py 150 || exit $?
+      LFM_LIBRARY=ablibs/fitst/liblfm.so $S fit_stamps_pooled 120 python -u scripts/fit_stamps.py 150 pooled || exit $?
       LFM_LIBRARY=ablibs/stamps/liblfm.so $S small_stamps 120 python -u scripts/small_stamps.py || exit $?
       $S fit_diag 200 python -u scripts/diag_fit.py || exit $?
       $S fit_pooled 200 python -u scripts/fit_pooled_time.py || exit $?
