@@ -35,14 +35,24 @@ struct SmallFactor {
   bool act;
   double* colbuf;
   double dc, y;      // the current column's pivot input and 1 / sqrt of it
-  double mp, mz;     // this lane's pivot and z entry
+  double mp, mz;     // this lane's pivot and z entry (one wave: mp = the pivot input d_r)
+  double inv;        // one wave, LDL^T columns: 1 / dc
+  double q;          // one wave: this row's sum of L[r][c]^2 (lane n: r^T Sigma^{-1} r)
   int bad;
 };
+// 1 / d to the last bit or so: v_rcp_f64 and two Newton steps (the sweep's reciprocal)
+__device__ __forceinline__ double rcp_2nr(double d) {
+  double v = __builtin_amdgcn_rcp(d);
+  v = fma(v, fma(-d, v, 1.0), v);
+  return fma(v, fma(-d, v, 1.0), v);
+}
 // window widths of the phases: 64 48 32 24 16 12 8
 template <int W>
 constexpr int small_next_w() {
   return W == 64 ? 48 : W == 48 ? 32 : W == 32 ? 24 : W == 24 ? 16 : W == 16 ? 12 : 8;
 }
+template <int W>
+__device__ __forceinline__ void small_factor_next(double (&d)[W], int c, SmallFactor& f);
 template <int W>
 __device__ __forceinline__ void small_factor_phase(double (&d)[W], int c, SmallFactor& f) {
   // phase W: the columns while more than the next width of them remain (the last phase: all)
@@ -52,9 +62,8 @@ __device__ __forceinline__ void small_factor_phase(double (&d)[W], int c, SmallF
   for (; c < cend; ++c) {
     if (!(f.dc > 0.0) && f.bad == 0) f.bad = c + 1;
     const double lc = f.r == c ? f.dc * f.y : d[0] * f.y;  // L[r][c]; lane c: the pivot
-    if (f.r == c) f.mp = lc;
-    const double zc = rdl(lc, f.n);  // L[n][c] = z[c]
-    if (f.r == c) f.mz = zc;
+    if (f.r == c) f.mp = f.dc;  // logdet = sum log d_c (L_cc^2 = d_c)
+    f.q = fma(lc, lc, f.q);
     // the next pivot: lane c + 1's d[1] - L[c + 1][c]^2 (past the last column: unused)
     const double dn = rdl(fma(-lc, lc, d[1]), c + 1);
     const double yn = rsqrt_1nr(dn);
@@ -81,12 +90,97 @@ __device__ __forceinline__ void small_factor_phase(double (&d)[W], int c, SmallF
     f.y = yn;
   }
   if constexpr (W > 8)
-    if (c < f.n) small_factor_phase<WN>(*reinterpret_cast<double(*)[WN]>(&d[0]), c, f);
+    if (c < f.n) small_factor_next<WN>(*reinterpret_cast<double(*)[WN]>(&d[0]), c, f);
 }
+#ifndef LFM_SMALL_PIPE
+#define LFM_SMALL_PIPE 1
+#endif
+// Windows of 32 and narrower: LDL^T (Sigma = L D L^T, unit L), software-pipelined by one
+// column. The trailing matrix is the same Schur complement as Cholesky's, so the two meet at a
+// phase boundary; what changes is what goes through LDS: a column's UNSCALED entries u_r (lane r's
+// window d[0]) instead of L[r][c] = u_r / sqrt(d_c). A lane scales its own multiplier,
+// l_r = u_r / d_c, so no reciprocal (square root) of the pivot sits between a column's last
+// update and its store. Column c: l_r, the next column's entry d[1] - l_r u_{c+1} first, stored;
+// column c + 1's reads issued; then the next pivot's reciprocal (v_rcp_f64 and two Newton steps,
+// uniform: lane c + 1's entry by v_readlane) and the rest of column c's multiply-adds, all under
+// that LDS round trip. logdet = sum log d_c; the residual row's sum of u_n^2 / d_c is
+// r^T Sigma^{-1} r (the window does not keep that row's diagonal: it narrows past it).
+// On entry col[q - 1] = u_{c + q} (q = 1 .. W - 1, reads possibly in flight), f.inv = 1 / d_c.
+template <int W>
+__device__ __forceinline__ void small_pipe_col(double (&d)[W], double (&cur)[W - 1],
+                                               double (&nxt)[W - 1], int c, SmallFactor& f) {
+  // column c's reads complete here, before column c + 1's are issued (lgkmcnt counts in order)
+#pragma unroll
+  for (int q = 0; q < W - 1; ++q) asm volatile("" : "+v"(cur[q]));
+  if (!(f.dc > 0.0) && f.bad == 0) f.bad = c + 1;
+  if (f.r == c) f.mp = f.dc;
+  const double l = d[0] * f.inv;             // l_r = u_r / d_c (lanes <= c: dead rows)
+  f.q = fma(l, d[0], f.q);                   // u_r^2 / d_c = L[r][c]^2
+  const double d0 = fma(-l, cur[0], d[1]);   // u_r of column c + 1
+  // (past the last column, c + 1 = n: unused; lanes past n store zeros) one basic block, so
+  // column c's update cannot be moved past column c + 1's head
+  f.colbuf[f.r] = (f.act && f.r > c + 1) ? d0 : 0.0;
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int q = 1; q < W; ++q) nxt[q - 1] = f.colbuf[c + 1 + q];
+  __builtin_amdgcn_sched_barrier(0);  // column c + 1's reads issued before column c's update
+  const double dn = rdl(d0, c + 1);   // d_{c + 1}
+  const double invn = rcp_2nr(dn);
+  d[0] = d0;
+#pragma unroll
+  for (int q = 2; q < W; ++q) d[q - 1] = fma(-l, cur[q - 1], d[q]);
+  d[W - 1] = 0.0;
+  // the update is done here, ahead of column c + 1's wait for its reads
+#pragma unroll
+  for (int q = 0; q < W - 1; ++q) asm volatile("" : "+v"(d[q]));
+  f.dc = dn;
+  f.inv = invn;
+}
+template <int W>
+__device__ __forceinline__ void small_factor_pipe(double (&d)[W], double (&col)[W - 1], int c,
+                                                  SmallFactor& f) {
+  constexpr int WN = small_next_w<W>();
+  const int cend = W > 8 ? max(c, f.n - WN) : f.n;
+  double alt[W - 1];
+  // two columns an iteration, the column buffers alternating (no register copies)
+#pragma unroll 1
+  for (; c + 1 < cend; c += 2) {
+    small_pipe_col<W>(d, col, alt, c, f);
+    small_pipe_col<W>(d, alt, col, c + 1, f);
+  }
+  if (c < cend) {
+    small_pipe_col<W>(d, col, alt, c, f);
+    ++c;
+#pragma unroll
+    for (int q = 0; q < W - 1; ++q) col[q] = alt[q];
+  }
+  if constexpr (W > 8)
+    if (c < f.n)
+      small_factor_pipe<WN>(*reinterpret_cast<double(*)[WN]>(&d[0]),
+                            *reinterpret_cast<double(*)[WN - 1]>(&col[0]), c, f);
+}
+// the phase of window W from column c: LDL^T pipelined for W <= 32 (its first column's entries
+// stored and read back here), Cholesky (small_factor_phase) above
+template <int W>
+__device__ __forceinline__ void small_factor_next(double (&d)[W], int c, SmallFactor& f) {
+  if constexpr (W <= 32 && LFM_SMALL_PIPE) {
+    f.inv = rcp_2nr(f.dc);
+    f.colbuf[f.r] = (f.act && f.r > c) ? d[0] : 0.0;
+    asm volatile("" ::: "memory");
+    double col[W - 1];
+#pragma unroll
+    for (int q = 1; q < W; ++q) col[q - 1] = f.colbuf[c + q];
+    small_factor_pipe<W>(d, col, c, f);
+  } else {
+    small_factor_phase<W>(d, c, f);
+  }
+}
+// Lane r < n ends with d_r (its pivot: logdet = sum log d_r); every lane with the quadratic form
+// r^T Sigma^{-1} r = sum_c L[n][c]^2 (lane n's sum).
 template <int MR>
 __device__ __forceinline__ void small_factor_regs(const double* __restrict__ sm, int ld, int n,
                                                   int M, double* colbuf, double* piv_r,
-                                                  double* z_r, int* bad_out) {
+                                                  double* quad, int* bad_out) {
   SmallFactor f;
   f.n = n;
   f.r = threadIdx.x;  // wave 0
@@ -97,11 +191,11 @@ __device__ __forceinline__ void small_factor_regs(const double* __restrict__ sm,
   for (int q = 0; q < MR; ++q) d[q] = (f.act && q <= f.r && q < n) ? sm[f.r * ld + q] : 0.0;
   f.dc = rdl(d[0], 0);
   f.y = rsqrt_1nr(f.dc);
-  f.mp = f.mz = 0.0;
+  f.mp = f.mz = f.q = 0.0;
   f.bad = 0;
-  small_factor_phase<MR>(d, 0, f);
+  small_factor_next<MR>(d, 0, f);
   *piv_r = f.mp;
-  *z_r = f.mz;
+  *quad = rdl(f.q, n);
   *bad_out = f.bad;
 }
 
@@ -450,30 +544,23 @@ __device__ __forceinline__ void small_body(const SmallProb P, int negative,
     // (256-thread barriers were ~60 % of the kernel at n = 28, two per column)
     if (tid >= 64) return;
     const int r = tid;
-    double pr, zr;
+    double pr, qp;
     int bad;
     colbuf[64 + r] = 0.0;
     if (LFM_SMALL_SKIP == 1 || LFM_SMALL_SKIP == 3) {
       pr = sm[r * ld + r];
-      zr = sm[n * ld + r];
+      qp = sm[n * ld + r];
       bad = 0;
     } else if (M <= 32)
-      small_factor_regs<32>(sm, ld, n, M, colbuf, &pr, &zr, &bad);
+      small_factor_regs<32>(sm, ld, n, M, colbuf, &pr, &qp, &bad);
     else
-      small_factor_regs<64>(sm, ld, n, M, colbuf, &pr, &zr, &bad);
+      small_factor_regs<64>(sm, ld, n, M, colbuf, &pr, &qp, &bad);
     const unsigned long long st3 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
-    double ldp = 0.0, qp = 0.0;
-    if (r < n) {
-      ldp = log(pr);
-      qp = zr * zr;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-      ldp += __shfl_xor(ldp, o);
-      qp += __shfl_xor(qp, o);
-    }
+    double ldp = r < n ? log(pr) : 0.0;
+    for (int o = 32; o > 0; o >>= 1) ldp += __shfl_xor(ldp, o);
     if (r == 0) {
       const double two_pi = 6.283185307179586476925;
-      double mll = -0.5 * ((double)n * log(two_pi) + 2.0 * ldp + qp);
+      double mll = -0.5 * ((double)n * log(two_pi) + ldp + qp);
       mll *= negative ? -1.0 : 1.0;
       if (bad) mll = __builtin_nan("");
       if (LFM_SMALL_STAMPS && blockIdx.x == 0) {

@@ -11,6 +11,8 @@
 # small      the small-kernel phase stamps: fit (ablibs/fitst, -DLFM_FIT_STAMPS=1) and MLL
 #            (ablibs/stamps, -DLFM_SMALL_STAMPS=1) (r05_fit_phase_stamps.txt,
 #            r05_c5_phase_stamps.txt), the fit / host-loop diagnostic, the pooled / C1 fit times
+# pipe       the small factor's pipelined LDL^T columns against ablibs/nopipe (stamps, C5 lines,
+#            the host split of a C5 step) (r05_ab_small_ldl.txt)
 # tests      the batch-gradient tests twice, then the farm / parity / edge / regime tests
 # Every step runs under its own time limit (scripts/gpu_step.sh); the first failure ends the run.
 set -u
@@ -54,6 +56,17 @@ for study in "$@"; do
       $S fit_diag 200 python -u scripts/diag_fit.py || exit $?
       $S fit_pooled 200 python -u scripts/fit_pooled_time.py || exit $?
       $S c5fit 300 python -u bench.py --workload c5fit --steps 20 --warmup 3 || exit $?
+      ;;
+    pipe)
+      # the one-wave factor's pipelined LDL^T columns (LFM_SMALL_PIPE, default) against ablibs/nopipe
+      # (make EXTRA=-DLFM_SMALL_PIPE=0): the MLL kernel's phase stamps, C5 lines interleaved
+      LFM_LIBRARY=ablibs/stamps/liblfm.so $S pipe_stamps 120 python -u scripts/small_stamps.py || exit $?
+      for i in 1 2; do
+        $S pipe_c5_on_$i 300 python -u bench.py --workload c5 --steps 3000 --warmup 300 --no-cpu-baseline || exit $?
+        LFM_LIBRARY=ablibs/nopipe/liblfm.so $S pipe_c5_off_$i 300 python -u bench.py --workload c5 \
+          --steps 3000 --warmup 300 --no-cpu-baseline || exit $?
+      done
+      $S pipe_split 200 python -u scripts/c5_host_split.py 3000 || exit $?
       ;;
     tests)
       $S tests_grad_a 300 python -u -m pytest tests/test_gpu_batch_grad.py $T || exit $?
