@@ -539,6 +539,8 @@ __device__ __forceinline__ void small_body(const SmallProb P, int negative,
   if (tid == 0) red[8] = 0.0;
   __syncthreads();
   const unsigned long long st2 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
+  // the shader clock's count beside the 100 MHz one: the factor's effective clock
+  const unsigned long long ct2 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
   if (M <= 64) {
     // one wave, the augmented matrix in registers (small_factor_regs); no workgroup barrier
     // (256-thread barriers were ~60 % of the kernel at n = 28, two per column)
@@ -556,6 +558,7 @@ __device__ __forceinline__ void small_body(const SmallProb P, int negative,
     else
       small_factor_regs<64>(sm, ld, n, M, colbuf, &pr, &qp, &bad);
     const unsigned long long st3 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memrealtime() : 0;
+    const unsigned long long ct3 = LFM_SMALL_STAMPS ? __builtin_amdgcn_s_memtime() : 0;
     double ldp = r < n ? log(pr) : 0.0;
     for (int o = 32; o > 0; o >>= 1) ldp += __shfl_xor(ldp, o);
     if (r == 0) {
@@ -569,8 +572,9 @@ __device__ __forceinline__ void small_body(const SmallProb P, int negative,
         out[2] = (double)(st2 - st0) * 0.01;
         out[3] = (double)(st3 - st0) * 0.01;
         out[4] = (double)(st4 - st0) * 0.01;
+        out[5] = st3 > st2 ? (double)(ct3 - ct2) / ((double)(st3 - st2) * 0.01) : 0.0;  // MHz
       }
-      if (!LFM_SMALL_STAMPS || blockIdx.x == 0 || blockIdx.x > 4) out[blockIdx.x] = mll;
+      if (!LFM_SMALL_STAMPS || blockIdx.x == 0 || blockIdx.x > 5) out[blockIdx.x] = mll;
       // the status word lands after the result: the host may take it as the problem's
       // completion (lfm_batch_mll_f64)
       __threadfence_system();
