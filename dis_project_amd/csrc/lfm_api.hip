@@ -1367,7 +1367,19 @@ namespace {
 // One launch of the batch's MLL kernel: results to `out` (the pinned buffer, or a device buffer
 // such as the farm's send slots), the status words (reset to -1 here, each written last by its
 // workgroup after a system-scope fence) to the pinned buffer.
+// The previous call on a batch returned on its status words, possibly before its kernel had
+// retired: a fault past that point surfaces at the batch's next call (this query of that launch's
+// completion event, long signalled in the normal case), not at some later synchronise.
+int batch_prev_ok(lfm_ctx* ctx, const lfm_batch* batch) {
+  if (!batch->done) return LFM_OK;
+  const hipError_t e = hipEventQuery(batch->done);
+  if (e != hipSuccess && e != hipErrorNotReady)
+    return hip_fail(ctx, e, "the batch's previous launch");
+  return LFM_OK;
+}
+
 int batch_launch(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative, double* out) {
+  if (int r = batch_prev_ok(ctx, batch)) return r;
   const int64_t np = batch->nprob;
   int* hst = reinterpret_cast<int*>(batch->hbuf + batch->nhyp + np);
   for (int64_t q = 0; q < np; ++q) hst[q] = -1;  // a problem's status word is written last
@@ -1458,6 +1470,7 @@ int lfm_batch_mll_grad_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, in
   const int64_t np = batch->nprob;
   double* hres = batch->hbuf + batch->nhyp;
   int* hst = reinterpret_cast<int*>(hres + np);
+  if (int e = batch_prev_ok(ctx, batch)) return e;
   for (int64_t q = 0; q < np; ++q) hst[q] = -1;
   int r;
   if (batch->use_args) {
