@@ -177,8 +177,9 @@ int lfm_batch_hyp_size(const lfm_batch* batch, int64_t* out);
  * each problem in order, l, obs_stddev, jitter. out[p] per problem (NaN where not PD, with
  * status[p] = LFM_E_NOT_PD; status may be NULL); returns LFM_E_NOT_PD if any problem was.
  * Returns once every problem's result has landed in host memory (the kernel may still be
- * retiring: later work on the ctx's stream is ordered after it, and lfm_batch_destroy drains
- * the device before it frees). */
+ * retiring: later work on the ctx's stream is ordered after it, lfm_batch_destroy waits for the
+ * batch's last launch before it frees, and a fault that launch hits after the return is
+ * reported as LFM_E_HIP by the batch's next value / gradient call). */
 int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative,
                       double* out, int* status);
 /* Value and gradient of every problem's CustomConjMLL(negative).step in ONE launch, one
