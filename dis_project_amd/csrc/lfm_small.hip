@@ -46,6 +46,16 @@ __device__ __forceinline__ double rcp_2nr(double d) {
   v = fma(v, fma(-d, v, 1.0), v);
   return fma(v, fma(-d, v, 1.0), v);
 }
+__device__ __forceinline__ double swap_halves(double v) {
+  // lane i < 32 gets lane i + 32's value and lane i + 32 lane i's (v_permlane32_swap_b32)
+  const long long b = __double_as_longlong(v);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false,
+                                                   false);
+  const bool low = (threadIdx.x & 32) == 0;
+  const unsigned l = low ? lo[1] : lo[0], h = low ? hi[1] : hi[0];
+  return __longlong_as_double(((long long)h << 32) | l);
+}
 // window widths of the phases: 64 48 32 24 16 12 8
 template <int W>
 constexpr int small_next_w() {
@@ -175,6 +185,46 @@ __device__ __forceinline__ void small_factor_next(double (&d)[W], int c, SmallFa
     small_factor_phase<W>(d, c, f);
   }
 }
+#ifndef LFM_SMALL_TWO
+#define LFM_SMALL_TWO 1
+#endif
+// n + 1 <= 32, the columns while more than 16 remain: LDL^T with each row on TWO lanes (lane i
+// slots 0..15 of row i's window, lane i + 32 slots 16..31), so a column's read-back is 16 values
+// a lane instead of up to 31 — the column step is bound by the wave's LDS read rate
+// (r05_ubench_lds_chain.txt). Column c: l = u_i / d_c (u_i: the low lane's slot 0, the high
+// lane gets it by v_permlane32_swap); the low lanes store u_i; each half reads its 16 entries
+// u_{c + 16 hi + k}; slots shift down one with d[q - 1] = d[q] - l u_{c + q}, the high lane's
+// updated slot 16 crossing to the low lane's slot 15. The same arithmetic as the one-lane LDL^T
+// columns. On return the low lanes' 16 slots are the one-lane window of width 16 at column c.
+__device__ __forceinline__ int small_factor_two(double (&a)[16], SmallFactor& f) {
+  const int hi = (int)(threadIdx.x >> 5), i = (int)(threadIdx.x & 31);
+  const bool act = i < f.n + 1;
+  if (hi) f.colbuf[32 + i] = 0.0;  // entries past the rows (the high half reads up to c + 31)
+  int c = 0;
+  f.inv = rcp_2nr(f.dc);
+#pragma unroll 1
+  for (; f.n - c > 16; ++c) {
+    if (!(f.dc > 0.0) && f.bad == 0) f.bad = c + 1;
+    if (hi == 0 && i == c) f.mp = f.dc;
+    const double part = swap_halves(a[0]);
+    const double u = hi ? part : a[0];  // row i's column-c entry
+    const double l = u * f.inv;
+    f.q = fma(l, u, f.q);
+    if (hi == 0) f.colbuf[i] = (act && i > c) ? u : 0.0;
+    asm volatile("" ::: "memory");  // in-order LDS: the reads see every lane's store
+    double col[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) col[k] = f.colbuf[c + 16 * hi + k];
+    __builtin_amdgcn_sched_barrier(0);  // every read issued before the first use
+    const double t = swap_halves(fma(-l, col[0], a[0]));  // the high lane's slot 16, updated
+#pragma unroll
+    for (int k = 1; k < 16; ++k) a[k - 1] = fma(-l, col[k], a[k]);
+    a[15] = hi ? 0.0 : t;
+    f.dc = rdl(a[0], c + 1);  // d_{c + 1}: row c + 1's new slot 0 (a low lane)
+    f.inv = rcp_2nr(f.dc);
+  }
+  return c;
+}
 // Lane r < n ends with d_r (its pivot: logdet = sum log d_r); every lane with the quadratic form
 // r^T Sigma^{-1} r = sum_c L[n][c]^2 (lane n's sum).
 template <int MR>
@@ -186,14 +236,30 @@ __device__ __forceinline__ void small_factor_regs(const double* __restrict__ sm,
   f.r = threadIdx.x;  // wave 0
   f.act = f.r < M;
   f.colbuf = colbuf;
-  double d[MR];
-#pragma unroll
-  for (int q = 0; q < MR; ++q) d[q] = (f.act && q <= f.r && q < n) ? sm[f.r * ld + q] : 0.0;
-  f.dc = rdl(d[0], 0);
-  f.y = rsqrt_1nr(f.dc);
   f.mp = f.mz = f.q = 0.0;
   f.bad = 0;
-  small_factor_next<MR>(d, 0, f);
+  if constexpr (MR == 32 && LFM_SMALL_TWO) {
+    // two lanes a row while more than 16 columns remain, then the one-lane phases from W = 16
+    // (the high lanes are rows past n there: inactive)
+    const int hi = f.r >> 5, i = f.r & 31;
+    double d[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int q = 16 * hi + u;
+      d[u] = (i < M && q <= i && q < n) ? sm[i * ld + q] : 0.0;
+    }
+    f.dc = rdl(d[0], 0);
+    const int c = small_factor_two(d, f);
+    f.y = rsqrt_1nr(f.dc);
+    if (c < n) small_factor_next<16>(d, c, f);
+  } else {
+    double d[MR];
+#pragma unroll
+    for (int q = 0; q < MR; ++q) d[q] = (f.act && q <= f.r && q < n) ? sm[f.r * ld + q] : 0.0;
+    f.dc = rdl(d[0], 0);
+    f.y = rsqrt_1nr(f.dc);
+    small_factor_next<MR>(d, 0, f);
+  }
   *piv_r = f.mp;
   *quad = rdl(f.q, n);
   *bad_out = f.bad;
@@ -813,16 +879,6 @@ __device__ __forceinline__ void small_sweep_w(const double (&a)[MR], int n, doub
 // reads its 16 row entries (16 B a read) and A[i][k], d from the buffer; the high lane also forms
 // the new value of slot 16, which moves to the low lane's slot 15 (v_permlane32_swap), and takes
 // the swept column into slot 31. On return slot q holds column (q + n) mod 32, as before.
-__device__ __forceinline__ double swap_halves(double v) {
-  // lane i < 32 gets lane i + 32's value and lane i + 32 lane i's (v_permlane32_swap_b32)
-  const long long b = __double_as_longlong(v);
-  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)b, (unsigned)b, false, false);
-  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(b >> 32), (unsigned)(b >> 32), false,
-                                                   false);
-  const bool low = (threadIdx.x & 32) == 0;
-  const unsigned l = low ? lo[1] : lo[0], h = low ? hi[1] : hi[0];
-  return __longlong_as_double(((long long)h << 32) | l);
-}
 
 __device__ __forceinline__ void small_sweep_half(const double* __restrict__ A, int ld, int n,
                                                  double* buf, double (&a)[16], double* logdet,
