@@ -423,8 +423,9 @@ __host__ __device__ inline size_t small_map(double* sm, int n, int G, int T, int
 #ifndef LFM_SMALL_SKIP
 #define LFM_SMALL_SKIP 0
 #endif
-// timing experiment (make EXTRA=-DLFM_SMALL_STAMPS=1; results of problems 1-4 invalid): block 0
-// writes its phase times (µs from its start) into out[1..4]
+// timing experiment (make EXTRA=-DLFM_SMALL_STAMPS=1, or 2 for a warm second pass in the args
+// kernel; results of problems 1-5 invalid): block 0
+// writes its phase times (µs from its start) into out[1..4] and the factor's clock (MHz) into out[5]
 #ifndef LFM_SMALL_STAMPS
 #define LFM_SMALL_STAMPS 0
 #endif
@@ -728,6 +729,11 @@ __global__ __launch_bounds__(256) void small_mll_kernel_args(SmallArgs a) {
   P.dsb = a.hyp + a.dsb_off[blockIdx.x];
   P.sc = a.hyp + a.sc_off[blockIdx.x];
   small_body(P, a.negative, a.out, a.status, a.tabs, st0);
+#if LFM_SMALL_STAMPS == 2
+  // a second pass over the same problem, its stamps overwriting the first's: the phases with the
+  // instruction and data caches warm (the same barrier count on every wave: see small_body)
+  small_body(P, a.negative, a.out, a.status, a.tabs, __builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 // ------------------------------------------------ value and gradient (one workgroup)
