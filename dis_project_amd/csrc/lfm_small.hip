@@ -1106,8 +1106,8 @@ __device__ __forceinline__ double small_value_grad(const SmallProb P, const Smal
   __syncthreads();
   fit_stamp(m, 1);
   if (M > 64) {
-    // two waves hold the rows (small_factor_regs2, one barrier a column); the derivative
-    // tables first, by every thread (waves 2 and 3 only keep the factor's barrier count)
+    // every wave takes part in the sweep below (small_sweep4, one barrier a step): the
+    // derivative tables first, by every thread
     if (P.T > 0) {
       const int ngg = (int)grad_tables_doubles(G, P.T);
       for (int q = tid; q < ngg; q += 256) m.gg[q] = grad_table_entry(h, P.T, P.dt, m.tms, q);
