@@ -325,6 +325,12 @@ class Farm:
         slots are all-gathered. Returns every problem's value on every rank."""
         if len(models) != len(datasets):
             raise ValueError("models and datasets must pair up")
+        if self.world == 1 and len(models):
+            # one rank: the whole round is this rank's block (no index lists, no exchange)
+            vals = np.asarray(evaluate(models, datasets), dtype=np.float64).reshape(-1)
+            if vals.size != len(models):
+                raise ValueError("evaluate returned the wrong number of values")
+            return vals.copy()
         return self.run(len(models), lambda idx: evaluate([models[i] for i in idx],
                                                           [datasets[i] for i in idx]))
 
