@@ -1405,12 +1405,30 @@ int batch_launch(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int negative
   return LFM_OK;
 }
 
+// Result words the host is still waiting for: a signalling-NaN payload that no kernel writes
+// (its arithmetic yields values or the canonical quiet NaN; the padding slots are all-ones).
+constexpr uint64_t RESULT_PENDING = 0x7FF41F0DCAFE0001ull;
+void mark_pending(double* p, int64_t count) {
+  uint64_t* w = reinterpret_cast<uint64_t*>(p);
+  for (int64_t q = 0; q < count; ++q) w[q] = RESULT_PENDING;
+}
+bool all_landed(const double* p, int64_t count) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(p);
+  for (int64_t q = 0; q < count; ++q)
+    if (__atomic_load_n(&w[q], __ATOMIC_ACQUIRE) == RESULT_PENDING) return false;
+  return true;
+}
+
 // The host side of a call whose kernel writes results and status words into the batch's
-// pinned buffer: spin on the status words (each written last, after a system-scope fence, by
-// its workgroup; ~µs sooner than the kernel's end-of-dispatch signal behind
-// hipStreamSynchronize); past 20 ms, or while profiling (the events want the stream),
+// pinned buffer: spin until EVERY word the call reads has landed — the status words (-1 before
+// the launch), the results and the gradient (RESULT_PENDING before the launch) — rather than on
+// the status words alone: each word is its own completion flag, so the host never depends on the
+// order in which two posted writes to host memory become visible (the kernel's system-scope fence
+// orders their issue). ~µs sooner than the kernel's end-of-dispatch signal
+// behind hipStreamSynchronize; past 20 ms, or while profiling (the events want the stream),
 // synchronise the stream instead, which also surfaces a kernel fault.
-int batch_wait(lfm_ctx* ctx, int64_t np, const int* hst) {
+int batch_wait(lfm_ctx* ctx, int64_t np, const int* hst, const double* vals, int64_t nv,
+               const double* grads = nullptr, int64_t ng = 0) {
   bool landed = false;
   if (!ctx->prof) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -1418,6 +1436,7 @@ int batch_wait(lfm_ctx* ctx, int64_t np, const int* hst) {
       landed = true;
       for (int64_t q = 0; q < np && landed; ++q)
         landed = __atomic_load_n(&hst[q], __ATOMIC_ACQUIRE) != -1;
+      landed = landed && all_landed(vals, nv) && all_landed(grads, ng);
       if (landed || std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
       __builtin_ia32_pause();
     }
@@ -1449,9 +1468,10 @@ int lfm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, int neg
   DeviceGuard g(ctx->device);
   const int64_t np = batch->nprob;
   double* hres = batch->hbuf + batch->nhyp;
+  mark_pending(hres, np);
   int r = batch_launch(ctx, batch, hyp, negative, hres);
   if (r) return r;
-  r = batch_wait(ctx, np, reinterpret_cast<const int*>(hres + np));
+  r = batch_wait(ctx, np, reinterpret_cast<const int*>(hres + np), hres, np);
   if (r) return r;
   std::memcpy(out, hres, (size_t)np * 8);
   return batch_status(ctx, batch, status);
@@ -1472,6 +1492,8 @@ int lfm_batch_mll_grad_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, in
   int* hst = reinterpret_cast<int*>(hres + np);
   if (int e = batch_prev_ok(ctx, batch)) return e;
   for (int64_t q = 0; q < np; ++q) hst[q] = -1;
+  mark_pending(hres, np);
+  mark_pending(batch->hgrad, batch->nhyp);
   int r;
   if (batch->use_args) {
     SmallArgs a;
@@ -1489,7 +1511,7 @@ int lfm_batch_mll_grad_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, in
   }
   if (r) return r;
   hipEventRecord(batch->done, ctx->stream);
-  r = batch_wait(ctx, np, hst);
+  r = batch_wait(ctx, np, hst, hres, np, batch->hgrad, batch->nhyp);
   if (r) return r;
   int worst = LFM_OK;
   std::memcpy(grad, batch->hgrad, (size_t)batch->nhyp * 8);
@@ -1516,6 +1538,7 @@ int lfm_batch_fit_f64(lfm_ctx* ctx, lfm_batch* batch, const lfm_adam* opt, int n
                                    "within 160 KB of LDS");
   if (nsteps == 0) return LFM_OK;
   DeviceGuard g(ctx->device);
+  if (int e = batch_prev_ok(ctx, batch)) return e;
   const int64_t np = batch->nprob, nh = batch->nhyp;
   const size_t b_par = 3 * (size_t)nh * 8, b_bias = 2 * (size_t)nsteps * 8;
   const size_t b_hist = (size_t)nsteps * np * 8, b_st = (size_t)np * sizeof(int);
@@ -1989,6 +2012,7 @@ int farm_gather_publish(lfm_ctx* ctx, int64_t slots, double* recv) {
     return r;
   }
   const unsigned seq = ++ctx->farm_seq;
+  mark_pending(ctx->farm_pub, count);
   hipLaunchKernelGGL(farm_publish_kernel, dim3(1), dim3(64), 0, ctx->stream, drecv, count,
                      ctx->farm_pub, seq_word, seq);
   hipError_t e = hipGetLastError();
@@ -2009,16 +2033,19 @@ int farm_wait(lfm_ctx* ctx, const unsigned* seq_word, unsigned seq, int64_t coun
   const double end = mono_s() + rccl_timeout_s(ctx);
   const Backoff bo;
   const auto t_spin = std::chrono::steady_clock::now() + std::chrono::milliseconds(2);
-  while (__atomic_load_n(seq_word, __ATOMIC_ACQUIRE) != seq &&
-         std::chrono::steady_clock::now() < t_spin)
-    __builtin_ia32_pause();
-  while (__atomic_load_n(seq_word, __ATOMIC_ACQUIRE) != seq) {
+  // published: the sequence word AND every slot (each marked RESULT_PENDING before the round;
+  // no reliance on the order in which the slots' and the word's writes reach host memory)
+  auto published = [&] {
+    return __atomic_load_n(seq_word, __ATOMIC_ACQUIRE) == seq && all_landed(ctx->farm_pub, count);
+  };
+  while (!published() && std::chrono::steady_clock::now() < t_spin) __builtin_ia32_pause();
+  while (!published()) {
     e = hipStreamQuery(ctx->stream);
     if (e != hipSuccess && e != hipErrorNotReady) {
       rccl_drop(ctx);
       return hip_fail(ctx, e, "farm round");
     }
-    if (e == hipSuccess && __atomic_load_n(seq_word, __ATOMIC_ACQUIRE) != seq) {
+    if (e == hipSuccess && !published()) {
       rccl_drop(ctx);
       return set_err(ctx, LFM_E_HIP, "farm round: the stream drained without publishing");
     }
@@ -2132,6 +2159,7 @@ int lfm_farm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, in
       int* hst = reinterpret_cast<int*>(batch->hbuf + batch->nhyp + np);
       for (int64_t q = 0; q < np; ++q) hst[q] = -1;
       unsigned* seq_word = reinterpret_cast<unsigned*>(ctx->farm_pub + count);
+      mark_pending(ctx->farm_pub, count);
       __atomic_store_n(seq_word, 0u, __ATOMIC_RELEASE);
       hipError_t e = hipGraphLaunch(ctx->farm_exec, ctx->stream);
       if (e != hipSuccess) {
@@ -2145,9 +2173,11 @@ int lfm_farm_batch_mll_f64(lfm_ctx* ctx, lfm_batch* batch, const double* hyp, in
     }
   }
   // this rank's padding slots: NaN (all-ones bytes), then the kernel writes its nprob slots
-  if (slots > batch->nprob)
-    hipMemsetAsync(ctx->farm_buf + batch->nprob, 0xFF, (size_t)(slots - batch->nprob) * 8,
-                   ctx->stream);
+  if (slots > batch->nprob) {
+    const hipError_t e = hipMemsetAsync(ctx->farm_buf + batch->nprob, 0xFF,
+                                        (size_t)(slots - batch->nprob) * 8, ctx->stream);
+    if (e != hipSuccess) return hip_fail(ctx, e, "farm round: padding slots");
+  }
   r = batch_launch(ctx, batch, hyp, negative, ctx->farm_buf);
   if (r) return r;
   r = farm_gather_publish(ctx, slots, recv);
@@ -2163,8 +2193,11 @@ int lfm_farm_allgather_f64(lfm_ctx* ctx, const double* send, int64_t count, doub
   int rs = farm_drain_stale(ctx);
   if (rs) return rs;
   const size_t in = (size_t)count * 8, out = in * ctx->nranks;
+  const double* before = ctx->farm_buf;
   int r = ensure(ctx, (void**)&ctx->farm_buf, &ctx->farm_bytes, in + out);
   if (r) return r;
+  // the captured farm round holds the old device buffer's addresses: forget it
+  if (ctx->farm_buf != before) farm_graph_reset(ctx);
   // host side through a pinned buffer of the farm's own: every copy is truly asynchronous (a
   // copy into pageable memory would block past the deadline below), and a copy a timed-out call
   // leaves queued can only ever write into this buffer — never the caller's, never the staging

@@ -270,7 +270,8 @@ struct SmallArgs {
   double* grad;  // small_grad_kernel_args: the gradient, packed as hyp
 };
 static_assert(sizeof(SmallArgs) <= 4096, "kernel argument block");
-// value and gradient of a batch of small problems (n <= 63): a = the kernel-argument form
+// value and gradient of a batch of small problems (n <= SMALL_GRAD_MAX = 127; the launch's LDS
+// map within 160 KB): a = the kernel-argument form
 // (problem table and hyperparameters in the arguments) or NULL (d_probs, d_offs: the table and
 // each problem's offsets of its vectors [0, nprob) and scalars [nprob, 2 nprob) in the packed
 // layout, hyperparameters read through SmallProb::dsb / sc)

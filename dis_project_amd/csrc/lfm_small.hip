@@ -56,6 +56,18 @@ __device__ __forceinline__ double swap_halves(double v) {
   const unsigned l = low ? lo[1] : lo[0], h = low ? hi[1] : hi[0];
   return __longlong_as_double(((long long)h << 32) | l);
 }
+// An LDS hand-off between the lanes of ONE wave (the form of HIP's __syncwarp): a release and an
+// acquire fence at wavefront scope around a wave barrier. Every lane's LDS stores before it are
+// ordered before every lane's LDS reads after it, and every read before it before every store
+// after it (the next step's overwrite of a buffer the other lanes were reading). On gfx950 both
+// fences are empty (a wave's LDS operations are performed in issue order) and the wave barrier
+// only fences code motion, so the ISA is unchanged; what it adds over a bare compiler fence is the
+// language-level ordering the reads rely on.
+__device__ __forceinline__ void wave_lds_handoff() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 // window widths of the phases: 64 48 32 24 16 12 8
 template <int W>
 constexpr int small_next_w() {
@@ -77,9 +89,9 @@ __device__ __forceinline__ void small_factor_phase(double (&d)[W], int c, SmallF
     // the next pivot: lane c + 1's d[1] - L[c + 1][c]^2 (past the last column: unused)
     const double dn = rdl(fma(-lc, lc, d[1]), c + 1);
     const double yn = rsqrt_1nr(dn);
+    wave_lds_handoff();  // the previous column's reads of colbuf before this column's stores
     f.colbuf[f.r] = (f.act && f.r > c) ? lc : 0.0;
-    // the wave's LDS operations complete in order: the reads see every lane's store
-    asm volatile("" ::: "memory");
+    wave_lds_handoff();  // every lane's store before the reads
     // the column comes back in chunks of at most 32, every read of a chunk issued before its
     // first use (sched_barrier: the scheduler would otherwise sink the reads to their uses and
     // expose the LDS latency two or three reads at a time)
@@ -129,8 +141,9 @@ __device__ __forceinline__ void small_pipe_col(double (&d)[W], double (&cur)[W -
   const double d0 = fma(-l, cur[0], d[1]);   // u_r of column c + 1
   // (past the last column, c + 1 = n: unused; lanes past n store zeros) one basic block, so
   // column c's update cannot be moved past column c + 1's head
+  wave_lds_handoff();  // column c's reads (completed above) before column c + 1's stores
   f.colbuf[f.r] = (f.act && f.r > c + 1) ? d0 : 0.0;
-  asm volatile("" ::: "memory");
+  wave_lds_handoff();  // every lane's store before column c + 1's reads
 #pragma unroll
   for (int q = 1; q < W; ++q) nxt[q - 1] = f.colbuf[c + 1 + q];
   __builtin_amdgcn_sched_barrier(0);  // column c + 1's reads issued before column c's update
@@ -175,8 +188,9 @@ template <int W>
 __device__ __forceinline__ void small_factor_next(double (&d)[W], int c, SmallFactor& f) {
   if constexpr (W <= 32 && LFM_SMALL_PIPE) {
     f.inv = rcp_2nr(f.dc);
+    wave_lds_handoff();  // the previous phase's reads of colbuf before these stores
     f.colbuf[f.r] = (f.act && f.r > c) ? d[0] : 0.0;
-    asm volatile("" ::: "memory");
+    wave_lds_handoff();
     double col[W - 1];
 #pragma unroll
     for (int q = 1; q < W; ++q) col[q - 1] = f.colbuf[c + q];
@@ -210,8 +224,9 @@ __device__ __forceinline__ int small_factor_two(double (&a)[16], SmallFactor& f)
     const double u = hi ? part : a[0];  // row i's column-c entry
     const double l = u * f.inv;
     f.q = fma(l, u, f.q);
+    wave_lds_handoff();  // the previous column's reads before this column's stores
     if (hi == 0) f.colbuf[i] = (act && i > c) ? u : 0.0;
-    asm volatile("" ::: "memory");  // in-order LDS: the reads see every lane's store
+    wave_lds_handoff();  // every lane's store before the reads
     double col[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) col[k] = f.colbuf[c + 16 * hi + k];
@@ -795,14 +810,14 @@ __device__ __forceinline__ void small_sweep_regs(const double* __restrict__ A, i
   asm volatile("" ::: "memory");  // the rows are loaded before the buffers are written
 #pragma unroll 1
   for (int k = 0; k < n; ++k) {
+    wave_lds_handoff();  // step k - 1's reads of the row buffers before step k's stores
     if (i < MR) {
       buf[i] = a[0];
       buf[i + MR] = a[0];
       bufS[i + 1] = a[0];
       bufS[i + 1 + MR] = a[0];
     }
-    // the wave's LDS operations complete in order: the reads see every lane's store
-    asm volatile("" ::: "memory");
+    wave_lds_handoff();  // every lane's stores before the row's reads
     // row k from its pivot on: r[u] = buf[k + u] (r[0] = d), 16 B a read from buf when k is
     // even, else from bufS (buf shifted by one); the pivot's read is the oldest, so its
     // arithmetic starts while the rest of the row is in flight
@@ -860,11 +875,12 @@ __device__ __forceinline__ void small_sweep_w(const double (&a)[MR], int n, doub
   const int i = threadIdx.x;  // wave 0
   // alpha at alS[MR - n + j] (slot q of every row holds column j = q - (MR - n)), so that
   // every read and store below has a compile-time offset; alpha also into al
+  wave_lds_handoff();  // the sweep's last reads of its row buffers (alS) before these stores
   if (i < n) {
     al[i] = a[0];
     alS[MR - n + i] = a[0];
   }
-  asm volatile("" ::: "memory");  // alpha in LDS before it is read back (in order)
+  wave_lds_handoff();  // alpha in LDS before every lane reads it back
   double alj[MR];
 #pragma unroll
   for (int q = 1; q < MR; ++q) alj[q] = alS[q];
@@ -875,7 +891,7 @@ __device__ __forceinline__ void small_sweep_w(const double (&a)[MR], int n, doub
   double* row = wb + min(i, n) * LDW - 1;
 #pragma unroll
   for (int q = 1; q < MR; ++q) row[q] = fma(ai, alj[q], a[q]);
-  asm volatile("" ::: "memory");  // the row stored before its diagonal is read back
+  wave_lds_handoff();  // the rows stored before the diagonal is read back
   if (i < n) wd[i] = row[MR - n + i];
 }
 
@@ -907,13 +923,14 @@ __device__ __forceinline__ void small_sweep_half(const double* __restrict__ A, i
   asm volatile("" ::: "memory");  // the rows are loaded before the buffers are written
 #pragma unroll 1
   for (int k = 0; k < n; ++k) {
+    wave_lds_handoff();  // step k - 1's reads of the row buffers before step k's stores
     if (hi == 0) {
       buf[i] = a[0];
       buf[i + MR] = a[0];
       bufS[i + 1] = a[0];
       bufS[i + 1 + MR] = a[0];
     }
-    asm volatile("" ::: "memory");  // in-order LDS: the reads see every lane's store
+    wave_lds_handoff();  // every lane's stores before the row's reads
     const int s0 = k + hi * 16;  // this half's row entries buf[s0 + u], u = 0..15
     const double* src = (s0 & 1) ? bufS + 1 : buf;
     const double d = buf[k];
@@ -952,11 +969,12 @@ __device__ __forceinline__ void small_sweep_w_half(const double (&a)[16], int n,
   constexpr int MR = 32, LDW = MR | 1;
   const int lane = threadIdx.x;
   const int i = lane & 31, hi = lane >> 5;
+  wave_lds_handoff();  // the sweep's last reads of its row buffers (alS) before these stores
   if (hi == 0 && i < n) {
     al[i] = a[0];
     alS[MR - n + i] = a[0];
   }
-  asm volatile("" ::: "memory");  // alpha in LDS before it is read back (in order)
+  wave_lds_handoff();  // alpha in LDS before every lane reads it back
   const double ai = al[min(i, max(n - 1, 0))];
   double alj[16];
 #pragma unroll
@@ -966,7 +984,7 @@ __device__ __forceinline__ void small_sweep_w_half(const double (&a)[16], int n,
 #pragma unroll
   for (int u = 0; u < 16; ++u)
     if (hi || u > 0) row[u] = fma(ai, alj[u], a[u]);
-  asm volatile("" ::: "memory");  // both halves' stores before the diagonal is read back
+  wave_lds_handoff();  // both halves' stores before the diagonal is read back
   if (hi == 0 && i < n) wd[i] = wb[i * LDW - 1 + MR - n + i];
 }
 
@@ -1422,7 +1440,7 @@ __global__ __launch_bounds__(256) void small_grad_kernel_args(SmallArgs a) {
 //   value and gradient (small_value_grad), history[s] = the value
 //   chain rule: g_raw = g softplus'(raw) = g sigmoid(raw); l: g 3 sigmoid (1 - sigmoid)
 //   optax.adam: mu = b1 mu + (1 - b1) g, nu = b2 nu + (1 - b2) g^2,
-//               raw += -lr (mu / c1) / (sqrt(nu / c2 + eps_root) + eps)
+//               raw += -lr ((mu / c1) / (sqrt(nu / c2 + eps_root) + eps))  (optax's order)
 //     with c1 = 1 - b1^count, c2 = 1 - b2^count from the host (bias[2 s], bias[2 s + 1]: the
 //     host's pow, as the restatement's)
 //   after_epoch (trainer.py:133-160, 205-210): every num_steps_per_epoch steps (step 0
@@ -1487,24 +1505,29 @@ __global__ __launch_bounds__(256) void small_fit_kernel(FitArgs a) {
     if (bad && !first_bad) first_bad = (int)s + 1;
     if (tid == 0) a.history[s * a.nprob + b] = v;
     // the update, after_epoch on the unconstrained leaves, and the next step's constrained model,
-    // each parameter by its own thread (one barrier a step)
-    if (tid < nh - 1) {
-      const double x = m.raw[tid], g = m.gout[tid];
+    // each parameter by its own thread (one barrier a step; 3G + 2 > 256 parameters, G >= 85,
+    // take a second pass)
+    const double c1 = a.bias[2 * s], c2 = a.bias[2 * s + 1];
+    const bool epoch = a.fix && (a.step0 + s) % a.spe == 0 && G > 3;
+    for (int i = tid; i < nh - 1; i += 256) {
+      const double x = m.raw[i], g = m.gout[i];
       const double sg = sigmoid_d(x);
-      const double gr = tid == 3 * G ? g * 3.0 * sg * (1.0 - sg) : g * sg;
-      const double c1 = a.bias[2 * s], c2 = a.bias[2 * s + 1];
-      const double mu = a.b1 * m.mu[tid] + (1.0 - a.b1) * gr;
-      const double nu = a.b2 * m.nu[tid] + (1.0 - a.b2) * (gr * gr);
-      const double upd = -a.lr * (mu / c1) / (sqrt(nu / c2 + a.eps_root) + a.eps);
-      m.mu[tid] = mu;
-      m.nu[tid] = nu;
+      const double gr = i == 3 * G ? g * 3.0 * sg * (1.0 - sg) : g * sg;
+      const double mu = a.b1 * m.mu[i] + (1.0 - a.b1) * gr;
+      const double nu = a.b2 * m.nu[i] + (1.0 - a.b2) * (gr * gr);
+      // optax's order: scale_by_adam's mu_hat / (sqrt(nu_hat + eps_root) + eps), then
+      // scale(-learning_rate)
+      const double u = (mu / c1) / (sqrt(nu / c2 + a.eps_root) + a.eps);
+      const double upd = -a.lr * u;
+      m.mu[i] = mu;
+      m.nu[i] = nu;
       double xn = x + upd;
-      if (a.fix && (a.step0 + s) % a.spe == 0 && G > 3) {
-        if (tid == G + 3) xn = 1.0;  // true_s[3]
-        if (tid == 3) xn = 0.8;      // true_d[3]
+      if (epoch) {
+        if (i == G + 3) xn = 1.0;  // true_s[3]
+        if (i == 3) xn = 0.8;      // true_d[3]
       }
-      m.raw[tid] = xn;
-      m.hyp[tid] = constrain(tid, xn);
+      m.raw[i] = xn;
+      m.hyp[i] = constrain(i, xn);
     }
     __syncthreads();
     fit_stamp(m, 6);

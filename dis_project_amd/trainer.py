@@ -114,8 +114,10 @@ class adam:  # noqa: N801 — optax.adam(learning_rate) spelling
               for k, g in grads.items()}
         c1 = 1 - self.b1**count
         c2 = 1 - self.b2**count
-        upd = {k: -self.learning_rate * (mu[k] / c1) / (np.sqrt(nu[k] / c2 + self.eps_root)
-                                                         + self.eps) for k in grads}
+        # optax's order: scale_by_adam's mu_hat / (sqrt(nu_hat + eps_root) + eps), then
+        # scale(-learning_rate) multiplies
+        upd = {k: -self.learning_rate * ((mu[k] / c1) / (np.sqrt(nu[k] / c2 + self.eps_root)
+                                                          + self.eps)) for k in grads}
         return upd, AdamState(count, mu, nu)
 
 

@@ -597,7 +597,7 @@ int lfm_cpu_fit(const double* x, const double* y, int64_t n, int64_t G, double* 
       const double gr = i == 3 * G ? g[i] * 3.0 * sg * (1.0 - sg) : g[i] * sg;
       mu[i] = b1 * mu[i] + (1.0 - b1) * gr;
       nu[i] = b2 * nu[i] + (1.0 - b2) * (gr * gr);
-      raw[i] = raw[i] + -lr * (mu[i] / c1) / (std::sqrt(nu[i] / c2 + eps_root) + eps);
+      raw[i] = raw[i] + -lr * ((mu[i] / c1) / (std::sqrt(nu[i] / c2 + eps_root) + eps));  // optax's order
     }
     if (fix && s % spe == 0 && G > 3) {
       raw[G + 3] = 1.0;

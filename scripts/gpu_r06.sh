@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round 6's GPU steps, one named study per argument (each step under its own time limit via
+# scripts/gpu_step.sh; the first failing step ends the call — never retried):
+#   tests    the whole -m gpu suite, then smoke()
+#   handoff  the small kernels before / after the wave hand-off hardening (ablibs/r05 = round 5's
+#            library), c5 and c5fit bench lines interleaved, two rounds
+#   c2 c3 c5 c5fit   one bench line each (the default step counts of the round's profile set)
+set -u
+export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+S=scripts/gpu_step.sh
+for study in "$@"; do
+  case $study in
+    tests)
+      $S r06_tests 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread || exit $?
+      $S r06_smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit $?
+      ;;
+    handoff)
+      for r in 1 2; do
+        for lib in ablibs/r05/liblfm.so dis_project_amd/liblfm.so; do
+          tag=$(basename "$(dirname "$lib")")
+          LFM_LIBRARY=$lib $S r06_handoff_c5_${tag}_$r 120 python -u bench.py --workload c5 --steps 3000 --warmup 300 --no-cpu-baseline || exit $?
+          LFM_LIBRARY=$lib $S r06_handoff_c5fit_${tag}_$r 120 python -u bench.py --workload c5fit --steps 30 --warmup 3 --no-cpu-baseline || exit $?
+        done
+      done
+      ;;
+    c2) $S r06_bench_c2 300 python -u bench.py --workload c2 --steps 20 --warmup 3 || exit $? ;;
+    c3) $S r06_bench_c3 400 python -u bench.py --workload c3 --steps 5 --warmup 1 --no-cpu-baseline || exit $? ;;
+    c5) $S r06_bench_c5 300 python -u bench.py --workload c5 --steps 3000 --warmup 300 || exit $? ;;
+    c5fit) $S r06_bench_c5fit 300 python -u bench.py --workload c5fit --steps 30 --warmup 3 || exit $? ;;
+    *) echo "unknown study $study"; exit 2 ;;
+  esac
+done
+echo done

@@ -517,6 +517,13 @@ def test_device_farm_round_one_rank(monkeypatch, graph):
             finally:
                 ev2.close()
             np.testing.assert_array_equal(ev.farm_round(models, 15), want)
+            # a host-path all-gather larger than the round's buffers reallocates them: the next
+            # round must not replay a graph holding the freed addresses
+            big = np.arange(4096, dtype=np.float64)
+            np.testing.assert_array_equal(g(big), big)
+            moved = [m.replace(l=m.l * 1.3) for m in models]
+            np.testing.assert_array_equal(ev.farm_round(moved, 15), ev(moved))
+            np.testing.assert_array_equal(ev.farm_round(models, 15), want)
         finally:
             ev.close()
             g.close()
