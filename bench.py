@@ -22,12 +22,16 @@ stopped). Workloads; the default is c2 on one GPU and c3 on s
   c4  configs[3]: a step = one fp32 lower-triangle gram fill at N = 65536 (256 genes x 256
       timepoints, 8.6 GB written) into a 17.2 GB device buffer; the HBM roofline of the fill.
       One GPU (replicas at N > 1: every rank fills its own; weak scaling).
-  c5  configs[4]: a step = the 15 replicate x leave-one-gene-out problems (N = 28), each
-      rank's share in one batched launch, then the all-gather. Strong scaling.
+  c5  configs[4]: a step = the 15 replicate x leave-one-gene-out problems (N = 28) at --rounds
+      R hyperparameter rounds per rank (default 1 on one GPU: configs[4]'s own step; 16 on
+      several), each rank's R x 15 in one batched launch, then one all-gather. Weak scaling
+      over rounds (a round is one hyperparameter set of each of the 15 problems).
   c5fit  configs[4]'s actual workflow (notebook.py:55-75): a step = JaxTrainer.fit of the 15
       problems, 150 steps of adam(0.01) on CustomConjMLL(negative=True) each, in ONE launch
       (lfm_batch_fit_f64: every problem's value_and_grad + Adam loop inside one workgroup).
-      value = problem training steps / s (15 x 150 per step). One GPU (replicas at N > 1).
+      value = problem training steps / s (15 x 150 per step). Several GPUs: the 15 fits
+      partitioned (farm.partition), one all-gather of their final raw parameters and loss
+      histories (trainer.FarmTrainer's exchange). Strong scaling.
 torch.distributed (gloo, CPU) is only the control plane: barrier, max-over-ranks timing and
 shipping the RCCL unique id.
 
@@ -79,6 +83,9 @@ FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix, AMD spec (not in the 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 METRIC = "log-marginal-likelihood evals/sec + fp64 Cholesky GFLOP/s at N=16384"
 PARITY_RTOL = 1e-9             # GPU vs C++ CPU restatement (north_star: 1e-5)
+# c5 at W > 1: hyperparameter rounds of the 15 problems per rank per step (240 workgroups: one
+# per CU, one launch and one exchange per step)
+C5_ROUNDS_MULTI = 16
 EPS64 = np.finfo(np.float64).eps
 
 
@@ -96,6 +103,10 @@ def parse(argv=None):
                    help="c3: evaluations in flight per GPU (farm.ConcurrentEvaluator, schedule-1 "
                         "worker contexts); 1 = one schedule-3 context, one evaluation at a time; "
                         "0 (default) = farm.choose_workers for the rank's share")
+    p.add_argument("--rounds", type=int, default=0,
+                   help="c5: hyperparameter rounds of the 15 problems per rank per step (weak "
+                        "scaling over rounds, one launch and one exchange per step); 0 (default) "
+                        "= 1 on one GPU (configs[4]'s step), 16 on several")
     p.add_argument("--fit-iters", type=int, default=150,
                    help="c5fit: Adam steps per fit (notebook.py:64 / main.py:54: 150)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -119,6 +130,8 @@ def parse(argv=None):
         a.workload = "c2" if a.gpus == 1 else "c3"
     if a.genes is None:
         a.genes = 256 if a.workload == "c4" else 64
+    if a.rounds <= 0:
+        a.rounds = 1 if a.gpus == 1 else C5_ROUNDS_MULTI
     return a
 
 
@@ -364,16 +377,42 @@ def cpu_baseline_c5(models, datasets, gpu_values, min_seconds=2.0):
     t = time.perf_counter() - t0
     ref = np.asarray(vals)
     rel = np.abs(ref - np.asarray(gpu_values)) / np.abs(ref)
+    # the same problems across the allowed cores: one problem per OpenMP thread at a time
+    # (oracle/lfm_cpu.cpp lfm_cpu_mll_batch), many rounds in one parallel loop
+    thr = len(os.sched_getaffinity(0))
+    genes = [m.num_genes for m in models]
+    hyp = np.concatenate([np.concatenate([m.true_d, m.true_s, m.true_b]) for m in models] +
+                         [np.array([[m.l, m.obs_stddev, m.jitter] for m in models]).reshape(-1)])
+    xs, ys = [d.X for d in datasets], [d.y for d in datasets]
+    reps, tt = 64, 0.0
+    while True:
+        t1 = time.perf_counter()
+        got = lfm_cpu.mll_batch(xs, ys, genes, hyp, threads=thr, reps=reps)
+        tt = time.perf_counter() - t1
+        if tt >= min_seconds or reps >= 1 << 24:
+            break
+        reps *= max(2, min(16, int(min_seconds / max(tt, 1e-3)) + 1))
+    if not np.array_equal(got, ref):
+        raise SystemExit("the threaded CPU baseline disagrees with the sequential one")
     return {
         "value": rounds * len(models) / t,
         "unit": "MLL evals/s",
         "cores": 1,
         "kind": "port",
         "sample": (f"oracle/lfm_cpu.cpp: the {len(models)} problems (N={datasets[0].n}) "
-                   f"sequentially on 1 thread, {rounds} full rounds in {t:.2f} s; "
+                   f"sequentially on ONE core, {rounds} full rounds in {t:.2f} s; "
                    "timed in full, not extrapolated"),
         "host_cpus": os.cpu_count(),
         "gpu_vs_cpu_rel": float(rel.max()),
+        "threads": {
+            "value": reps * len(models) / tt,
+            "unit": "MLL evals/s",
+            "cores": thr,
+            "sample": (f"oracle/lfm_cpu.cpp lfm_cpu_mll_batch: {reps} rounds of the "
+                       f"{len(models)} problems in one OpenMP loop, one problem per thread at a "
+                       f"time on {thr} threads (this process's CPU affinity of {os.cpu_count()} "
+                       f"host CPUs), {tt:.2f} s"),
+        },
     }
 
 
@@ -405,16 +444,44 @@ def cpu_baseline_c5fit(models, datasets, raw0, iters, gpu_final, min_seconds=2.0
     ref = np.asarray(finals)
     rel = np.abs(ref - np.asarray(gpu_final)) / np.abs(ref)
     per_step = len(models) * iters
+    # the same fits across the allowed cores: one problem per OpenMP thread at a time
+    # (lfm_cpu_fit_batch), repeated until min_seconds have passed
+    thr = len(os.sched_getaffinity(0))
+    xs, ys = [d.X for d in datasets], [d.y for d in datasets]
+    r0 = []
+    off = 0
+    for p, G in enumerate(genes):
+        r0.append(np.concatenate([raw0[off:off + 3 * G], raw0[nvec + 3 * p: nvec + 3 * p + 3]]))
+        off += 3 * G
+    trounds, t1 = 0, time.perf_counter()
+    while True:
+        hist, _ = lfm_cpu.fit_batch(xs, ys, genes, [r.copy() for r in r0], iters, lr=0.01,
+                                    spe=1000, fix=False, negative=True, threads=thr)
+        trounds += 1
+        if time.perf_counter() - t1 >= min_seconds:
+            break
+    tt = time.perf_counter() - t1
+    if not np.array_equal(hist[:, -1], ref):
+        raise SystemExit("the threaded CPU fit disagrees with the sequential one")
     return {
         "value": rounds * per_step / t,
         "unit": "problem training steps/s",
         "cores": 1,
         "kind": "port",
         "sample": (f"oracle/lfm_cpu.cpp fit: the {len(models)} problems (N={datasets[0].n}) x "
-                   f"{iters} Adam steps sequentially on 1 thread, {rounds} full fits in "
+                   f"{iters} Adam steps sequentially on ONE core, {rounds} full fits in "
                    f"{t:.2f} s ({t / rounds * 1e3:.0f} ms per fit); timed in full"),
         "host_cpus": os.cpu_count(),
         "gpu_vs_cpu_rel": float(rel.max()),
+        "threads": {
+            "value": trounds * per_step / tt,
+            "unit": "problem training steps/s",
+            "cores": thr,
+            "sample": (f"oracle/lfm_cpu.cpp lfm_cpu_fit_batch: the {len(models)} fits in one "
+                       f"OpenMP loop, one problem per thread at a time on {thr} threads (this "
+                       f"process's CPU affinity of {os.cpu_count()} host CPUs; at most "
+                       f"{len(models)} busy), {trounds} rounds in {tt:.2f} s"),
+        },
     }
 
 
@@ -601,43 +668,84 @@ def main(argv=None):
 
         models, datasets = farm.workload("c5")
         n = datasets[0].n
-        fit_ev = farm.BatchEvaluator(ctx, datasets, negative=True)
-        close = fit_ev.close
-        batch = fit_ev.registered([m.num_genes for m in models])
-        raw0 = TR.pack_raw([TR.unconstrain(m) for m in models], [m.jitter for m in models])
+        P = len(models)
+        genes = [m.num_genes for m in models]
+        gmax = max(genes)
+        # the fits farmed: rank r fits its static block (farm.partition) in one launch, then
+        # one all-gather of every fit's final raw parameters and loss history
+        # (Farm.run_records; trainer.FarmTrainer); one rank: the whole batch, no exchange
+        mine = farm.partition(P, world, rank)
+        my_models = [models[i] for i in mine]
+        raw0 = TR.pack_raw([TR.unconstrain(m) for m in my_models], [m.jitter for m in my_models])
         # notebook.py:55-75: adam(0.01), fix_params=False, num_steps_per_epoch=1000
         fit_opt = _lib.LfmAdam(0.01, 0.9, 0.999, 1e-8, 0.0, 1000, 0)
         iters = a.fit_iters
-        per_step = world * len(models) * iters  # replicas: every rank fits the 15 problems
-        fit_hist = np.empty((iters, len(models)))
+        per_step = P * iters  # the 15 fits' training steps, each on exactly one rank
+        fit_hist = np.empty((iters, len(mine)))
+        close = (lambda: None)
+        if len(mine):
+            fit_ev = farm.BatchEvaluator(ctx, [datasets[i] for i in mine], negative=True)
+            close = fit_ev.close
+            batch = fit_ev.registered([m.num_genes for m in my_models])
 
-        def step():
+        def fit_block():
             raw = raw0.copy()
             mu, nu = np.zeros_like(raw), np.zeros_like(raw)
             ctx.check(lib.lfm_batch_fit_f64(h, batch, _lib.ctypes.byref(fit_opt), 1, 0, iters,
                                             _lib.dptr(raw), _lib.dptr(mu), _lib.dptr(nu),
                                             _lib.dptr(fit_hist), None))
-            return fit_hist[-1].copy()  # each problem's final loss
+            return raw
+
+        if world == 1:
+            def step():
+                fit_block()
+                return fit_hist[-1].copy()  # each problem's final loss
+        else:
+            rec_len = 3 * gmax + 2 + iters
+
+            def block(idx):
+                raw = fit_block()
+                return TR.fit_records(TR.unpack_raw(raw, [genes[i] for i in idx]), fit_hist.T,
+                                      gmax)
+
+            def step():
+                rec = fm.run_records(P, rec_len, block)
+                step.records = rec
+                return rec[:, -1].copy()  # each problem's final loss
+    elif a.workload == "c5":
+        # rounds: R hyperparameter rounds of the 15 problems per rank (round-major, so the
+        # static partition gives each rank whole rounds); a step evaluates this rank's R x 15
+        # problems in ONE batched launch (hyperparameters packed once) and exchanges them in ONE
+        # all-gather (over RCCL: the device-side round, lfm_farm_batch_mll_f64). One GPU with
+        # R = 1 is configs[4]'s own step, the 15 problems
+        R = a.rounds
+        models, datasets = farm.workload("c5", rounds=world * R)
+        n = datasets[0].n
+        P = len(models)
+        mine = farm.partition(P, world, rank)
+        per_step = P
+        fev = farm.BatchEvaluator(ctx, [datasets[i] for i in mine])
+        close = fev.close
+        c5_hyp = fev.pack([models[i] for i in mine])
+        if world == 1:
+            def step():
+                return fev.evaluate_packed(c5_hyp)
+        elif exchange == "rccl":
+            def step():
+                return fm.run_fused(P, lambda slots: fev.farm_round_packed(c5_hyp, slots))
+        else:
+            def step():
+                return fm.run(P, lambda idx: fev.evaluate_packed(c5_hyp))
     else:
         models, datasets = farm.workload(a.workload, a.genes, a.timepoints, a.restarts)
         n = datasets[0].n
         mine = farm.partition(len(models), world, rank)
         workers = a.workers if a.workers > 0 else farm.choose_workers(len(mine))
         per_step = len(models)
-        if a.workload == "c5" and exchange == "rccl" and len(mine):
-            # the device-side round: this rank's block evaluated straight into its RCCL send
-            # slots, all-gathered on the device, published to the host (lfm_farm_batch_mll_f64)
-            my_models = [models[i] for i in mine]
-            fev = farm.BatchEvaluator(ctx, [datasets[i] for i in mine])
-            close = fev.close
+        evaluate, close = farm.gpu_evaluator(ctx, datasets, negative=False, workers=workers)
 
-            def step():
-                return fm.run_fused(len(models), lambda slots: fev.farm_round(my_models, slots))
-        else:
-            evaluate, close = farm.gpu_evaluator(ctx, datasets, negative=False, workers=workers)
-
-            def step():
-                return fm.run_problems(models, datasets, evaluate)
+        def step():
+            return fm.run_problems(models, datasets, evaluate)
 
     results = []
 
@@ -692,7 +800,14 @@ def main(argv=None):
     # all-gather of this workload's NaN-padded slots, outside the timed region
     collective = None
     if world > 1:
-        slots = max(farm.slots_per_rank(per_step, world), 1)
+        # this workload's own exchange size: the records of c5fit's fits, c5's rounds, c3's
+        # restarts, one slot per rank for c2 / c4
+        if a.workload == "c5fit":
+            slots = farm.slots_per_rank(P, world) * (3 * gmax + 2 + iters)
+        elif a.workload in ("c2", "c4"):
+            slots = 1
+        else:
+            slots = max(farm.slots_per_rank(per_step, world), 1)
         lat = []
         for _ in range(25):
             barrier()
@@ -762,6 +877,60 @@ def main(argv=None):
     if not np.all(res == res[0]):
         raise SystemExit("timed steps disagree (the same inputs gave different results)")
 
+    # multi-rank farms, checked after the timed region on rank 0: the gathered results are the
+    # bits of one rank doing the whole step alone (the same kernels on the same inputs)
+    if world > 1 and rank == 0 and a.workload == "c5":
+        evl = farm.BatchEvaluator(ctx, datasets)
+        try:
+            local = evl.evaluate_packed(evl.pack(models))
+        finally:
+            evl.close()
+        if not np.array_equal(local, res[0]):
+            raise SystemExit("the gathered c5 rounds differ from one rank's evaluation of them")
+    if world > 1 and rank == 0 and a.workload == "c5fit":
+        from dis_project_amd import trainer as TR
+
+        evl = farm.BatchEvaluator(ctx, datasets, negative=True)
+        try:
+            bl = evl.registered(genes)
+            raw = TR.pack_raw([TR.unconstrain(m) for m in models], [m.jitter for m in models])
+            mu, nu = np.zeros_like(raw), np.zeros_like(raw)
+            hist1 = np.empty((iters, P))
+            ctx.check(lib.lfm_batch_fit_f64(h, bl, _lib.ctypes.byref(fit_opt), 1, 0, iters,
+                                            _lib.dptr(raw), _lib.dptr(mu), _lib.dptr(nu),
+                                            _lib.dptr(hist1), None))
+        finally:
+            evl.close()
+        want = TR.fit_records(TR.unpack_raw(raw, genes), hist1.T, gmax)
+        if not np.array_equal(np.isnan(want), np.isnan(step.records)) or \
+                not np.array_equal(want[~np.isnan(want)], step.records[~np.isnan(want)]):
+            raise SystemExit("the gathered fits differ from one rank's fit of all 15")
+    c5_rounds16 = None
+    if world == 1 and a.workload == "c5" and a.rounds == 1:
+        # the per-GPU capacity at the multi-GPU lines' round count (C5_ROUNDS_MULTI rounds of
+        # the 15 in one launch): the W = 1 point of the weak-scaling curve over rounds
+        m16, d16 = farm.workload("c5", rounds=C5_ROUNDS_MULTI)
+        ev16 = farm.BatchEvaluator(ctx, d16)
+        try:
+            h16 = ev16.pack(m16)
+            for _ in range(max(a.warmup, 10)):
+                v16 = ev16.evaluate_packed(h16)
+            t16 = []
+            for _ in range(a.steps):
+                t1 = time.perf_counter()
+                v16 = ev16.evaluate_packed(h16)
+                t16.append((time.perf_counter() - t1) * 1e3)
+        finally:
+            ev16.close()
+        if not np.allclose(v16[:len(res[0])], res[0], rtol=1e-12, atol=0):
+            raise SystemExit("round 0 of the 16-round batch differs from the 15-problem step")
+        c5_rounds16 = {"rounds": C5_ROUNDS_MULTI, "problems_per_step": len(m16),
+                       "ms_per_step": float(np.median(t16)),
+                       "value": len(m16) * 1e3 / float(np.median(t16)), "unit": "MLL evals/s",
+                       "note": "one launch of the 16 rounds x 15 problems (hyperparameters read "
+                               "from pinned memory: more than 16 problems), the W = 1 point of "
+                               "the multi-GPU lines' weak scaling over rounds"}
+
     # value: the median step, max over ranks — one slow step (a clock dip, the
     # first step's HIP-event records) does not move it; the mean over the K steps between the
     # barriers is kept beside it (mean_value, mean_ms_per_step)
@@ -769,7 +938,8 @@ def main(argv=None):
     value = per_step * 1e3 / med_ms
     ms_per_step = med_ms
     chol_flops = n**3 / 3.0
-    scaling = "strong" if a.workload in ("c3", "c5") else "weak"
+    # c3 and c5fit: a fixed set of problems partitioned over the ranks; c5: R rounds per rank
+    scaling = "strong" if a.workload in ("c3", "c5fit") else "weak"
     if a.workload == "c2":
         wl = (f"configs[1]: one MLL eval per rank, {a.genes} genes x {a.timepoints} timepoints, "
               f"N={n}, fp64")
@@ -784,10 +954,14 @@ def main(argv=None):
     elif a.workload == "c5fit":
         wl = (f"configs[4]'s training workflow (notebook.py:55-75): JaxTrainer.fit of the 15 "
               f"replicate x leave-one-gene-out problems (N={n}), {a.fit_iters} adam(0.01) steps "
-              f"each, fix_params=False, in one launch per fit (lfm_batch_fit_f64)")
+              f"each, fix_params=False; each rank fits its block of the 15 in one launch "
+              f"(lfm_batch_fit_f64)" + (", then one all-gather of the fits' final raw parameters "
+                                        "and loss histories" if world > 1 else ""))
     else:
-        wl = (f"configs[4]: 3 replicates x 5 leave-one-gene-out ablations (N={n}) per step, "
-              f"farmed over {world} GPU(s), one batched launch per rank")
+        wl = (f"configs[4]: 3 replicates x 5 leave-one-gene-out ablations (N={n}), "
+              f"{a.rounds} hyperparameter round(s) of the 15 per rank per step "
+              f"({per_step} evaluations over {world} GPU(s)), one batched launch per rank"
+              + (" and one all-gather" if world > 1 else ""))
     c4 = a.workload == "c4"
     fit = a.workload == "c5fit"
     line = {
@@ -814,7 +988,12 @@ def main(argv=None):
         "config": {"workload": wl, "N": n,
                    "genes": a.genes if a.workload not in ("c5", "c5fit") else 4,
                    "timepoints": a.timepoints if a.workload not in ("c5", "c5fit") else 7,
-                   "problems_per_step": per_step, "parallelism": f"replicas{world}",
+                   "problems_per_step": per_step,
+                   "parallelism": (f"replicas{world}: {a.rounds} hyperparameter round(s) of the "
+                                   "15 problems per rank (weak scaling over rounds)"
+                                   if a.workload == "c5" else
+                                   f"replicas{world}: the 15 fits partitioned over the ranks"
+                                   if a.workload == "c5fit" else f"replicas{world}"),
                    "exchange": {"rccl": "RCCL all-gather of NaN-padded per-rank result slots",
                                 "gloo": "gloo all-gather (rehearsal)",
                                 "gloo-fallback": "gloo all-gather of the same slots (the RCCL "
@@ -831,6 +1010,8 @@ def main(argv=None):
         line["config"]["workers_per_gpu"] = workers
     if collective:
         line["collective"] = collective
+    if c5_rounds16:
+        line["rounds16"] = c5_rounds16
     if a.workload in ("c2", "c3"):
         line["cholesky_gflops_per_gpu"] = chol_flops * value / world / 1e9
     if a.workload == "c3":

@@ -38,6 +38,12 @@ def sigmoid_bounded(x, low=0.5, high=3.5):
     return low + (high - low) / (1.0 + np.exp(-np.asarray(x, np.float64)))
 
 
+def logit_bounded(y, low=0.5, high=3.5):
+    """sigmoid_bounded's inverse."""
+    u = (np.asarray(y, np.float64) - low) / (high - low)
+    return np.log(u) - np.log1p(-u)
+
+
 @dataclass
 class Workload:
     name: str
@@ -99,6 +105,27 @@ def c5_ablations(seeds=(10, 11, 12)):
             x, y, _ = dataset_3d(data)
             out.append(Workload(f"rep{r}_minus_{drop}", ExactLFM(jitter=1e-4, num_genes=4),
                                 Dataset(x, y)))
+    return out
+
+
+def c5_rounds(base_models, rounds, first_seed=500):
+    """Hyperparameter rounds of the C5 problems (bench.py --workload c5 --rounds):
+    round 0 is the problems' own models (the reference init, notebook.py:51); round k > 0
+    perturbs every problem's hyperparameters independently, raw + 0.5 N(0, 1) in the
+    bijectors' unconstrained space (seed first_seed + k), like C3's restarts of C2. Returns the
+    models round-major: [round 0's P models, round 1's, ...]."""
+    out = list(base_models)
+    for k in range(1, rounds):
+        rng = np.random.default_rng(first_seed + k)
+        for m in base_models:
+            G = m.num_genes
+            raw = 0.5 * rng.standard_normal(3 * G + 2)
+            out.append(m.replace(
+                true_d=softplus(softplus_inverse(m.true_d) + raw[:G]),
+                true_s=softplus(softplus_inverse(m.true_s) + raw[G:2 * G]),
+                true_b=softplus(softplus_inverse(m.true_b) + raw[2 * G:3 * G]),
+                obs_stddev=float(softplus(softplus_inverse(m.obs_stddev) + raw[3 * G])),
+                l=float(sigmoid_bounded(logit_bounded(m.l) + raw[3 * G + 1]))))
     return out
 
 

@@ -219,6 +219,36 @@ class BatchEvaluator:
         self.ctx.check(rc, allow_not_pd=True)
         return self._out.copy()
 
+    def pack(self, models) -> np.ndarray:
+        """The models' hyperparameters in the library's packed layout (a copy; the batch is
+        registered for their gene layout): a sweep whose hyperparameter sets are known up front
+        packs them once and passes the array to ``evaluate_packed`` / ``farm_round_packed``."""
+        self._pack(models)
+        return self._buf.copy()
+
+    def _packed(self, hyp) -> int:
+        if self.batch is None or hyp.dtype != np.float64 or hyp.size != self._buf.size or \
+                not hyp.flags.c_contiguous:
+            raise ValueError("a packed array of this batch's layout (BatchEvaluator.pack)")
+        return hyp.ctypes.data
+
+    def evaluate_packed(self, hyp: np.ndarray) -> np.ndarray:
+        """__call__ on pre-packed hyperparameters (``pack``)."""
+        rc = self.ctx.lib.lfm_batch_mll_f64(self.ctx.handle, self.batch, self._packed(hyp),
+                                            int(self.negative), self._out_ptr, self._st_ptr)
+        self.ctx.check(rc, allow_not_pd=True)
+        return self._out.copy()
+
+    def farm_round_packed(self, hyp: np.ndarray, slots: int) -> np.ndarray:
+        """farm_round on pre-packed hyperparameters (``pack``)."""
+        nranks = max(1, int(getattr(self.ctx, "farm_ranks", 1)))
+        recv = np.empty(nranks * int(slots))
+        rc = self.ctx.lib.lfm_farm_batch_mll_f64(self.ctx.handle, self.batch, self._packed(hyp),
+                                                 int(self.negative), int(slots), _lib.dptr(recv),
+                                                 self._st_ptr)
+        self.ctx.check(rc, allow_not_pd=True)
+        return recv
+
     def farm_round(self, models, slots: int) -> np.ndarray:
         """One device-side farm round (``lfm_farm_batch_mll_f64``): this rank's problems
         evaluated straight into its ``slots`` RCCL send slots (NaN-padded), all-gathered on the
@@ -252,13 +282,17 @@ class BatchEvaluator:
             self._genes = None
 
 
-def workload(kind: str, genes: int = 64, timepoints: int = 256, restarts: int = 32):
+def workload(kind: str, genes: int = 64, timepoints: int = 256, restarts: int = 32,
+             rounds: int = 1):
     """Problems of a farm workload as (models, datasets):
 
     ``c3``  BASELINE.json configs[2]: the C2 grid (``genes`` x ``timepoints``) under
             ``restarts`` random-restart hyperparameter sets (configs.c3_restarts), one dataset;
     ``c5``  configs[4]: 3 synthetic replicates x 5 leave-one-gene-out ablations at N = 28
-            (configs.c5_ablations, notebook.py:33-75).
+            (configs.c5_ablations, notebook.py:33-75); ``rounds`` > 1: that many
+            hyperparameter rounds of the 15 (configs.c5_rounds; round 0 the problems' own),
+            round-major — farm.partition then gives each of W ranks whole rounds when W
+            divides ``rounds``.
     """
     from . import configs
 
@@ -269,7 +303,10 @@ def workload(kind: str, genes: int = 64, timepoints: int = 256, restarts: int = 
         return models, [base.data] * len(models)
     if kind == "c5":
         ws = configs.c5_ablations()
-        return [w.model for w in ws], [w.data for w in ws]
+        models, datasets = [w.model for w in ws], [w.data for w in ws]
+        if rounds > 1:
+            models, datasets = configs.c5_rounds(models, rounds), datasets * rounds
+        return models, datasets
     raise ValueError(f"unknown farm workload {kind!r}")
 
 
@@ -314,6 +351,29 @@ class Farm:
         per = max(slots_per_rank(nprob, self.world), 1)
         recv = np.asarray(round_fn(per), dtype=np.float64).reshape(self.world, -1)
         out = np.empty(nprob)
+        for r in range(self.world):
+            rr = partition(nprob, self.world, r)
+            out[rr.start:rr.stop] = recv[r, : len(rr)]
+        return out
+
+    def run_records(self, nprob: int, rec_len: int,
+                    block_fn: Callable[[range], np.ndarray]) -> np.ndarray:
+        """One round whose per-problem result is a fixed-length record (a fit's final raw
+        parameters and loss history): ``block_fn(mine) -> [len(mine), rec_len]`` on this rank's
+        block, then ONE all-gather of ceil(P/W) NaN-padded records per rank. Returns every
+        problem's record [P, rec_len], in problem order, on every rank."""
+        per = slots_per_rank(nprob, self.world)
+        mine = partition(nprob, self.world, self.rank)
+        send = np.full((max(per, 1), rec_len), np.nan)
+        if len(mine):
+            rec = np.asarray(block_fn(mine), dtype=np.float64)
+            if rec.shape != (len(mine), rec_len):
+                raise ValueError("block_fn returned records of the wrong shape")
+            send[: len(mine)] = rec
+        if self.world == 1:
+            return send[:nprob].copy()
+        recv = self.gather(send.reshape(-1)).reshape(self.world, -1, rec_len)
+        out = np.empty((nprob, rec_len))
         for r in range(self.world):
             rr = partition(nprob, self.world, r)
             out[rr.start:rr.stop] = recv[r, : len(rr)]

@@ -290,3 +290,90 @@ class BatchTrainer:
 
     def close(self):
         self._ev.close()
+
+
+def fit_records(raws: Sequence[dict], hist: np.ndarray, gmax: int) -> np.ndarray:
+    """Each problem's fit result as one fixed-length fp64 record (FarmTrainer's exchange):
+    raw true_d / true_s / true_b (G each, NaN-padded to gmax), raw l, raw obs_stddev, then the
+    loss history. hist: [P, iters]."""
+    hist = np.asarray(hist, np.float64)
+    rec = np.full((len(raws), 3 * gmax + 2 + hist.shape[1]), np.nan)
+    for q, r in enumerate(raws):
+        G = np.asarray(r["true_d"]).size
+        for k, key in enumerate(("true_d", "true_s", "true_b")):
+            rec[q, k * gmax: k * gmax + G] = r[key]
+        rec[q, 3 * gmax] = r["l"]
+        rec[q, 3 * gmax + 1] = r["obs_stddev"]
+        rec[q, 3 * gmax + 2:] = hist[q]
+    return rec
+
+
+def unfit_records(rec: np.ndarray, genes: Sequence[int], gmax: int):
+    """fit_records' inverse: (raws, hist [P, iters])."""
+    raws = []
+    for q, G in enumerate(genes):
+        r = rec[q]
+        raws.append({"true_d": r[:G].copy(), "true_s": r[gmax:gmax + G].copy(),
+                     "true_b": r[2 * gmax:2 * gmax + G].copy(), "l": float(r[3 * gmax]),
+                     "obs_stddev": float(r[3 * gmax + 1])})
+    return raws, np.ascontiguousarray(rec[:, 3 * gmax + 2:])
+
+
+class FarmTrainer:
+    """``JaxTrainer.fit`` of P independent problems farmed over W ranks (one process per GPU;
+    the reference runs one JaxTrainer.fit per ablation problem, notebook.py:58-75 over
+    trainer.py:162-228): rank r fits its static block ``farm.partition(P, W, r)`` in ONE
+    ``lfm_batch_fit_f64`` launch (a BatchTrainer over the block), then ONE all-gather exchanges
+    every problem's final raw parameters and loss history as NaN-padded fixed-length records
+    (``Farm.run_records``, ``fit_records``). Every rank ends with every problem's fitted model
+    and history — the bits of a one-rank BatchTrainer.fit of all P (each problem's fit is one
+    workgroup's, whatever else shares its launch). ``fit`` always starts from the models given
+    here (a fresh JaxTrainer per problem). ``block_fit(indices, fix_params, spe) -> (raws,
+    hist)`` replaces the GPU block (the CPU tests drive the exchange with the C++ port)."""
+
+    def __init__(self, models, objective, training_data, optim: adam, farm, num_iters: int = 150,
+                 ctx: Any = None, block_fit=None):
+        self.models = list(models)
+        self.training_data = list(training_data)
+        if len(self.models) != len(self.training_data):
+            raise ValueError("one model per dataset")
+        self.objective, self.optim, self.farm = objective, optim, farm
+        self.num_iters, self.ctx = int(num_iters), ctx
+        self.genes = [int(m.num_genes) for m in self.models]
+        self.gmax = max(self.genes)
+        self._raw0 = [unconstrain(m) for m in self.models]
+        self._block_fit = block_fit or self._gpu_block
+        self._bt = None
+        self.raws, self.history = None, None
+
+    def _gpu_block(self, idx, fix_params, spe):
+        if self._bt is None:
+            self._bt = BatchTrainer([self.models[i] for i in idx], self.objective,
+                                    [self.training_data[i] for i in idx], self.optim,
+                                    num_iters=self.num_iters, ctx=self.ctx)
+        self._bt.raws = [self._raw0[i] for i in idx]
+        _, hist = self._bt.fit(fix_params=fix_params, num_steps_per_epoch=spe)
+        return self._bt.raws, hist
+
+    def fit(self, fix_params: bool = True, num_steps_per_epoch: int = 1000):
+        """trainer.py:162-228 for every problem, farmed; returns (models, histories [P, iters])
+        on every rank."""
+        def block(idx):
+            raws, hist = self._block_fit(list(idx), fix_params, num_steps_per_epoch)
+            return fit_records(raws, hist, self.gmax)
+
+        rec = self.farm.run_records(len(self.models), 3 * self.gmax + 2 + self.num_iters, block)
+        self.raws, self.history = unfit_records(rec, self.genes, self.gmax)
+        out = []
+        for r, like in zip(self.raws, self.models):
+            m = constrain(r, like)
+            if fix_params:  # trainer.py:218-222, on the constrained model
+                c = JaxTrainer.after_epoch({"true_s": m.true_s, "true_d": m.true_d}, True)
+                m = m.replace(true_s=c["true_s"], true_d=c["true_d"])
+            out.append(m)
+        return out, self.history
+
+    def close(self):
+        if self._bt is not None:
+            self._bt.close()
+            self._bt = None

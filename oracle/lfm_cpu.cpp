@@ -607,4 +607,45 @@ int lfm_cpu_fit(const double* x, const double* y, int64_t n, int64_t G, double* 
   return failed;
 }
 
+// The CPU baselines across cores (bench.py's c5 / c5fit cpu_baseline "threads" variants): nprob
+// independent problems, one per OpenMP thread at a time (dynamic, 1), each evaluated or fitted
+// serially (nested regions inactive). x / y / n / G per problem; hyp in lfm_batch_mll_f64's
+// packed layout (each problem's D S B, then each problem's l, obs_stddev, jitter).
+// reps > 1: the nprob problems evaluated reps times over (a timing sample), out from any rep.
+// Inside a team of several threads the problem's own parallel regions are nested, so inactive
+// (serial); a team of one passes threads = 1 so that they do not spread over the cores.
+int lfm_cpu_mll_batch(int64_t nprob, const double* const* x, const double* const* y,
+                      const int64_t* n, const int64_t* G, const double* hyp, int negative,
+                      int threads, int64_t reps, double* out) {
+  if (nprob < 1 || reps < 1) return 1;
+  std::vector<int64_t> off((size_t)nprob), nvec(1, 0);
+  for (int64_t q = 0; q < nprob; ++q) {
+    off[q] = nvec[0];
+    nvec[0] += 3 * G[q];
+  }
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads > 0 ? threads : omp_get_max_threads())
+  for (int64_t t = 0; t < nprob * reps; ++t) {
+    const int64_t q = t % nprob;
+    const double* v = hyp + off[q];
+    const double* sc = hyp + nvec[0] + 3 * q;
+    out[q] = lfm_cpu_mll(x[q], y[q], n[q], G[q], v, v + G[q], v + 2 * G[q], sc[0], sc[1], sc[2],
+                         negative, omp_get_num_threads() > 1 ? 0 : 1, nullptr, nullptr);
+  }
+  return 0;
+}
+
+// raw[q]: problem q's [3G + 3] unconstrained parameters (in / out); history [nprob][iters].
+// Returns the number of failed steps over all problems.
+int lfm_cpu_fit_batch(int64_t nprob, const double* const* x, const double* const* y,
+                      const int64_t* n, const int64_t* G, double* const* raw, int64_t iters,
+                      double lr, double b1, double b2, double eps, double eps_root, int64_t spe,
+                      int fix, int negative, int threads, double* history) {
+  int failed = 0;
+#pragma omp parallel for schedule(dynamic, 1) reduction(+ : failed) num_threads(threads > 0 ? threads : omp_get_max_threads())
+  for (int64_t q = 0; q < nprob; ++q)
+    failed += lfm_cpu_fit(x[q], y[q], n[q], G[q], raw[q], iters, lr, b1, b2, eps, eps_root, spe,
+                          fix, negative, history + q * iters);
+  return failed;
+}
+
 }  // extern "C"

@@ -44,6 +44,14 @@ def load():
         lib.lfm_cpu_fit.restype = c_int
         lib.lfm_cpu_fit.argtypes = [_dp, _dp, c_int64, c_int64, _dp, c_int64, c_double, c_double,
                                     c_double, c_double, c_double, c_int64, c_int, c_int, _dp]
+        vp = ctypes.c_void_p
+        lib.lfm_cpu_mll_batch.restype = c_int
+        lib.lfm_cpu_mll_batch.argtypes = [c_int64, vp, vp, vp, vp, _dp, c_int, c_int, c_int64,
+                                          _dp]
+        lib.lfm_cpu_fit_batch.restype = c_int
+        lib.lfm_cpu_fit_batch.argtypes = [c_int64, vp, vp, vp, vp, vp, c_int64, c_double,
+                                          c_double, c_double, c_double, c_double, c_int64, c_int,
+                                          c_int, c_int, _dp]
         _lib = lib
     return _lib
 
@@ -137,4 +145,43 @@ def fit(x, y, G, raw, iters, lr=0.01, b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0, 
     hist = np.empty(int(iters))
     bad = lib.lfm_cpu_fit(_p(x), _p(y), x.shape[0], int(G), _p(raw), int(iters), lr, b1, b2, eps,
                           eps_root, int(spe), int(bool(fix)), int(bool(negative)), _p(hist))
+    return hist, int(bad)
+
+def _ptrs(arrs):
+    return (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+
+
+def mll_batch(xs, ys, genes, hyp, negative=False, threads=0, reps=1):
+    """Every problem's CustomConjMLL(negative).step, one problem per OpenMP thread at a time
+    (threads = 0: all allowed); hyp in lfm_batch_mll_f64's packed layout; reps > 1 evaluates
+    the P problems reps times over in the same parallel loop (a timing sample). Returns [P]."""
+    lib = load()
+    xs = [_f64(x).reshape(-1, 3) for x in xs]
+    ys = [_f64(y).reshape(-1) for y in ys]
+    ns = np.array([x.shape[0] for x in xs], np.int64)
+    gs = np.array(genes, np.int64)
+    hyp = _f64(hyp)
+    out = np.empty(len(xs))
+    rc = lib.lfm_cpu_mll_batch(len(xs), _ptrs(xs), _ptrs(ys), ns.ctypes.data, gs.ctypes.data,
+                               _p(hyp), int(bool(negative)), int(threads), int(reps), _p(out))
+    if rc:
+        raise ValueError("lfm_cpu_mll_batch: bad arguments")
+    return out
+
+
+def fit_batch(xs, ys, genes, raws, iters, lr=0.01, b1=0.9, b2=0.999, eps=1e-8, eps_root=0.0,
+              spe=1000, fix=False, negative=True, threads=0):
+    """fit() of every problem, one problem per OpenMP thread at a time; raws: per problem a
+    [3G + 3] float64 array, updated in place. Returns (history [P, iters], failures)."""
+    lib = load()
+    xs = [_f64(x).reshape(-1, 3) for x in xs]
+    ys = [_f64(y).reshape(-1) for y in ys]
+    ns = np.array([x.shape[0] for x in xs], np.int64)
+    gs = np.array(genes, np.int64)
+    for r, g in zip(raws, genes):
+        assert r.dtype == np.float64 and r.flags.c_contiguous and r.size == 3 * g + 3
+    hist = np.empty((len(xs), int(iters)))
+    bad = lib.lfm_cpu_fit_batch(len(xs), _ptrs(xs), _ptrs(ys), ns.ctypes.data, gs.ctypes.data,
+                                _ptrs(raws), int(iters), lr, b1, b2, eps, eps_root, int(spe),
+                                int(bool(fix)), int(bool(negative)), int(threads), _p(hist))
     return hist, int(bad)

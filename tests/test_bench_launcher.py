@@ -51,6 +51,11 @@ def test_default_workload_follows_gpu_count():
     assert bench.parse(["--gpus", "2", "--workload", "c5"]).workload == "c5"
     assert bench.parse(["--workload", "c4"]).genes == 256
     assert bench.parse(["--workload", "c3"]).genes == 64
+    # c5's hyperparameter rounds per rank: configs[4]'s own 15-problem step on one GPU, 16
+    # rounds (one launch of 240 problems and one exchange per step) on several
+    assert bench.parse(["--workload", "c5"]).rounds == 1
+    assert bench.parse(["--gpus", "2", "--workload", "c5"]).rounds == bench.C5_ROUNDS_MULTI == 16
+    assert bench.parse(["--gpus", "8", "--workload", "c5", "--rounds", "4"]).rounds == 4
 
 
 def test_launcher_wires_every_rank(tmp_path, rank_script):

@@ -46,6 +46,52 @@ def _oracle_eval(models, datasets):
             for m, d in zip(models, datasets)]
 
 
+def _port_eval(models, datasets):
+    """The C++ port's MLLs of a block (oracle/lfm_cpu.cpp; test-only)."""
+    from oracle import lfm_cpu
+
+    hyp = np.concatenate([np.concatenate([m.true_d, m.true_s, m.true_b]) for m in models] +
+                         [np.array([[m.l, m.obs_stddev, m.jitter] for m in models]).reshape(-1)])
+    return lfm_cpu.mll_batch([d.X for d in datasets], [d.y for d in datasets],
+                             [m.num_genes for m in models], hyp, threads=1)
+
+
+def _cpu_block_fit(models, datasets, iters):
+    """trainer.FarmTrainer's block_fit with the C++ port's JaxTrainer.fit standing in for the
+    GPU launch (test-only): (raws, hist [k, iters])."""
+    from oracle import lfm_cpu
+    from dis_project_amd import trainer as TR
+
+    def block(idx, fix_params, spe):
+        raws, hist = [], []
+        for i in idx:
+            m = models[i]
+            r0 = TR.unconstrain(m)
+            r = np.concatenate([r0["true_d"], r0["true_s"], r0["true_b"],
+                                [r0["l"], r0["obs_stddev"], m.jitter]])
+            h, _ = lfm_cpu.fit(datasets[i].X, datasets[i].y, m.num_genes, r, iters, spe=spe,
+                               fix=fix_params, negative=True)
+            hist.append(h)
+            raws.append(TR.unpack_raw(np.concatenate([r[:-3], r[-3:]]), [m.num_genes])[0])
+        return raws, np.asarray(hist)
+
+    return block
+
+
+def _farm_fit(f, iters=12):
+    from dis_project_amd import farm as F
+    from dis_project_amd import trainer as TR
+    from dis_project_amd.objectives import CustomConjMLL
+
+    models, datasets = F.workload("c5")
+    ft = TR.FarmTrainer(models, CustomConjMLL(negative=True), datasets, TR.adam(0.01), f,
+                        num_iters=iters, block_fit=_cpu_block_fit(models, datasets, iters))
+    out, hist = ft.fit(fix_params=True, num_steps_per_epoch=5)
+    fitted = [np.concatenate([m.true_d, m.true_s, m.true_b, [m.l, m.obs_stddev]]).tolist()
+              for m in out]
+    return fitted, hist
+
+
 # the farm workloads bench.py runs (--workload c5 / c3), c3 at a CPU-oracle size
 WORKLOADS = [("c5", {}), ("c3", dict(genes=4, timepoints=16, restarts=5))]
 
@@ -67,7 +113,14 @@ def _worker(rank, world, port, q):
         models, datasets = F.workload(kind, **kw)
         outs.append(f.run_problems(models, datasets, _oracle_eval).tolist())
     out_odd = f.run(3, lambda idx: [float(i) for i in idx])  # fewer problems than slots
-    q.put((rank, outs, out_odd.tolist()))
+    # bench.py --workload c5 at W > 1: whole hyperparameter rounds per rank, one exchange
+    models, datasets = F.workload("c5", rounds=2 * world)
+    outs.append(f.run(len(models), lambda idx: _port_eval([models[i] for i in idx],
+                                                          [datasets[i] for i in idx])).tolist())
+    # bench.py --workload c5fit / trainer.FarmTrainer at W > 1: the fits partitioned, one
+    # all-gather of their final raw parameters and loss histories
+    fitted, hist = _farm_fit(f)
+    q.put((rank, outs, out_odd.tolist(), fitted, hist.tolist()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -85,11 +138,17 @@ def test_farm_gloo_world2(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     refs = [_oracle_eval(*farm.workload(kind, **kw)) for kind, kw in WORKLOADS]
-    for rank, outs, out_odd in res:
+    refs.append(_port_eval(*farm.workload("c5", rounds=2 * world)))
+    fit1, hist1 = _farm_fit(farm.Farm(1, 0, None))  # one rank: the whole fit, no exchange
+    assert hist1.shape == (15, 12) and np.all(np.isfinite(hist1))
+    for rank, outs, out_odd, fitted, hist in res:
         for out, ref in zip(outs, refs):
             np.testing.assert_array_equal(np.array(out), np.array(ref))
             assert not any(math.isnan(v) for v in out)
         assert out_odd == [0.0, 1.0, 2.0]
+        # the farmed fits: every rank holds every problem's fit, the bits of one rank's
+        np.testing.assert_array_equal(np.array(hist), hist1)
+        np.testing.assert_array_equal(np.array(fitted), np.array(fit1))
 
 
 @pytest.mark.gpu
