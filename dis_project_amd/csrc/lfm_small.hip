@@ -63,10 +63,17 @@ __device__ __forceinline__ double swap_halves(double v) {
 // fences are empty (a wave's LDS operations are performed in issue order) and the wave barrier
 // only fences code motion, so the ISA is unchanged; what it adds over a bare compiler fence is the
 // language-level ordering the reads rely on.
+#ifndef LFM_WAVE_HANDOFF
+#define LFM_WAVE_HANDOFF 1  // A/B only (make EXTRA=-DLFM_WAVE_HANDOFF=0): round 5's compiler fence
+#endif
 __device__ __forceinline__ void wave_lds_handoff() {
+#if LFM_WAVE_HANDOFF
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#else
+  asm volatile("" ::: "memory");
+#endif
 }
 // window widths of the phases: 64 48 32 24 16 12 8
 template <int W>

@@ -3,7 +3,10 @@
 # scripts/gpu_step.sh; the first failing step ends the call — never retried):
 #   tests    the whole -m gpu suite, then smoke()
 #   handoff  the small kernels before / after the wave hand-off hardening (ablibs/r05 = round 5's
-#            library), c5 and c5fit bench lines interleaved, two rounds
+#            library, ablibs/nohandoff = this tree with -DLFM_WAVE_HANDOFF=0), c5 and c5fit bench
+#            lines interleaved, two rounds
+#   rehearse two ranks sharing the card, gloo exchange: c5 (16 rounds per rank) and c5fit
+#            (the 15 fits partitioned)
 #   c2 c3 c5 c5fit   one bench line each (the default step counts of the round's profile set)
 set -u
 export TMPDIR=/tmp
@@ -18,12 +21,19 @@ for study in "$@"; do
       ;;
     handoff)
       for r in 1 2; do
-        for lib in ablibs/r05/liblfm.so dis_project_amd/liblfm.so; do
+        for lib in ablibs/r05/liblfm.so ablibs/nohandoff/liblfm.so dis_project_amd/liblfm.so; do
           tag=$(basename "$(dirname "$lib")")
           LFM_LIBRARY=$lib $S r06_handoff_c5_${tag}_$r 120 python -u bench.py --workload c5 --steps 3000 --warmup 300 --no-cpu-baseline || exit $?
           LFM_LIBRARY=$lib $S r06_handoff_c5fit_${tag}_$r 120 python -u bench.py --workload c5fit --steps 30 --warmup 3 --no-cpu-baseline || exit $?
         done
       done
+      ;;
+    rehearse)
+      R="python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1"
+      $S r06_reh_c5 300 $R --master-port 29532 bench.py --gpus 2 --workload c5 --steps 500 --warmup 50 \
+        --share-gpus --gather gloo --no-cpu-baseline || exit $?
+      $S r06_reh_c5fit 300 $R --master-port 29533 bench.py --gpus 2 --workload c5fit --steps 5 --warmup 1 \
+        --share-gpus --gather gloo --no-cpu-baseline || exit $?
       ;;
     c2) $S r06_bench_c2 300 python -u bench.py --workload c2 --steps 20 --warmup 3 || exit $? ;;
     c3) $S r06_bench_c3 400 python -u bench.py --workload c3 --steps 5 --warmup 1 --no-cpu-baseline || exit $? ;;
