@@ -668,6 +668,8 @@ void release_partition(lfm_ctx* ctx) {
 //                        memory instead of the kernel arguments
 //   LFM_FARM_GRAPH       0: a device-side farm round is enqueued call by call instead of
 //                        replayed as one captured graph
+//   LFM_S1_MASK_CUS      (A/B) a schedule-1 context's streams avoid CUs [0, k) (CU-masked,
+//                        without the side stream's priority)
 // Every knob is read here, once: a call never consults the environment.
 hipError_t create_streams(lfm_ctx* ctx) {
   ctx->sched = env_int_api("LFM_SCHED", 3) == 1 ? 1 : 3;
@@ -701,6 +703,13 @@ hipError_t create_streams(lfm_ctx* ctx) {
   if (prop.multiProcessorCount > 0) ctx->cus = prop.multiProcessorCount;
   // ctx->side (schedule 1's high-priority stream) is created on first use: schedule 3 never
   // launches on it, and an idle hardware queue beside the running ones costs
+  ctx->s1_mask = ctx->sched == 1 ? std::max(0, env_int_api("LFM_S1_MASK_CUS", 0)) : 0;
+  if (ctx->s1_mask > 0 && ctx->s1_mask < ctx->cus) {
+    std::vector<uint32_t> mk((ctx->cus + 31) / 32, 0u);
+    for (int c = ctx->s1_mask; c < ctx->cus; ++c) mk[c / 32] |= 1u << (c % 32);
+    return hipExtStreamCreateWithCUMask(&ctx->stream, (uint32_t)mk.size(), mk.data());
+  }
+  ctx->s1_mask = 0;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e != hipSuccess || ctx->sched != 3) return e;
   return create_partition(ctx, ctx->side_req);

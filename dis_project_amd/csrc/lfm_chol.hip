@@ -2373,11 +2373,19 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     if (r) return r;
   }
   if (!s3 && !ctx->side) {
-    // schedule 1's high-priority side stream, created on first use (schedule 3 never needs it)
+    // schedule 1's high-priority side stream, created on first use (schedule 3 never needs it);
+    // a CU-masked schedule-1 context (LFM_S1_MASK_CUS) masks it the same way instead
     int least = 0, greatest = 0;
     hipDeviceGetStreamPriorityRange(&least, &greatest);
-    if (hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest) != hipSuccess)
-      return hip_fail(ctx, hipErrorOutOfMemory, "side stream creation");
+    hipError_t e;
+    if (ctx->s1_mask > 0) {
+      std::vector<uint32_t> mk((ctx->cus + 31) / 32, 0u);
+      for (int c = ctx->s1_mask; c < ctx->cus; ++c) mk[c / 32] |= 1u << (c % 32);
+      e = hipExtStreamCreateWithCUMask(&ctx->side, (uint32_t)mk.size(), mk.data());
+    } else {
+      e = hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest);
+    }
+    if (e != hipSuccess) return hip_fail(ctx, hipErrorOutOfMemory, "side stream creation");
   }
   hipStream_t main = ctx->stream, side = ctx->side;
   hipEvent_t* ev = ctx->evs.data();  // [0]: inputs ready; E1_s = ev[1 + 2s]; E2_s = ev[2 + 2s]

@@ -50,6 +50,9 @@ struct lfm_ctx {
   hipStream_t m3 = nullptr;      // schedule 3: bulk stream (CUs outside the chain's)
   hipStream_t s3 = nullptr;      // schedule 3: factor-chain stream (LFM_SIDE_CUS CUs)
   int side_req = 32;             // LFM_SIDE_CUS at creation: the reservation to (re)create
+  // LFM_S1_MASK_CUS (A/B, schedule-1 contexts): the context's streams leave CUs [0, k) alone —
+  // a schedule-1 filler beside a schedule-3 context, off its factor chain's CUs
+  int s1_mask = 0;
   int cus = 256;                 // compute units of the device
   std::vector<hipEvent_t> evs;   // cross-stream dependency events (timing disabled)
   std::string err;

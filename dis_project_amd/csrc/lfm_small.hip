@@ -1512,14 +1512,13 @@ __global__ __launch_bounds__(256) void small_fit_kernel(FitArgs a) {
     if (bad && !first_bad) first_bad = (int)s + 1;
     if (tid == 0) a.history[s * a.nprob + b] = v;
     // the update, after_epoch on the unconstrained leaves, and the next step's constrained model,
-    // each parameter by its own thread (one barrier a step; 3G + 2 > 256 parameters, G >= 85,
-    // take a second pass)
-    const double c1 = a.bias[2 * s], c2 = a.bias[2 * s + 1];
-    const bool epoch = a.fix && (a.step0 + s) % a.spe == 0 && G > 3;
-    for (int i = tid; i < nh - 1; i += 256) {
+    // each parameter by its own thread (one barrier a step); 3G + 2 > 256 parameters (G >= 85)
+    // take a second pass
+    auto update = [&](int i) {
       const double x = m.raw[i], g = m.gout[i];
       const double sg = sigmoid_d(x);
       const double gr = i == 3 * G ? g * 3.0 * sg * (1.0 - sg) : g * sg;
+      const double c1 = a.bias[2 * s], c2 = a.bias[2 * s + 1];
       const double mu = a.b1 * m.mu[i] + (1.0 - a.b1) * gr;
       const double nu = a.b2 * m.nu[i] + (1.0 - a.b2) * (gr * gr);
       // optax's order: scale_by_adam's mu_hat / (sqrt(nu_hat + eps_root) + eps), then
@@ -1529,13 +1528,15 @@ __global__ __launch_bounds__(256) void small_fit_kernel(FitArgs a) {
       m.mu[i] = mu;
       m.nu[i] = nu;
       double xn = x + upd;
-      if (epoch) {
+      if (a.fix && (a.step0 + s) % a.spe == 0 && G > 3) {
         if (i == G + 3) xn = 1.0;  // true_s[3]
         if (i == 3) xn = 0.8;      // true_d[3]
       }
       m.raw[i] = xn;
       m.hyp[i] = constrain(i, xn);
-    }
+    };
+    if (tid < nh - 1) update(tid);
+    if (nh - 1 > 256 && tid + 256 < nh - 1) update(tid + 256);
     __syncthreads();
     fit_stamp(m, 6);
   }

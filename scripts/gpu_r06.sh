@@ -35,6 +35,23 @@ for study in "$@"; do
       $S r06_reh_c5fit 300 $R --master-port 29533 bench.py --gpus 2 --workload c5fit --steps 5 --warmup 1 \
         --share-gpus --gather gloo --no-cpu-baseline || exit $?
       ;;
+    mixed)
+      # C3: one schedule-3 evaluation at a time against it plus 1 / 2 schedule-1 fillers off the
+      # chain's CUs (bench.py --mixed), interleaved, two rounds
+      for r in 1 2; do
+        $S r06_mixed0_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --workers 1 --no-cpu-baseline || exit $?
+        $S r06_mixed1_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --mixed 1 --no-cpu-baseline || exit $?
+        $S r06_mixed2_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --mixed 2 --no-cpu-baseline || exit $?
+      done
+      ;;
+    fitab)
+      for r in 1 2; do
+        for lib in ablibs/r05/liblfm.so dis_project_amd/liblfm.so; do
+          tag=$(basename "$(dirname "$lib")")
+          LFM_LIBRARY=$lib $S r06_fitab_${tag}_$r 120 python -u bench.py --workload c5fit --steps 30 --warmup 3 --no-cpu-baseline || exit $?
+        done
+      done
+      ;;
     c2) $S r06_bench_c2 300 python -u bench.py --workload c2 --steps 20 --warmup 3 || exit $? ;;
     c3) $S r06_bench_c3 400 python -u bench.py --workload c3 --steps 5 --warmup 1 --no-cpu-baseline || exit $? ;;
     c5) $S r06_bench_c5 300 python -u bench.py --workload c5 --steps 3000 --warmup 300 || exit $? ;;
