@@ -33,7 +33,7 @@ LFM_E_OOM = 4
 LFM_E_RCCL = 5
 LFM_E_STATE = 6
 LFM_E_TIMEOUT = 7
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 LFM_UPLO_FULL = 0
 LFM_UPLO_LOWER = 1
@@ -151,6 +151,8 @@ PRODUCT_SIGNATURES = [
     ("lfm_data_create", c_int, [_c_ctx, c_void_p, c_void_p, c_int64, POINTER(c_void_p)]),
     ("lfm_data_destroy", c_int, [c_void_p]),
     ("lfm_mll_f64_data", c_int, [_c_ctx, c_void_p, POINTER(LfmHyp), c_int, _dptr]),
+    ("lfm_mll_multi_f64", c_int,
+     [_c_ctx, c_void_p, c_int64, POINTER(LfmHyp), c_int, _dptr, _dptr]),
     ("lfm_gram_f64_dev", c_int,
      [_c_ctx, c_void_p, c_int64, POINTER(LfmHyp), c_double, c_int, c_void_p, c_int64]),
     ("lfm_gram_f32_dev", c_int,

@@ -370,39 +370,47 @@ int with_s3_fallback(lfm_ctx* ctx, F&& attempt) {
   return r;
 }
 
-// Fill the lower triangle of ctx->A (lda = Mp) with Sigma = (K + jitter I) + sigma^2 I for x on
-// the device, the residual row n and identity padding; then factor and reduce.
+// Enqueue one MLL on ctx's streams: the lower triangle of ctx->A (lda = Mp) with Sigma = (K +
+// jitter I) + sigma^2 I for x on the device (or generated inside the first update), the residual
+// row n and identity padding; then the factorisation and the reduction into ctx->result.
+int mll_enqueue(lfm_ctx* ctx, const Staged& st, const double* d_x, const double* d_y,
+                const double* d_loc, int64_t n, const lfm_hyp* hyp, int negative) {
+  const int64_t Mp = round_up(n + 1, 128);
+  const double noise = hyp->obs_stddev * hyp->obs_stddev;  // objectives.py:66
+  GramGen gen;
+  const bool fuse = chol_fuses_gram(ctx, CHOL_MLL, st.lay, n);
+  int r = LFM_OK;
+  if (st.lay.ok) {
+    r = ensure(ctx, (void**)&ctx->tab, &ctx->tab_bytes,
+               tables_doubles(st.h.G, st.lay.T) * sizeof(double));
+    if (r) return r;
+    r = launch_tables(ctx, st.h, st.lay, st.d_times, ctx->tab);
+    if (r) return r;
+    // fused: the factorisation writes / generates Sigma itself (GramGen, lfm_chol.hip)
+    if (fuse) gen = GramGen{ctx->tab, st.d_bg, st.h.G, st.lay.T, hyp->jitter, noise, n};
+    else
+      r = launch_gram_grid<double>(ctx, st.h, st.lay, ctx->tab, st.d_bg, n, hyp->jitter, noise,
+                                   LFM_UPLO_LOWER, ctx->A, Mp);
+  } else {
+    r = launch_gram_direct<double>(ctx, st.h, d_x, n, d_x, n, hyp->jitter, noise,
+                                   LFM_UPLO_LOWER, ctx->A, Mp);
+  }
+  if (r) return r;
+  r = launch_augment(ctx, st.h, d_x, d_y, d_loc, n, ctx->A, Mp, Mp);
+  if (r) return r;
+  return chol_factor_solve(ctx, ctx->A, Mp, n, Mp, negative, ctx->result, CHOL_MLL,
+                           fuse ? &gen : nullptr);
+}
+
+// mll_enqueue, then the result to the host (synchronous).
 int mll_blocked(lfm_ctx* ctx, const Staged& st, const double* d_x, const double* d_y,
                 const double* d_loc, int64_t n, const lfm_hyp* hyp, int negative, double* out) {
   const int64_t Mp = round_up(n + 1, 128);
   int r = ensure(ctx, (void**)&ctx->A, &ctx->A_bytes, (size_t)Mp * Mp * sizeof(double));
   if (r) return r;
-  const double noise = hyp->obs_stddev * hyp->obs_stddev;  // objectives.py:66
   DeviceTenancy tenancy(ctx, s3_on(ctx));  // held to the final synchronise (finish)
   return with_s3_fallback(ctx, [&]() -> int {
-    GramGen gen;
-    const bool fuse = chol_fuses_gram(ctx, CHOL_MLL, st.lay, n);
-    int r = LFM_OK;
-    if (st.lay.ok) {
-      r = ensure(ctx, (void**)&ctx->tab, &ctx->tab_bytes,
-                 tables_doubles(st.h.G, st.lay.T) * sizeof(double));
-      if (r) return r;
-      r = launch_tables(ctx, st.h, st.lay, st.d_times, ctx->tab);
-      if (r) return r;
-      // fused: the factorisation writes / generates Sigma itself (GramGen, lfm_chol.hip)
-      if (fuse) gen = GramGen{ctx->tab, st.d_bg, st.h.G, st.lay.T, hyp->jitter, noise, n};
-      else
-        r = launch_gram_grid<double>(ctx, st.h, st.lay, ctx->tab, st.d_bg, n, hyp->jitter, noise,
-                                     LFM_UPLO_LOWER, ctx->A, Mp);
-    } else {
-      r = launch_gram_direct<double>(ctx, st.h, d_x, n, d_x, n, hyp->jitter, noise,
-                                     LFM_UPLO_LOWER, ctx->A, Mp);
-    }
-    if (r) return r;
-    r = launch_augment(ctx, st.h, d_x, d_y, d_loc, n, ctx->A, Mp, Mp);
-    if (r) return r;
-    r = chol_factor_solve(ctx, ctx->A, Mp, n, Mp, negative, ctx->result, CHOL_MLL,
-                          fuse ? &gen : nullptr);
+    int r = mll_enqueue(ctx, st, d_x, d_y, d_loc, n, hyp, negative);
     if (r) return r;
     double* hres = ctx->hpin + (ctx->hpin_bytes / 8 - 8);
     hipMemcpyAsync(hres, ctx->result, 5 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
@@ -635,7 +643,9 @@ hipError_t create_partition(lfm_ctx* ctx, int side_cus) {
 // CU-masked queues of other contexts in the process oversubscribe the hardware scheduler —
 // one schedule-1 evaluation at a time ran 23.3 evals/s beside three idle partitioned contexts
 // against 29.1 alone.
+void twins_drop(lfm_ctx* ctx);
 void release_partition(lfm_ctx* ctx) {
+  twins_drop(ctx);  // they borrow the pair
   for (hipStream_t* st : {&ctx->s3, &ctx->m3})
     if (*st) {
       hipStreamSynchronize(*st);
@@ -670,6 +680,9 @@ void release_partition(lfm_ctx* ctx) {
 //                        replayed as one captured graph
 //   LFM_S1_MASK_CUS      (A/B) a schedule-1 context's streams avoid CUs [0, k) (CU-masked,
 //                        without the side stream's priority)
+//   LFM_OVERLAP / LFM_OVL_AT / LFM_OVL_RESERVE   lfm_mll_multi_f64's restart pipeline: on/off,
+//                        the trailing rows below which an evaluation's tail starts (the next one's
+//                        prologue may run), main CUs the overlap stream leaves to that tail
 // Every knob is read here, once: a call never consults the environment.
 hipError_t create_streams(lfm_ctx* ctx) {
   ctx->sched = env_int_api("LFM_SCHED", 3) == 1 ? 1 : 3;
@@ -698,6 +711,9 @@ hipError_t create_streams(lfm_ctx* ctx) {
   if (const char* sl = std::getenv("LFM_DEBUG_SPIN_LIMIT"))
     ctx->wait_ticks = (unsigned)std::strtoul(sl, nullptr, 10);
   ctx->side_req = env_int_api("LFM_SIDE_CUS", 32);
+  ctx->ovl_on = env_int_api("LFM_OVERLAP", 1);
+  ctx->ovl_at = env_int_api("LFM_OVL_AT", 6144);
+  ctx->ovl_reserve = std::max(0, env_int_api("LFM_OVL_RESERVE", 64));
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, ctx->device);
   if (prop.multiProcessorCount > 0) ctx->cus = prop.multiProcessorCount;
@@ -764,6 +780,13 @@ int lfm_ctx_create(int device, lfm_ctx** out) {
 void lfm_ctx_destroy(lfm_ctx* ctx) {
   if (!ctx) return;
   hipSetDevice(ctx->device);
+  twins_drop(ctx);
+  if (ctx->borrowed) {
+    // a restart-pipeline workspace: its streams are its primary's (drained by twins_drop)
+    ctx->stream = ctx->m3 = ctx->s3 = nullptr;
+    for (hipEvent_t e : {ctx->ovl_tail, ctx->ovl_done, ctx->ovl_res})
+      if (e) hipEventDestroy(e);
+  }
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
   lfm_farm_destroy(ctx);
   for (void* p : {(void*)ctx->A, (void*)ctx->tab, (void*)ctx->tab32, (void*)ctx->par,
@@ -1179,6 +1202,206 @@ int lfm_mll_f64_data(lfm_ctx* ctx, lfm_data* data, const lfm_hyp* hyp, int negat
   r = stage_hyp(ctx, hyp, data->xh.data(), n, true, &st, &data->lay);
   if (r) return r;
   return mll_blocked(ctx, st, data->d_x, data->d_y, nullptr, n, hyp, negative, out);
+}
+
+}  // extern "C"
+
+namespace {
+// ------------------------------------------------------ C3 restart pipeline
+// Workspace i of ctx's restart pipeline (lfm_mll_multi_f64): an lfm_ctx with its own buffers,
+// events and flags, whose streams are ctx's — m3 / s3 (in stream order after the previous
+// evaluation's launches) and the overlap stream (CU-masked: every CU outside the chain's and the
+// first LFM_OVL_RESERVE main CUs, which the previous evaluation's tail keeps).
+int twin_get(lfm_ctx* ctx, int i, lfm_ctx** out) {
+  if (ctx->twin[i]) {
+    *out = ctx->twin[i];
+    return LFM_OK;
+  }
+  if (!ctx->ovl_stream) {
+    const int lo = std::min(ctx->cus - 64, ctx->side_cus + ctx->ovl_reserve);
+    std::vector<uint32_t> mk((ctx->cus + 31) / 32, 0u);
+    for (int c = lo; c < ctx->cus; ++c) mk[c / 32] |= 1u << (c % 32);
+    hipError_t e = hipExtStreamCreateWithCUMask(&ctx->ovl_stream, (uint32_t)mk.size(), mk.data());
+    if (e != hipSuccess) {
+      ctx->ovl_stream = nullptr;
+      return hip_fail(ctx, e, "overlap stream");
+    }
+  }
+  std::unique_ptr<lfm_ctx> t(new lfm_ctx());
+  t->borrowed = true;
+  t->device = ctx->device;
+  t->stream = ctx->ovl_stream;
+  t->m3 = ctx->m3;
+  t->s3 = ctx->s3;
+  t->side_req = ctx->side_req;
+  t->side_cus = ctx->side_cus;
+  t->cus = ctx->cus;
+  t->sched = 3;
+  t->wait_ticks = ctx->wait_ticks;
+  t->grad_direct = ctx->grad_direct;
+  t->gram_fuse = ctx->gram_fuse;
+  t->w4min = ctx->w4min;
+  t->w2min = ctx->w2min;
+  t->w0 = ctx->w0;
+  t->helper = ctx->helper;
+  t->helper_tc = ctx->helper_tc;
+  t->helper_min = ctx->helper_min;
+  t->s3_fallback = false;  // lfm_mll_multi_f64 re-runs a stalled set itself
+  t->ovl_at = ctx->ovl_at;
+  std::memset(t->stats, 0, sizeof(t->stats));
+  hipError_t e = hipMalloc((void**)&t->linvT, 128 * 128 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&t->status, 64);
+  if (e == hipSuccess) e = hipMalloc((void**)&t->result, 64 * sizeof(double));
+  if (e == hipSuccess) e = hipMalloc((void**)&t->psync, 64);
+  if (e == hipSuccess) e = hipMemsetAsync(t->psync, 0, 64, t->stream);
+  for (hipEvent_t* ev : {&t->ovl_tail, &t->ovl_done, &t->ovl_res})
+    if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipStreamSynchronize(t->stream);
+  if (e != hipSuccess) {
+    lfm_ctx_destroy(t.release());
+    return hip_fail(ctx, e, "restart pipeline workspace");
+  }
+  *out = ctx->twin[i] = t.release();
+  return LFM_OK;
+}
+
+// Drain and free the pipeline's workspaces and its overlap stream (the pair they borrow is
+// about to go, or the context is).
+void twins_drop(lfm_ctx* ctx) {
+  if (!ctx->twin[0] && !ctx->twin[1] && !ctx->ovl_stream) return;
+  for (hipStream_t st : {ctx->ovl_stream, ctx->m3, ctx->s3, ctx->stream})
+    if (st) hipStreamSynchronize(st);
+  for (lfm_ctx*& t : ctx->twin) {
+    lfm_ctx_destroy(t);
+    t = nullptr;
+  }
+  if (ctx->ovl_stream) hipStreamDestroy(ctx->ovl_stream);
+  ctx->ovl_stream = nullptr;
+}
+}  // namespace
+
+extern "C" {
+
+// C3 (BASELINE.json configs[2]): nsets hyperparameter sets on one resident dataset. On schedule
+// 3 the evaluations are pipelined over two workspaces: evaluation k + 1's prologue (staging, its
+// gram tables / region, chain(0), X_0, chain(1) and step 0) runs on the overlap stream while
+// evaluation k is in its chain-bound tail, and the rest of it follows evaluation k's launches
+// on the partitioned pair. Every evaluation runs the same kernels on the same inputs as
+// lfm_mll_f64_data: the values are bit-identical. Otherwise (small n, schedule 1, profiling,
+// LFM_OVERLAP=0, differing gene counts) the sets are evaluated one by one.
+int lfm_mll_multi_f64(lfm_ctx* ctx, lfm_data* data, int64_t nsets, const lfm_hyp* hyps,
+                      int negative, double* out, int* status) {
+  if (!ctx) return LFM_E_ARG;
+  if (!data || !out || nsets < 0 || (nsets > 0 && !hyps))
+    return set_err(ctx, LFM_E_ARG, "data / hyps / out is NULL or nsets < 0");
+  if (data->device != ctx->device) return set_err(ctx, LFM_E_ARG, "dataset of another device");
+  const int64_t n = data->n;
+  bool same_genes = true;
+  for (int64_t k = 0; k < nsets; ++k) {
+    int r = check_hyp(ctx, &hyps[k]);
+    if (!r) r = check_mean_shape(ctx, n, &hyps[k]);
+    if (r) return r;
+    same_genes = same_genes && hyps[k].num_genes == hyps[0].num_genes;
+  }
+  DeviceGuard g(ctx->device);
+  int worst = LFM_OK;
+  // one set through lfm_mll_f64_data (its own schedule-3 fallback): NOT_PD -> NaN and status
+  auto one = [&](int64_t k) -> int {
+    int r = lfm_mll_f64_data(ctx, data, &hyps[k], negative, &out[k]);
+    if (status) status[k] = r;
+    if (r == LFM_E_NOT_PD) {
+      out[k] = std::nan("");
+      worst = LFM_E_NOT_PD;
+      return LFM_OK;
+    }
+    return r;
+  };
+  const bool pipelined = nsets >= 2 && n > SMALL_MAX && ctx->ovl_on && s3_on(ctx) &&
+                         !ctx->prof && ctx->s3_events == 0 && !ctx->dbg_stamps &&
+                         !ctx->dbg_trace && same_genes;
+  if (!pipelined) {
+    for (int64_t k = 0; k < nsets; ++k)
+      if (int r = one(k)) return r;
+    if (worst) set_err(ctx, LFM_E_NOT_PD, "Cholesky failed for at least one hyperparameter set");
+    return worst;
+  }
+  if (data->lay_G != hyps[0].num_genes) {
+    data->lay = detect_grid(data->xh.data(), n, hyps[0].num_genes);
+    data->lay_G = hyps[0].num_genes;
+  }
+  DeviceTenancy tenancy(ctx, true);  // exclusive, to the last result
+  const int64_t Mp = round_up(n + 1, 128);
+  lfm_ctx* tw[2];
+  for (int i = 0; i < 2; ++i) {
+    int r = twin_get(ctx, i, &tw[i]);
+    if (!r) r = ensure(tw[i], (void**)&tw[i]->A, &tw[i]->A_bytes, (size_t)Mp * Mp * sizeof(double));
+    if (!r) r = ensure_pinned(tw[i], 1 << 16);
+    if (r) {
+      if (r != LFM_E_ARG) ctx->err = tw[i]->err.empty() ? ctx->err : tw[i]->err;
+      return r;
+    }
+  }
+  auto hres = [&](lfm_ctx* t) { return t->hpin + (t->hpin_bytes / 8 - 8); };
+  // enqueue set k on workspace k % 2, its prologue gated on set k - 1's tail
+  auto enqueue = [&](int64_t k) -> int {
+    lfm_ctx* t = tw[k & 1];
+    t->ovl = true;
+    t->err.clear();
+    if (k > 0) hipStreamWaitEvent(t->stream, tw[(k - 1) & 1]->ovl_tail, 0);
+    Staged st;
+    int r = stage_hyp(t, &hyps[k], data->xh.data(), n, true, &st, &data->lay);
+    if (!r) r = mll_enqueue(t, st, data->d_x, data->d_y, nullptr, n, &hyps[k], negative);
+    if (!r) {
+      hipStreamWaitEvent(ctx->stream, t->ovl_done, 0);
+      hipMemcpyAsync(hres(t), t->result, 5 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream);
+      hipEventRecord(t->ovl_res, ctx->stream);
+      r = hip_fail(ctx, hipGetLastError(), "restart pipeline enqueue");
+    } else {
+      ctx->err = t->err;
+    }
+    return r;
+  };
+  // the host side of set k: LFM_OK / LFM_E_NOT_PD (NaN), LFM_E_TIMEOUT (the caller re-runs)
+  auto collect = [&](int64_t k) -> int {
+    lfm_ctx* t = tw[k & 1];
+    hipError_t e = hipEventSynchronize(t->ovl_res);
+    if (e != hipSuccess) return hip_fail(ctx, e, "restart pipeline result");
+    const double* h = hres(t);
+    out[k] = h[0];
+    int r = status_code(t, h[3], h[4]);
+    if (status) status[k] = r;
+    if (r == LFM_E_NOT_PD) {
+      out[k] = std::nan("");
+      worst = LFM_E_NOT_PD;
+      r = LFM_OK;
+    }
+    if (r) ctx->err = t->err;
+    return r;
+  };
+  auto drain = [&] {
+    for (hipStream_t st : {ctx->ovl_stream, ctx->m3, ctx->s3, ctx->stream}) hipStreamSynchronize(st);
+    tw[0]->ovl = tw[1]->ovl = false;
+  };
+  int64_t done = 0;  // sets collected
+  int r = enqueue(0);
+  for (int64_t k = 1; !r && k <= nsets; ++k) {
+    if (k < nsets) r = enqueue(k);
+    if (!r) {
+      r = collect(k - 1);
+      if (!r) done = k;
+    }
+  }
+  drain();
+  if (r == LFM_E_TIMEOUT) {
+    // a device-side wait ran out (another tenant starved the chain): the rest one by one,
+    // each with lfm_mll_f64_data's own schedule-1 re-run
+    ctx->fallbacks += 1;
+    r = LFM_OK;
+    for (int64_t k = done; !r && k < nsets; ++k) r = one(k);
+  }
+  if (r) return r;
+  if (worst) set_err(ctx, LFM_E_NOT_PD, "Cholesky failed for at least one hyperparameter set");
+  return worst;
 }
 
 int lfm_mll_batch_f64(lfm_ctx* ctx, int64_t nprob, const lfm_problem* probs, int negative,

@@ -2403,10 +2403,14 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     // columns first, then the rest) and finishes with X_{s+1} = A21 Bd_{s+1}, the tall panel
     // solve as a GEMM, once the side stream's factor of block s + 1 has landed. Cross-stream
     // order within a step is by device flags (ctx->flags), reset per call.
+    // overlapped (a twin workspace of lfm_mll_multi_f64, ctx->ovl): chain(0), X_0, chain(1) and
+    // launch 0 run on ctx->stream (the primary's overlap stream, behind this evaluation's gram),
+    // the rest on the shared pair, after them and after the previous evaluation's launches
+    const bool ovl = ctx->ovl && ctx->s3_events == 0 && S >= 2;
     hipEventRecord(ev[0], ctx->stream);
     main = ctx->m3;
     side = ctx->s3;
-    hipStreamWaitEvent(main, ev[0], 0);
+    if (!ovl) hipStreamWaitEvent(main, ev[0], 0);
     // the trailing matrix of a step whose super-panel ends at column K1: rows / columns
     // [K1, Mp) (MLL), or the Mp-row window [K1, K1 + Mp) the identity border has reached
     // (bordered: rows Mp + j are zero in panel columns < j; the window size is constant)
@@ -2431,7 +2435,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     if (r) return r;
     unsigned* chain_done = ctx->flags;     // [S]
     unsigned* a_done = ctx->flags + S;     // [S][Tmax]
-    hipMemsetAsync(ctx->flags, 0, nflags * sizeof(unsigned), main);
+    hipMemsetAsync(ctx->flags, 0, nflags * sizeof(unsigned), ovl ? ctx->stream : main);
     zsplit = n;
     auto xbuf = [&](int s) { return ctx->xbuf + (size_t)(s & 1) * Mp * Wmax; };
     unsigned* bars = a_done + (size_t)S * Tmax;  // [S] grid barrier counters of chain(s)
@@ -2575,8 +2579,13 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     };
     // side: chain(0) after the gram; every later chain(s) follows chain(s - 1) in stream order
     // and waits on the device for its inputs (xready[s]) from the main launch in flight
-    hipEventRecord(ev[0], main);
-    hipStreamWaitEvent(side, ev[0], 0);
+    if (ovl) {
+      main = side = ctx->stream;
+    } else {
+      hipEventRecord(ev[0], main);
+      hipStreamWaitEvent(side, ev[0], 0);
+    }
+    bool tail_marked = false;
     if (ctx->s3_events == 1) {
       // The same work ordered by stream events only (tall units in launches of their own after
       // the factor's event, chains after the tall launch's event) — for tools that serialise
@@ -2674,8 +2683,21 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         const double alg_h =
             ctx->prof && hu > 0 ? units_alg(g.s0, g.T, g.wn, g.kd, total - hu, total) : 0.0;
         if (helped) hipStreamWaitEvent(main, evH[2 * (s - 1)], 0);
+        // overlapped: the next evaluation may start once the launches before this evaluation's
+        // tail have run (its first step below LFM_OVL_AT trailing rows)
+        if (ctx->ovl && !tail_marked && s >= 1 && rows_end(g.s0) - g.s0 < ctx->ovl_at) {
+          hipEventRecord(ctx->ovl_tail, main);
+          tail_marked = true;
+        }
         launch_step(g, alg_h);
         hipEventRecord(evL[2 * s], main);
+        if (ovl && s == 0) {
+          // the overlapped prologue ends with launch 0: the pair takes over after it
+          main = ctx->m3;
+          side = ctx->s3;
+          hipStreamWaitEvent(main, evL[0], 0);
+          hipStreamWaitEvent(side, evL[0], 0);
+        }
         helped = hu > 0;
         if (hu > 0) {
           StepArgs h = g;
@@ -2702,6 +2724,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         launch_step(g);
       }
     }
+    if (ctx->ovl && !tail_marked) hipEventRecord(ctx->ovl_tail, main);
     hipEventRecord(ev[2 * S + 1], side);
     hipStreamWaitEvent(main, ev[2 * S + 1], 0);
   } else {
@@ -2744,7 +2767,11 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(1024), 0, main, A, lda, n, ctx->parts,
                      (int)npb, ctx->status, negative, d_out, ctx->zvec, zsplit);
   prof_end(ctx, K_FINALIZE, pe, 0, (double)n * 8, main);
-  if (main != ctx->stream) {  // schedule 3 ran on the partitioned pair: back to ctx->stream
+  if (ctx->ovl) {
+    // overlapped: the caller reads the result after ovl_done; ctx->stream (the overlap stream)
+    // must not wait, the next evaluation's prologue is queued on it
+    hipEventRecord(ctx->ovl_done, main);
+  } else if (main != ctx->stream) {  // schedule 3 ran on the partitioned pair: back to ctx->stream
     hipEventRecord(ev[2 * S + 2], main);
     hipStreamWaitEvent(ctx->stream, ev[2 * S + 2], 0);
   }

@@ -198,209 +198,7 @@ __global__ __launch_bounds__(256) void gram_grid_aligned_kernel(
 }
 
 #ifdef LFM_GRAM_AB
-// A/B build only (make EXTRA=-DLFM_GRAM_AB; scripts/gram_ab.py, LFM_GRAM_AB=<mode> read per
-// call): store-shape variants of gram_grid_aligned_kernel, same tile, same arithmetic.
-//   1: 128 threads, a lane owns columns 2 l, 2 l + 1 (one 2-element vector store per row)
-//   2: 256 threads, wave w sweeps rows w, w + 4, ...: four 256-B stores cover a row's 1 KB
-//   3: 128 threads, wave w sweeps rows w, w + 2, ...: two 2-element vector stores per row
-//   5: the baseline's tiles and stores with nothing computed or staged (the value is the row
-//      index): the floor of this store pattern (results invalid)
-//   4: the baseline's body in a persistent grid (LFM_GRAM_AB_WG workgroups, default 2048) that
-//      strides over the tiles, one barrier before each restage
-template <typename T, int MODE>
-__global__ __launch_bounds__(MODE == 2 ? 256 : 128) void gram_ab_kernel(
-    const T* __restrict__ tab, int G, int Tn, const int* __restrict__ bg, int64_t n, T da1, T da2,
-    int lower, T* __restrict__ out, int64_t ldo) {
-  constexpr int R = 64, C = 256, WIN = C + R - 1, NT = MODE == 2 ? 256 : 128;
-  __shared__ T sWk[WIN + 1], sXk[WIN + 1], sWj[WIN + 1], sXj[WIN + 1];
-  __shared__ T sPk[R], sEj[R], sQj[R], sEk[C], sQk[C], sPj[C];
-  int64_t c0, r0;
-  if (lower) {
-    const int64_t b = blockIdx.x;
-    int64_t q = (int64_t)((sqrt(2.0 * (double)b + 1.0) - 1.0) * 0.5);
-    while (2 * (q + 1) * (q + 2) <= b) ++q;
-    while (2 * q * (q + 1) > b) --q;
-    const int64_t off = b - 2 * q * (q + 1);
-    r0 = (4 * q + off / (q + 1)) * R;
-    c0 = (off % (q + 1)) * C;
-  } else {
-    c0 = (int64_t)blockIdx.x * C;
-    r0 = (int64_t)blockIdx.y * R;
-  }
-  const int tid = threadIdx.x;
-  const int W = 2 * Tn - 1;
-  const T* Wt = tab;
-  const T* Xt = Wt + (int64_t)G * W;
-  const T* Pt = Xt + (int64_t)G * W;
-  const T* Et = Pt + (int64_t)G * Tn;
-  const T* Qt = Et + (int64_t)G * Tn;
-  const T* Cm = Qt + (int64_t)G * Tn;
-  const int j = bg[r0 / Tn], k = bg[c0 / Tn];
-  const int tau0 = (int)(r0 % Tn), tp0 = (int)(c0 % Tn);
-  const int dmin = tp0 - tau0 - (R - 1);
-  for (int e = tid; e < WIN; e += NT) {
-    const int d = dmin + e;
-    sWk[e] = Wt[(int64_t)k * W + (Tn - 1) + d];
-    sXk[e] = Xt[(int64_t)k * W + (Tn - 1) + d];
-    sWj[e] = Wt[(int64_t)j * W + (Tn - 1) - d];
-    sXj[e] = Xt[(int64_t)j * W + (Tn - 1) - d];
-  }
-  if (tid < R) {
-    sPk[tid] = Pt[(int64_t)k * Tn + tau0 + tid];
-    sEj[tid] = Et[(int64_t)j * Tn + tau0 + tid];
-    sQj[tid] = Qt[(int64_t)j * Tn + tau0 + tid];
-  }
-  for (int x = tid; x < C; x += NT) {
-    sEk[x] = Et[(int64_t)k * Tn + tp0 + x];
-    sQk[x] = Qt[(int64_t)k * Tn + tp0 + x];
-    sPj[x] = Pt[(int64_t)j * Tn + tp0 + x];
-  }
-  const T Cjk = Cm[(int64_t)j * G + k];
-  __syncthreads();
-  auto elem = [&](int i, int x) {
-    const int e = x + (R - 1) - i;
-    T v = sWk[e] + sWj[e];
-    v = fma(-sXk[e], sPk[i], v);
-    v = fma(-sXj[e], sPj[x], v);
-    v = fma(-(sEk[x] * sEj[i]), sQk[x] + sQj[i], v);
-    v = Cjk * v;
-    if (r0 + i == c0 + x) v = (v + da1) + da2;
-    return v;
-  };
-  using V2 = T __attribute__((ext_vector_type(2)));
-  const int lane = tid & 63, w = tid >> 6;
-  if constexpr (MODE == 1 || MODE == 3) {
-    constexpr int RS = MODE == 1 ? 1 : 2;  // rows per sweep step
-    constexpr int CS = MODE == 1 ? 1 : 2;  // vector stores per row
-    const int xb = MODE == 1 ? 2 * tid : 2 * lane;
-    for (int ii = MODE == 1 ? 0 : w; ii < R; ii += RS) {
-      const int64_t row = r0 + ii;
-#pragma unroll
-      for (int s = 0; s < CS; ++s) {
-        const int x = xb + 128 * s;
-        const int64_t c = c0 + x;
-        if (lower && c > row) continue;
-        const T v0 = elem(ii, x);
-        T* p = out + row * ldo + c;
-        if (!lower || c + 1 <= row) {
-          V2 v;
-          v.x = v0;
-          v.y = elem(ii, x + 1);
-          *(V2*)p = v;
-        } else {
-          *p = v0;
-        }
-      }
-    }
-  } else {
-    for (int ii = w; ii < R; ii += 4) {
-      const int64_t row = r0 + ii;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int x = lane + 64 * s;
-        const int64_t c = c0 + x;
-        if (lower && c > row) continue;
-        out[row * ldo + c] = elem(ii, x);
-      }
-    }
-  }
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void gram_ab_store_kernel(int64_t n, int lower, T* __restrict__ out,
-                                                            int64_t ldo) {
-  constexpr int R = 64, C = 256;
-  int64_t c0, r0;
-  if (lower) {
-    const int64_t b = blockIdx.x;
-    int64_t q = (int64_t)((sqrt(2.0 * (double)b + 1.0) - 1.0) * 0.5);
-    while (2 * (q + 1) * (q + 2) <= b) ++q;
-    while (2 * q * (q + 1) > b) --q;
-    const int64_t off = b - 2 * q * (q + 1);
-    r0 = (4 * q + off / (q + 1)) * R;
-    c0 = (off % (q + 1)) * C;
-  } else {
-    c0 = (int64_t)blockIdx.x * C;
-    r0 = (int64_t)blockIdx.y * R;
-  }
-  const int64_t c = c0 + threadIdx.x;
-  T* op = out + r0 * ldo + c;
-#pragma unroll 4
-  for (int i = 0; i < R; ++i) {
-    const int64_t row = r0 + i;
-    if (lower && c > row) continue;
-    op[(int64_t)i * ldo] = (T)row;
-  }
-}
-
-template <typename T>
-__global__ __launch_bounds__(256) void gram_ab_persist_kernel(
-    const T* __restrict__ tab, int G, int Tn, const int* __restrict__ bg, int64_t n, T da1, T da2,
-    int lower, T* __restrict__ out, int64_t ldo, int64_t ntiles) {
-  constexpr int R = 64, C = 256, WIN = C + R - 1;
-  __shared__ T sWk[WIN], sXk[WIN], sWj[WIN], sXj[WIN];
-  __shared__ T sPk[R], sEj[R], sQj[R];
-  const int tid = threadIdx.x;
-  const int W = 2 * Tn - 1;
-  const T* Wt = tab;
-  const T* Xt = Wt + (int64_t)G * W;
-  const T* Pt = Xt + (int64_t)G * W;
-  const T* Et = Pt + (int64_t)G * Tn;
-  const T* Qt = Et + (int64_t)G * Tn;
-  const T* Cm = Qt + (int64_t)G * Tn;
-  const int64_t ntc = n / C;
-  for (int64_t b = blockIdx.x; b < ntiles; b += gridDim.x) {
-    int64_t c0, r0;
-    if (lower) {
-      int64_t q = (int64_t)((sqrt(2.0 * (double)b + 1.0) - 1.0) * 0.5);
-      while (2 * (q + 1) * (q + 2) <= b) ++q;
-      while (2 * q * (q + 1) > b) --q;
-      const int64_t off = b - 2 * q * (q + 1);
-      r0 = (4 * q + off / (q + 1)) * R;
-      c0 = (off % (q + 1)) * C;
-    } else {
-      c0 = (b % ntc) * C;
-      r0 = (b / ntc) * R;
-    }
-    const int j = bg[r0 / Tn], k = bg[c0 / Tn];
-    const int tau0 = (int)(r0 % Tn), tp0 = (int)(c0 % Tn);
-    const int dmin = tp0 - tau0 - (R - 1);
-    __syncthreads();  // the previous tile's reads of the windows are done
-    for (int e = tid; e < WIN; e += 256) {
-      const int d = dmin + e;
-      sWk[e] = Wt[(int64_t)k * W + (Tn - 1) + d];
-      sXk[e] = Xt[(int64_t)k * W + (Tn - 1) + d];
-      sWj[e] = Wt[(int64_t)j * W + (Tn - 1) - d];
-      sXj[e] = Xt[(int64_t)j * W + (Tn - 1) - d];
-    }
-    if (tid < R) {
-      sPk[tid] = Pt[(int64_t)k * Tn + tau0 + tid];
-      sEj[tid] = Et[(int64_t)j * Tn + tau0 + tid];
-      sQj[tid] = Qt[(int64_t)j * Tn + tau0 + tid];
-    }
-    const int tp = tp0 + tid;
-    const T Ek = Et[(int64_t)k * Tn + tp];
-    const T Qk = Qt[(int64_t)k * Tn + tp];
-    const T Pj = Pt[(int64_t)j * Tn + tp];
-    const T Cjk = Cm[(int64_t)j * G + k];
-    __syncthreads();
-    const int64_t c = c0 + tid;
-    T* op = out + r0 * ldo + c;
-#pragma unroll 4
-    for (int i = 0; i < R; ++i) {
-      const int64_t row = r0 + i;
-      if (lower && c > row) continue;
-      const int e = tid + (R - 1) - i;
-      T v = sWk[e] + sWj[e];
-      v = fma(-sXk[e], sPk[i], v);
-      v = fma(-sXj[e], Pj, v);
-      v = fma(-(Ek * sEj[i]), Qk + sQj[i], v);
-      v = Cjk * v;
-      if (row == c) v = (v + da1) + da2;
-      op[(int64_t)i * ldo] = v;
-    }
-  }
-}
+#include "lfm_gram_ab.inc"  // A/B-only store-shape variants (make EXTRA=-DLFM_GRAM_AB)
 #endif
 
 __global__ void f64_to_f32_kernel(const double* __restrict__ a, float* __restrict__ b, int64_t n) {
@@ -434,29 +232,7 @@ int launch_gram_grid(lfm_ctx* ctx, const HypDev& h, const GridLayout& lay, const
     const int64_t Q = n / 256;
     dim3 grid = lower ? dim3((unsigned)(2 * Q * (Q + 1))) : dim3((unsigned)(n / 256), (unsigned)(n / 64));
 #ifdef LFM_GRAM_AB
-    const char* abm = getenv("LFM_GRAM_AB");
-    const int mode = abm ? atoi(abm) : 0;
-    if (mode == 1)
-      hipLaunchKernelGGL((gram_ab_kernel<OutT, 1>), grid, dim3(128), 0, ctx->stream, tabT, h.G,
-                         lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out, ldo);
-    else if (mode == 2)
-      hipLaunchKernelGGL((gram_ab_kernel<OutT, 2>), grid, dim3(256), 0, ctx->stream, tabT, h.G,
-                         lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out, ldo);
-    else if (mode == 3)
-      hipLaunchKernelGGL((gram_ab_kernel<OutT, 3>), grid, dim3(128), 0, ctx->stream, tabT, h.G,
-                         lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out, ldo);
-    else if (mode == 5)
-      hipLaunchKernelGGL((gram_ab_store_kernel<OutT>), grid, dim3(256), 0, ctx->stream, n, lower,
-                         out, ldo);
-    else if (mode == 4) {
-      const char* wg = getenv("LFM_GRAM_AB_WG");
-      const int64_t nt = (int64_t)grid.x * grid.y;
-      const int64_t g = std::min<int64_t>(nt, wg ? atoll(wg) : 2048);
-      hipLaunchKernelGGL((gram_ab_persist_kernel<OutT>), dim3((unsigned)g), dim3(256), 0,
-                         ctx->stream, tabT, h.G, lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out,
-                         ldo, nt);
-    }
-    else
+    if (!gram_ab_launch<OutT>(ctx, grid, tabT, h, lay.T, bg, n, da1, da2, lower, out, ldo))
 #endif
     hipLaunchKernelGGL((gram_grid_aligned_kernel<OutT>), grid, dim3(256), 0, ctx->stream, tabT,
                        h.G, lay.T, bg, n, (OutT)da1, (OutT)da2, lower, out, ldo);

@@ -137,6 +137,24 @@ struct lfm_ctx {
   uint64_t farm_exec_batch = 0, comm_gen = 0, farm_exec_gen = 0;
   int64_t farm_exec_slots = 0;
   int farm_exec_neg = -1;
+
+  // C3's restart pipeline (lfm_mll_multi_f64): evaluation k runs on workspace
+  // twin[k % 2], whose first launches (staging, gram, chain(0), X_0, chain(1), step 0) go to the
+  // primary's overlap stream (CU-masked: the main CUs less LFM_OVL_RESERVE of them) once the
+  // previous evaluation's tail has started, and whose later launches follow the previous
+  // evaluation's in the primary's stream pair (m3 / s3, in stream order)
+  lfm_ctx* twin[2] = {nullptr, nullptr};
+  hipStream_t ovl_stream = nullptr;  // primary: the overlap stream
+  bool borrowed = false;             // twin: stream (= the primary's ovl_stream), m3, s3 borrowed
+  bool ovl = false;                  // twin: the factorisation in flight runs overlapped
+  hipEvent_t ovl_tail = nullptr;     // twin: recorded on m3 ahead of its tail's first launch
+  hipEvent_t ovl_done = nullptr;     // twin: recorded on m3 after its finalize
+  hipEvent_t ovl_res = nullptr;      // twin: its result copied to the host (primary's stream)
+  int ovl_on = 1;                    // LFM_OVERLAP: 0 evaluates lfm_mll_multi_f64's sets one by one
+  int64_t ovl_at = 5120;             // LFM_OVL_AT: the tail starts at the first step whose
+                                     // trailing matrix has fewer rows than this
+  int ovl_reserve = 64;              // LFM_OVL_RESERVE: main CUs the overlap stream leaves to the
+                                     // previous evaluation's tail
 };
 
 // ---------------------------------------------------------------- helpers

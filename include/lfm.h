@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define LFM_ABI_VERSION 4
+#define LFM_ABI_VERSION 5
 
 enum {
   LFM_OK = 0,
@@ -266,6 +266,14 @@ int lfm_data_destroy(lfm_data* data);
 /* As lfm_mll_f64_dev on a dataset handle. */
 int lfm_mll_f64_data(lfm_ctx* ctx, lfm_data* data, const lfm_hyp* hyp, int negative,
                      double* out);
+/* nsets hyperparameter sets on one dataset (the random restarts of BASELINE.json configs[2]:
+ * CustomConjMLL.step of each model in src/notebook.py:33-75's loop over one Dataset) ->
+ * out[nsets], status[nsets] (optional: LFM_OK / LFM_E_NOT_PD per set; not PD -> NaN). The
+ * values are lfm_mll_f64_data's, bit for bit. On schedule 3 the evaluations are pipelined: the
+ * next set's prologue runs while the previous set's factorisation is in its chain-bound tail
+ * (LFM_OVERLAP, default 1). Returns LFM_E_NOT_PD if any set failed. (ABI 5) */
+int lfm_mll_multi_f64(lfm_ctx* ctx, lfm_data* data, int64_t nsets, const lfm_hyp* hyps,
+                      int negative, double* out, int* status);
 /* As lfm_gram_f64 / _f32 with x and out on the device. */
 int lfm_gram_f64_dev(lfm_ctx* ctx, const double* d_x, int64_t n, const lfm_hyp* hyp,
                      double diag_add, int uplo, double* d_out, int64_t ldo);

@@ -44,6 +44,17 @@ for study in "$@"; do
         $S r06_mixed2_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --mixed 2 --no-cpu-baseline || exit $?
       done
       ;;
+    overlap)
+      # C3's restart pipeline (lfm_mll_multi_f64): its tests, then c3 lines with it off / on at
+      # several tail starts and reserves, interleaved, two rounds
+      $S r06_ovl_tests 400 python -u -m pytest tests/test_gpu_full.py -m gpu -x -v --timeout 200 --timeout-method thread -k pipeline || exit $?
+      for r in 1 2; do
+        for v in "LFM_OVERLAP=0" "LFM_OVERLAP=1" "LFM_OVL_AT=8192" "LFM_OVL_AT=4096" "LFM_OVL_RESERVE=32" "LFM_OVL_RESERVE=128"; do
+          tag=${v//=/_}
+          env $v $S r06_ovl_${tag}_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --no-cpu-baseline || exit $?
+        done
+      done
+      ;;
     fitab)
       for r in 1 2; do
         for lib in ablibs/r05/liblfm.so dis_project_amd/liblfm.so; do

@@ -22,7 +22,7 @@ def header_functions(name="lfm.h"):
 
 def test_library_builds_and_loads():
     lib = _lib.load_library()
-    assert lib.lfm_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.lfm_abi_version() == _lib.ABI_VERSION == 5
 
 
 @pytest.mark.parametrize("header,sigs", [("lfm.h", "PRODUCT_SIGNATURES"),

@@ -368,3 +368,99 @@ def test_side_cu_helper_forced_on_every_step(monkeypatch, G, T):
     assert np.isfinite(out["1"][0]) and out["1"][0] == out["0"][0]
 
 
+
+
+def _multi(ctx, data, models, negative=0):
+    from dis_project_amd import _lib
+
+    hps = [m.hyp() for m in models]
+    arr = (_lib.LfmHyp * len(hps))(*[hp.struct for hp in hps])
+    out = np.empty(len(models))
+    st = np.full(len(models), -7, np.int32)
+    rc = ctx.lib.lfm_mll_multi_f64(ctx.handle, data, len(hps), arr, negative, _lib.dptr(out),
+                                   _lib.dptr(st))
+    return rc, out, st
+
+
+@pytest.mark.parametrize("knobs", [{}, {"LFM_OVL_AT": "16384"}, {"LFM_OVERLAP": "0"}])
+def test_restart_pipeline_bit_identical(full, c2_dev, monkeypatch, knobs):
+    """C3's restart pipeline (lfm_mll_multi_f64: set k + 1's prologue — its gram tables and
+    region, chain(0), X_0, chain(1), step 0 — on the overlap stream under set k's tail, the rest
+    after set k's launches on the partitioned pair): six N = 16384 restarts, one of them not PD
+    (NaN, its status, the others unaffected), bit-identical to one lfm_mll_f64_data call each;
+    restarts 0 / 1 against the goldens. Tail start at the default 6144 rows, at 16384 (the next
+    set's prologue from the first launch on) and the pipeline off (LFM_OVERLAP=0)."""
+    from dis_project_amd import _lib, configs
+
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    _, work, dx, dy = c2_dev
+    ctx = _lib.Context(0)  # the knobs are read at context creation
+    data = _lib.c_void_p()
+    try:
+        ctx.check(ctx.lib.lfm_data_create(ctx.handle, dx, dy, work.n, _lib.ctypes.byref(data)))
+        models = configs.c3_restarts(work, 6)
+        models[3] = models[3].replace(jitter=-50.0, obs_stddev=0.0)
+        rc, got, st = _multi(ctx, data, models)
+        assert rc == _lib.LFM_E_NOT_PD and st[3] == _lib.LFM_E_NOT_PD and np.isnan(got[3])
+        assert np.all(st[[0, 1, 2, 4, 5]] == 0)
+        one = np.empty(1)
+        for k, m in enumerate(models):
+            rc1 = ctx.lib.lfm_mll_f64_data(ctx.handle, data, m.hyp().ref, 0, _lib.dptr(one))
+            if k == 3:
+                assert rc1 == _lib.LFM_E_NOT_PD
+                continue
+            ctx.check(rc1)
+            assert got[k] == one[0], (k, got[k], one[0])
+        for k, rtol in ((0, MLL_RTOL), (1, 1e-5)):
+            ref = float(full[f"c3_r{k}_mll"])
+            assert abs(got[k] - ref) <= rtol * abs(ref), (k, got[k], ref)
+        # a second call reuses the workspaces; the same bits
+        rc2, got2, _ = _multi(ctx, data, models)
+        assert rc2 == _lib.LFM_E_NOT_PD
+        np.testing.assert_array_equal(got2, got)
+        assert ctx.fallbacks == 0
+    finally:
+        if data:
+            ctx.lib.lfm_data_destroy(data)
+        ctx.close()
+
+
+def test_restart_pipeline_small_and_grid_sizes():
+    """The pipeline on an aligned grid (G = 16, T = 256: N = 4096, the fused gram) and off it
+    (G = 8, T = 100: N = 800, the separate gram fill), four sets each, bit-identical to one call
+    per set; a schedule change on the context drops the pipeline's workspaces (they borrow its
+    stream pair) and the next call rebuilds them."""
+    from dis_project_amd import _lib, configs
+
+    ctx = _lib.get_context(0)
+    for G, T in ((16, 256), (8, 100)):
+        work = configs.grid_workload(f"pipe_{G}x{T}", G, T, seed_params=7, seed_y=8)
+        x = np.ascontiguousarray(work.data.X)
+        y = np.ascontiguousarray(work.data.y.reshape(-1))
+        dx, dy, data = _lib.c_void_p(), _lib.c_void_p(), _lib.c_void_p()
+        ctx.check(ctx.lib.lfm_dev_alloc(ctx.handle, x.nbytes, _lib.ctypes.byref(dx)))
+        ctx.check(ctx.lib.lfm_dev_alloc(ctx.handle, y.nbytes, _lib.ctypes.byref(dy)))
+        try:
+            ctx.check(ctx.lib.lfm_memcpy_h2d(ctx.handle, dx, x.ctypes.data, x.nbytes))
+            ctx.check(ctx.lib.lfm_memcpy_h2d(ctx.handle, dy, y.ctypes.data, y.nbytes))
+            ctx.check(ctx.lib.lfm_data_create(ctx.handle, dx, dy, work.n, _lib.ctypes.byref(data)))
+            models = configs.c3_restarts(work, 4)
+            for rep in range(2):
+                rc, got, st = _multi(ctx, data, models, negative=1)
+                assert rc in (0, _lib.LFM_E_NOT_PD) and np.sum(st == 0) >= 2, (rc, st)
+                one = np.empty(1)
+                for k, m in enumerate(models):
+                    rc1 = ctx.lib.lfm_mll_f64_data(ctx.handle, data, m.hyp().ref, 1,
+                                                   _lib.dptr(one))
+                    assert rc1 == st[k], (G, T, k, rc1, st[k])
+                    if rc1 == 0:
+                        assert got[k] == one[0], (G, T, k, got[k], one[0])
+                if rep == 0:
+                    ctx.schedule = 1
+                    ctx.schedule = 3
+        finally:
+            if data:
+                ctx.lib.lfm_data_destroy(data)
+            ctx.lib.lfm_dev_free(ctx.handle, dx)
+            ctx.lib.lfm_dev_free(ctx.handle, dy)
