@@ -714,6 +714,8 @@ hipError_t create_streams(lfm_ctx* ctx) {
   ctx->ovl_on = env_int_api("LFM_OVERLAP", 1);
   ctx->ovl_at = env_int_api("LFM_OVL_AT", 6144);
   ctx->ovl_reserve = std::max(0, env_int_api("LFM_OVL_RESERVE", 64));
+  ctx->ovl_prio = env_int_api("LFM_OVL_PRIO", 0);
+  ctx->ovl_chains = env_int_api("LFM_OVL_CHAINS", 0);
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, ctx->device);
   if (prop.multiProcessorCount > 0) ctx->cus = prop.multiProcessorCount;
@@ -1227,8 +1229,23 @@ int twin_get(lfm_ctx* ctx, int i, lfm_ctx** out) {
       return hip_fail(ctx, e, "overlap stream");
     }
   }
+  if (ctx->ovl_chains && !ctx->ovl_chain_stream) {
+    const int lo = ctx->side_cus, hi = std::min(ctx->cus - 64, ctx->side_cus + ctx->ovl_reserve);
+    if (hi - lo < ctx->side_cus) return set_err(ctx, LFM_E_ARG, "LFM_OVL_CHAINS: reserve < side CUs");
+    std::vector<uint32_t> mk((ctx->cus + 31) / 32, 0u);
+    for (int c = lo; c < hi; ++c) mk[c / 32] |= 1u << (c % 32);
+    hipError_t e =
+        hipExtStreamCreateWithCUMask(&ctx->ovl_chain_stream, (uint32_t)mk.size(), mk.data());
+    if (e != hipSuccess) {
+      ctx->ovl_chain_stream = nullptr;
+      return hip_fail(ctx, e, "overlap chain stream");
+    }
+  }
   std::unique_ptr<lfm_ctx> t(new lfm_ctx());
   t->borrowed = true;
+  t->ovl_chain_stream = ctx->ovl_chain_stream;
+  t->ovl_prio = ctx->ovl_prio;
+  t->ovl_chains = ctx->ovl_chains;
   t->device = ctx->device;
   t->stream = ctx->ovl_stream;
   t->m3 = ctx->m3;
@@ -1268,15 +1285,18 @@ int twin_get(lfm_ctx* ctx, int i, lfm_ctx** out) {
 // Drain and free the pipeline's workspaces and its overlap stream (the pair they borrow is
 // about to go, or the context is).
 void twins_drop(lfm_ctx* ctx) {
-  if (!ctx->twin[0] && !ctx->twin[1] && !ctx->ovl_stream) return;
-  for (hipStream_t st : {ctx->ovl_stream, ctx->m3, ctx->s3, ctx->stream})
+  if (ctx->borrowed || (!ctx->twin[0] && !ctx->twin[1] && !ctx->ovl_stream)) return;
+  for (hipStream_t st : {ctx->ovl_stream, ctx->ovl_chain_stream, ctx->m3, ctx->s3, ctx->stream})
     if (st) hipStreamSynchronize(st);
   for (lfm_ctx*& t : ctx->twin) {
     lfm_ctx_destroy(t);
     t = nullptr;
   }
-  if (ctx->ovl_stream) hipStreamDestroy(ctx->ovl_stream);
-  ctx->ovl_stream = nullptr;
+  for (hipStream_t* st : {&ctx->ovl_stream, &ctx->ovl_chain_stream})
+    if (*st) {
+      hipStreamDestroy(*st);
+      *st = nullptr;
+    }
 }
 }  // namespace
 
@@ -1379,7 +1399,8 @@ int lfm_mll_multi_f64(lfm_ctx* ctx, lfm_data* data, int64_t nsets, const lfm_hyp
     return r;
   };
   auto drain = [&] {
-    for (hipStream_t st : {ctx->ovl_stream, ctx->m3, ctx->s3, ctx->stream}) hipStreamSynchronize(st);
+    for (hipStream_t st : {ctx->ovl_stream, ctx->ovl_chain_stream, ctx->m3, ctx->s3, ctx->stream})
+      if (st) hipStreamSynchronize(st);
     tw[0]->ovl = tw[1]->ovl = false;
   };
   int64_t done = 0;  // sets collected

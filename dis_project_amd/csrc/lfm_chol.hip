@@ -1324,6 +1324,8 @@ struct StepArgs {
                      // enumeration (the side-CU helper launch takes the tail of it)
   unsigned long long* trace;  // diagnostics (NULL: off): 4 words per workgroup (lfm_debug_trace)
   unsigned long long trace_tag;  // launch tag, bits 40+ of each record's last word
+  int prio;  // restart pipeline (LFM_OVL_PRIO): the tail's launches issue ahead (s_setprio 2) of
+             // the next evaluation's prologue sharing their CUs
 };
 
 // Diagnostics: atomic max of the 100 MHz clock (or of its bitwise NOT: the earliest start)
@@ -1492,6 +1494,7 @@ __device__ __forceinline__ void step_body(const StepArgs& g, unsigned long long*
   tall_or_xcd_range(seg, cnt[seg], b - base, &lo, &hi);
   const int64_t u = lo;
   if (u >= hi) return;
+  if (g.prio) __builtin_amdgcn_s_setprio(2);
   const int role = seg + 1;
   if (ran && threadIdx.x == 0) *ran = ((unsigned long long)role << 32) | (unsigned long long)u;
   unsigned long long* const st = g.stamps;
@@ -2581,6 +2584,13 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     // and waits on the device for its inputs (xready[s]) from the main launch in flight
     if (ovl) {
       main = side = ctx->stream;
+      if (ctx->ovl_chains) {
+        // the prologue's chains on their own stream (the reserve's CUs), beside X_0 / launch 0
+        // as in the unpipelined schedule (whose tall units wait for them on the device)
+        side = ctx->ovl_chain_stream;
+        hipEventRecord(ev[0], ctx->stream);
+        hipStreamWaitEvent(side, ev[0], 0);
+      }
     } else {
       hipEventRecord(ev[0], main);
       hipStreamWaitEvent(side, ev[0], 0);
@@ -2689,10 +2699,12 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
           hipEventRecord(ctx->ovl_tail, main);
           tail_marked = true;
         }
+        g.prio = ctx->ovl && tail_marked && ctx->ovl_prio ? 1 : 0;
         launch_step(g, alg_h);
         hipEventRecord(evL[2 * s], main);
         if (ovl && s == 0) {
-          // the overlapped prologue ends with launch 0: the pair takes over after it
+          // the overlapped prologue ends with launch 0: the pair takes over after it (launch
+          // 0's tall units waited for chain(1), so its chains are done too)
           main = ctx->m3;
           side = ctx->s3;
           hipStreamWaitEvent(main, evL[0], 0);

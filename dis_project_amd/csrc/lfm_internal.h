@@ -155,6 +155,9 @@ struct lfm_ctx {
                                      // trailing matrix has fewer rows than this
   int ovl_reserve = 64;              // LFM_OVL_RESERVE: main CUs the overlap stream leaves to the
                                      // previous evaluation's tail
+  int ovl_prio = 0;                  // LFM_OVL_PRIO: the tail's launches at wave priority 2
+  int ovl_chains = 0;                // LFM_OVL_CHAINS: the prologue's chains on the reserve's CUs
+  hipStream_t ovl_chain_stream = nullptr;  // primary (twins borrow it): CU-masked to the reserve
 };
 
 // ---------------------------------------------------------------- helpers
