@@ -716,6 +716,7 @@ hipError_t create_streams(lfm_ctx* ctx) {
   ctx->ovl_reserve = std::max(0, env_int_api("LFM_OVL_RESERVE", 64));
   ctx->ovl_prio = env_int_api("LFM_OVL_PRIO", 0);
   ctx->ovl_chains = env_int_api("LFM_OVL_CHAINS", 0);
+  ctx->ovl_launches = std::max(1, env_int_api("LFM_OVL_LAUNCHES", 1));
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, ctx->device);
   if (prop.multiProcessorCount > 0) ctx->cus = prop.multiProcessorCount;
@@ -1246,6 +1247,7 @@ int twin_get(lfm_ctx* ctx, int i, lfm_ctx** out) {
   t->ovl_chain_stream = ctx->ovl_chain_stream;
   t->ovl_prio = ctx->ovl_prio;
   t->ovl_chains = ctx->ovl_chains;
+  t->ovl_launches = ctx->ovl_launches;
   t->device = ctx->device;
   t->stream = ctx->ovl_stream;
   t->m3 = ctx->m3;

@@ -2685,7 +2685,8 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         // units store without write-through and bump no counter, so they never include a lead
         // tile of chain(s + 2).
         const int64_t total = g.nr;  // the step's rest enumeration
-        const int64_t hu = s >= 1 && s + 2 < S
+        const bool in_prologue = ovl && s + 1 <= std::min<int>(ctx->ovl_launches, S - 1);
+        const int64_t hu = s >= 1 && s + 2 < S && !in_prologue
                                ? helper_clamp(helper_share(g, steps[s + 1].second), (int)total,
                                               g.T, g.wn, g.xready ? g.lead : 0, LFM_SUPERTILE)
                                : 0;
@@ -2702,13 +2703,14 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         g.prio = ctx->ovl && tail_marked && ctx->ovl_prio ? 1 : 0;
         launch_step(g, alg_h);
         hipEventRecord(evL[2 * s], main);
-        if (ovl && s == 0) {
-          // the overlapped prologue ends with launch 0: the pair takes over after it (launch
-          // 0's tall units waited for chain(1), so its chains are done too)
+        if (ovl && s + 1 == std::min<int>(ctx->ovl_launches, S - 1)) {
+          // the overlapped prologue ends with launch s (0 by default, LFM_OVL_LAUNCHES): the pair
+          // takes over after it (its tall units waited for chain(s + 1), so the prologue's
+          // chains are done too)
           main = ctx->m3;
           side = ctx->s3;
-          hipStreamWaitEvent(main, evL[0], 0);
-          hipStreamWaitEvent(side, evL[0], 0);
+          hipStreamWaitEvent(main, evL[2 * s], 0);
+          hipStreamWaitEvent(side, evL[2 * s], 0);
         }
         helped = hu > 0;
         if (hu > 0) {

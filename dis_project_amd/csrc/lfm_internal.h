@@ -157,6 +157,7 @@ struct lfm_ctx {
                                      // previous evaluation's tail
   int ovl_prio = 0;                  // LFM_OVL_PRIO: the tail's launches at wave priority 2
   int ovl_chains = 0;                // LFM_OVL_CHAINS: the prologue's chains on the reserve's CUs
+  int ovl_launches = 1;              // LFM_OVL_LAUNCHES: step launches in the prologue
   hipStream_t ovl_chain_stream = nullptr;  // primary (twins borrow it): CU-masked to the reserve
 };
 

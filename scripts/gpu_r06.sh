@@ -66,6 +66,15 @@ for study in "$@"; do
         done
       done
       ;;
+    overlap3)
+      $S r06_ovl3_tests 400 env LFM_OVL_RESERVE=96 LFM_OVL_LAUNCHES=2 LFM_OVL_PRIO=1 python -u -m pytest tests/test_gpu_full.py -m gpu -x -v --timeout 200 --timeout-method thread -k pipeline || exit $?
+      for r in 1 2; do
+        for v in "LFM_OVERLAP=0" "LFM_OVL_RESERVE=96" "LFM_OVL_RESERVE=96 LFM_OVL_PRIO=1" "LFM_OVL_RESERVE=80" "LFM_OVL_RESERVE=112" "LFM_OVL_RESERVE=96 LFM_OVL_LAUNCHES=2" "LFM_OVL_RESERVE=96 LFM_OVL_AT=5120"; do
+          tag=${v//=/_}; tag=${tag// /_}
+          env $v $S r06_ovl3_${tag}_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --no-cpu-baseline || exit $?
+        done
+      done
+      ;;
     fitab)
       for r in 1 2; do
         for lib in ablibs/r05/liblfm.so dis_project_amd/liblfm.so; do
