@@ -75,6 +75,16 @@ for study in "$@"; do
         done
       done
       ;;
+    ovltrace)
+      # kernel traces of the C3 step with the pipeline off / on (reserve 96): each kernel's
+      # queue, start and end (scripts/ovl_timeline.py)
+      for v in 0 1; do
+        export LFM_OVERLAP=$v LFM_OVL_RESERVE=96
+        $S r06_ovltrace_$v 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r06_ovltrace_$v -o run -- \
+          python3 bench.py --workload c3 --steps 2 --warmup 1 --no-cpu-baseline --no-profile || exit $?
+      done
+      unset LFM_OVERLAP LFM_OVL_RESERVE
+      ;;
     fitab)
       for r in 1 2; do
         for lib in ablibs/r05/liblfm.so dis_project_amd/liblfm.so; do
