@@ -717,6 +717,7 @@ hipError_t create_streams(lfm_ctx* ctx) {
   ctx->ovl_prio = env_int_api("LFM_OVL_PRIO", 0);
   ctx->ovl_chains = env_int_api("LFM_OVL_CHAINS", 0);
   ctx->ovl_launches = std::max(1, env_int_api("LFM_OVL_LAUNCHES", 1));
+  ctx->ovl_head = std::min(100, std::max(0, env_int_api("LFM_OVL_HEAD", 0)));
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, ctx->device);
   if (prop.multiProcessorCount > 0) ctx->cus = prop.multiProcessorCount;
@@ -1248,6 +1249,7 @@ int twin_get(lfm_ctx* ctx, int i, lfm_ctx** out) {
   t->ovl_prio = ctx->ovl_prio;
   t->ovl_chains = ctx->ovl_chains;
   t->ovl_launches = ctx->ovl_launches;
+  t->ovl_head = ctx->ovl_head;
   t->device = ctx->device;
   t->stream = ctx->ovl_stream;
   t->m3 = ctx->m3;

@@ -2701,7 +2701,34 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
           tail_marked = true;
         }
         g.prio = ctx->ovl && tail_marked && ctx->ovl_prio ? 1 : 0;
+        // overlapped, the first launch after the prologue (LFM_OVL_HEAD percent): its ahead units
+        // and the head of its rest enumeration run on the overlap stream right behind the
+        // prologue — under the previous evaluation's tail — and the rest of it (with the tall
+        // units, which wait for chain(s + 1) and the ahead units' rows on the device) on the
+        // pair. Disjoint units with the launch's arithmetic: the same bits; both halves keep
+        // xready, so each bumps it for the lead tiles it holds.
+        bool headed = false;
+        if (ovl && ctx->ovl_head > 0 && s == std::min<int>(ctx->ovl_launches, S - 1)) {
+          const int64_t head = std::min<int64_t>(total - hu, total * ctx->ovl_head / 100);
+          if (head > 0) {
+            StepArgs ph = g;
+            ph.nt = 0;
+            ph.rest_off = 0;
+            ph.nr = (int)head;
+            hipStream_t keep = main;
+            main = ctx->stream;
+            launch_step(ph);
+            main = keep;
+            hipEventRecord(ev[2 * S + 3], ctx->stream);
+            g.na = 0;
+            g.rest_off = head;
+            g.nr = (int)(total - hu - head);
+            headed = true;
+          }
+        }
         launch_step(g, alg_h);
+        // launch s + 1 and step s + 1's helper read the tiles the head updated
+        if (headed) hipStreamWaitEvent(main, ev[2 * S + 3], 0);
         hipEventRecord(evL[2 * s], main);
         if (ovl && s + 1 == std::min<int>(ctx->ovl_launches, S - 1)) {
           // the overlapped prologue ends with launch s (0 by default, LFM_OVL_LAUNCHES): the pair

@@ -158,6 +158,8 @@ struct lfm_ctx {
   int ovl_prio = 0;                  // LFM_OVL_PRIO: the tail's launches at wave priority 2
   int ovl_chains = 0;                // LFM_OVL_CHAINS: the prologue's chains on the reserve's CUs
   int ovl_launches = 1;              // LFM_OVL_LAUNCHES: step launches in the prologue
+  int ovl_head = 0;                  // LFM_OVL_HEAD: percent of the next launch's rest units
+                                     // run on the overlap stream behind the prologue
   hipStream_t ovl_chain_stream = nullptr;  // primary (twins borrow it): CU-masked to the reserve
 };
 

@@ -75,6 +75,16 @@ for study in "$@"; do
         done
       done
       ;;
+    overlap4)
+      # the head of the first post-prologue launch on the overlap stream (LFM_OVL_HEAD percent)
+      $S r06_ovl4_tests 400 env LFM_OVL_RESERVE=96 LFM_OVL_HEAD=50 python -u -m pytest tests/test_gpu_full.py -m gpu -x -v --timeout 200 --timeout-method thread -k pipeline || exit $?
+      for r in 1 2; do
+        for v in "LFM_OVERLAP=0" "LFM_OVL_HEAD=0" "LFM_OVL_HEAD=25" "LFM_OVL_HEAD=50" "LFM_OVL_HEAD=75" "LFM_OVL_HEAD=50 LFM_OVL_AT=8192"; do
+          tag=${v//=/_}; tag=${tag// /_}
+          env LFM_OVL_RESERVE=96 $v $S r06_ovl4_${tag}_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --no-cpu-baseline || exit $?
+        done
+      done
+      ;;
     ovltrace)
       # kernel traces of the C3 step with the pipeline off / on (reserve 96): each kernel's
       # queue, start and end (scripts/ovl_timeline.py)
