@@ -107,10 +107,6 @@ def parse(argv=None):
                    help="c5: hyperparameter rounds of the 15 problems per rank per step (weak "
                         "scaling over rounds, one launch and one exchange per step); 0 (default) "
                         "= 1 on one GPU (configs[4]'s step), 16 on several")
-    p.add_argument("--mixed", type=int, default=0,
-                   help="c3 A/B: one schedule-3 evaluation plus this many schedule-1 fillers per "
-                        "GPU, their streams off the factor chain's CUs (farm.ConcurrentEvaluator "
-                        "mixed=True)")
     p.add_argument("--fit-iters", type=int, default=150,
                    help="c5fit: Adam steps per fit (notebook.py:64 / main.py:54: 150)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -746,12 +742,7 @@ def main(argv=None):
         mine = farm.partition(len(models), world, rank)
         workers = a.workers if a.workers > 0 else farm.choose_workers(len(mine))
         per_step = len(models)
-        if a.mixed > 0:
-            workers = 1 + a.mixed
-            mev = farm.ConcurrentEvaluator(ctx, datasets[0], False, workers, mixed=True)
-            evaluate, close = (lambda models_, data_: mev(models_)), mev.close
-        else:
-            evaluate, close = farm.gpu_evaluator(ctx, datasets, negative=False, workers=workers)
+        evaluate, close = farm.gpu_evaluator(ctx, datasets, negative=False, workers=workers)
 
         def step():
             return fm.run_problems(models, datasets, evaluate)
@@ -955,10 +946,9 @@ def main(argv=None):
     elif a.workload == "c3":
         wl = (f"configs[2]: {len(res[0])} random restarts of the {a.genes}x{a.timepoints} grid "
               f"(N={n}, fp64) per step, farmed over {world} GPU(s), "
-              + (f"one schedule-3 evaluation and {a.mixed} schedule-1 filler(s) per GPU"
-                 if a.mixed > 0 else
-                 f"{workers} concurrent schedule-1 evaluations per GPU" if workers > 1
-                 else "one schedule-3 evaluation at a time per GPU"))
+              + (f"{workers} concurrent schedule-1 evaluations per GPU" if workers > 1
+                 else "one schedule-3 evaluation at a time per GPU, restarts pipelined "
+                      "(lfm_mll_multi_f64)"))
     elif a.workload == "c4":
         wl = (f"configs[3]: one fp32 lower-triangle gram fill per rank, {a.genes} genes x "
               f"{a.timepoints} timepoints, N={n} (Sigma stored as an N x N fp32 buffer)")

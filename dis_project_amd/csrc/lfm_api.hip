@@ -678,8 +678,6 @@ void release_partition(lfm_ctx* ctx) {
 //                        memory instead of the kernel arguments
 //   LFM_FARM_GRAPH       0: a device-side farm round is enqueued call by call instead of
 //                        replayed as one captured graph
-//   LFM_S1_MASK_CUS      (A/B) a schedule-1 context's streams avoid CUs [0, k) (CU-masked,
-//                        without the side stream's priority)
 //   LFM_OVERLAP / LFM_OVL_AT / LFM_OVL_RESERVE   lfm_mll_multi_f64's restart pipeline: on/off,
 //                        the trailing rows below which an evaluation's tail starts (the next one's
 //                        prologue may run), main CUs the overlap stream leaves to that tail
@@ -713,23 +711,12 @@ hipError_t create_streams(lfm_ctx* ctx) {
   ctx->side_req = env_int_api("LFM_SIDE_CUS", 32);
   ctx->ovl_on = env_int_api("LFM_OVERLAP", 1);
   ctx->ovl_at = env_int_api("LFM_OVL_AT", 6144);
-  ctx->ovl_reserve = std::max(0, env_int_api("LFM_OVL_RESERVE", 64));
-  ctx->ovl_prio = env_int_api("LFM_OVL_PRIO", 0);
-  ctx->ovl_chains = env_int_api("LFM_OVL_CHAINS", 0);
-  ctx->ovl_launches = std::max(1, env_int_api("LFM_OVL_LAUNCHES", 1));
-  ctx->ovl_head = std::min(100, std::max(0, env_int_api("LFM_OVL_HEAD", 0)));
+  ctx->ovl_reserve = std::max(0, env_int_api("LFM_OVL_RESERVE", 96));
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, ctx->device);
   if (prop.multiProcessorCount > 0) ctx->cus = prop.multiProcessorCount;
   // ctx->side (schedule 1's high-priority stream) is created on first use: schedule 3 never
   // launches on it, and an idle hardware queue beside the running ones costs
-  ctx->s1_mask = ctx->sched == 1 ? std::max(0, env_int_api("LFM_S1_MASK_CUS", 0)) : 0;
-  if (ctx->s1_mask > 0 && ctx->s1_mask < ctx->cus) {
-    std::vector<uint32_t> mk((ctx->cus + 31) / 32, 0u);
-    for (int c = ctx->s1_mask; c < ctx->cus; ++c) mk[c / 32] |= 1u << (c % 32);
-    return hipExtStreamCreateWithCUMask(&ctx->stream, (uint32_t)mk.size(), mk.data());
-  }
-  ctx->s1_mask = 0;
   hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
   if (e != hipSuccess || ctx->sched != 3) return e;
   return create_partition(ctx, ctx->side_req);
@@ -1231,25 +1218,8 @@ int twin_get(lfm_ctx* ctx, int i, lfm_ctx** out) {
       return hip_fail(ctx, e, "overlap stream");
     }
   }
-  if (ctx->ovl_chains && !ctx->ovl_chain_stream) {
-    const int lo = ctx->side_cus, hi = std::min(ctx->cus - 64, ctx->side_cus + ctx->ovl_reserve);
-    if (hi - lo < ctx->side_cus) return set_err(ctx, LFM_E_ARG, "LFM_OVL_CHAINS: reserve < side CUs");
-    std::vector<uint32_t> mk((ctx->cus + 31) / 32, 0u);
-    for (int c = lo; c < hi; ++c) mk[c / 32] |= 1u << (c % 32);
-    hipError_t e =
-        hipExtStreamCreateWithCUMask(&ctx->ovl_chain_stream, (uint32_t)mk.size(), mk.data());
-    if (e != hipSuccess) {
-      ctx->ovl_chain_stream = nullptr;
-      return hip_fail(ctx, e, "overlap chain stream");
-    }
-  }
   std::unique_ptr<lfm_ctx> t(new lfm_ctx());
   t->borrowed = true;
-  t->ovl_chain_stream = ctx->ovl_chain_stream;
-  t->ovl_prio = ctx->ovl_prio;
-  t->ovl_chains = ctx->ovl_chains;
-  t->ovl_launches = ctx->ovl_launches;
-  t->ovl_head = ctx->ovl_head;
   t->device = ctx->device;
   t->stream = ctx->ovl_stream;
   t->m3 = ctx->m3;
@@ -1290,17 +1260,14 @@ int twin_get(lfm_ctx* ctx, int i, lfm_ctx** out) {
 // about to go, or the context is).
 void twins_drop(lfm_ctx* ctx) {
   if (ctx->borrowed || (!ctx->twin[0] && !ctx->twin[1] && !ctx->ovl_stream)) return;
-  for (hipStream_t st : {ctx->ovl_stream, ctx->ovl_chain_stream, ctx->m3, ctx->s3, ctx->stream})
+  for (hipStream_t st : {ctx->ovl_stream, ctx->m3, ctx->s3, ctx->stream})
     if (st) hipStreamSynchronize(st);
   for (lfm_ctx*& t : ctx->twin) {
     lfm_ctx_destroy(t);
     t = nullptr;
   }
-  for (hipStream_t* st : {&ctx->ovl_stream, &ctx->ovl_chain_stream})
-    if (*st) {
-      hipStreamDestroy(*st);
-      *st = nullptr;
-    }
+  if (ctx->ovl_stream) hipStreamDestroy(ctx->ovl_stream);
+  ctx->ovl_stream = nullptr;
 }
 }  // namespace
 
@@ -1403,7 +1370,7 @@ int lfm_mll_multi_f64(lfm_ctx* ctx, lfm_data* data, int64_t nsets, const lfm_hyp
     return r;
   };
   auto drain = [&] {
-    for (hipStream_t st : {ctx->ovl_stream, ctx->ovl_chain_stream, ctx->m3, ctx->s3, ctx->stream})
+    for (hipStream_t st : {ctx->ovl_stream, ctx->m3, ctx->s3, ctx->stream})
       if (st) hipStreamSynchronize(st);
     tw[0]->ovl = tw[1]->ovl = false;
   };

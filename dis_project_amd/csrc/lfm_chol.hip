@@ -1324,8 +1324,6 @@ struct StepArgs {
                      // enumeration (the side-CU helper launch takes the tail of it)
   unsigned long long* trace;  // diagnostics (NULL: off): 4 words per workgroup (lfm_debug_trace)
   unsigned long long trace_tag;  // launch tag, bits 40+ of each record's last word
-  int prio;  // restart pipeline (LFM_OVL_PRIO): the tail's launches issue ahead (s_setprio 2) of
-             // the next evaluation's prologue sharing their CUs
 };
 
 // Diagnostics: atomic max of the 100 MHz clock (or of its bitwise NOT: the earliest start)
@@ -1494,7 +1492,6 @@ __device__ __forceinline__ void step_body(const StepArgs& g, unsigned long long*
   tall_or_xcd_range(seg, cnt[seg], b - base, &lo, &hi);
   const int64_t u = lo;
   if (u >= hi) return;
-  if (g.prio) __builtin_amdgcn_s_setprio(2);
   const int role = seg + 1;
   if (ran && threadIdx.x == 0) *ran = ((unsigned long long)role << 32) | (unsigned long long)u;
   unsigned long long* const st = g.stamps;
@@ -2376,19 +2373,11 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     if (r) return r;
   }
   if (!s3 && !ctx->side) {
-    // schedule 1's high-priority side stream, created on first use (schedule 3 never needs it);
-    // a CU-masked schedule-1 context (LFM_S1_MASK_CUS) masks it the same way instead
+    // schedule 1's high-priority side stream, created on first use (schedule 3 never needs it)
     int least = 0, greatest = 0;
     hipDeviceGetStreamPriorityRange(&least, &greatest);
-    hipError_t e;
-    if (ctx->s1_mask > 0) {
-      std::vector<uint32_t> mk((ctx->cus + 31) / 32, 0u);
-      for (int c = ctx->s1_mask; c < ctx->cus; ++c) mk[c / 32] |= 1u << (c % 32);
-      e = hipExtStreamCreateWithCUMask(&ctx->side, (uint32_t)mk.size(), mk.data());
-    } else {
-      e = hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest);
-    }
-    if (e != hipSuccess) return hip_fail(ctx, hipErrorOutOfMemory, "side stream creation");
+    if (hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, greatest) != hipSuccess)
+      return hip_fail(ctx, hipErrorOutOfMemory, "side stream creation");
   }
   hipStream_t main = ctx->stream, side = ctx->side;
   hipEvent_t* ev = ctx->evs.data();  // [0]: inputs ready; E1_s = ev[1 + 2s]; E2_s = ev[2 + 2s]
@@ -2584,13 +2573,6 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
     // and waits on the device for its inputs (xready[s]) from the main launch in flight
     if (ovl) {
       main = side = ctx->stream;
-      if (ctx->ovl_chains) {
-        // the prologue's chains on their own stream (the reserve's CUs), beside X_0 / launch 0
-        // as in the unpipelined schedule (whose tall units wait for them on the device)
-        side = ctx->ovl_chain_stream;
-        hipEventRecord(ev[0], ctx->stream);
-        hipStreamWaitEvent(side, ev[0], 0);
-      }
     } else {
       hipEventRecord(ev[0], main);
       hipStreamWaitEvent(side, ev[0], 0);
@@ -2685,8 +2667,7 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
         // units store without write-through and bump no counter, so they never include a lead
         // tile of chain(s + 2).
         const int64_t total = g.nr;  // the step's rest enumeration
-        const bool in_prologue = ovl && s + 1 <= std::min<int>(ctx->ovl_launches, S - 1);
-        const int64_t hu = s >= 1 && s + 2 < S && !in_prologue
+        const int64_t hu = s >= 1 && s + 2 < S
                                ? helper_clamp(helper_share(g, steps[s + 1].second), (int)total,
                                               g.T, g.wn, g.xready ? g.lead : 0, LFM_SUPERTILE)
                                : 0;
@@ -2700,44 +2681,15 @@ int chol_factor_solve(lfm_ctx* ctx, double* A, int64_t lda, int64_t n, int64_t M
           hipEventRecord(ctx->ovl_tail, main);
           tail_marked = true;
         }
-        g.prio = ctx->ovl && tail_marked && ctx->ovl_prio ? 1 : 0;
-        // overlapped, the first launch after the prologue (LFM_OVL_HEAD percent): its ahead units
-        // and the head of its rest enumeration run on the overlap stream right behind the
-        // prologue — under the previous evaluation's tail — and the rest of it (with the tall
-        // units, which wait for chain(s + 1) and the ahead units' rows on the device) on the
-        // pair. Disjoint units with the launch's arithmetic: the same bits; both halves keep
-        // xready, so each bumps it for the lead tiles it holds.
-        bool headed = false;
-        if (ovl && ctx->ovl_head > 0 && s == std::min<int>(ctx->ovl_launches, S - 1)) {
-          const int64_t head = std::min<int64_t>(total - hu, total * ctx->ovl_head / 100);
-          if (head > 0) {
-            StepArgs ph = g;
-            ph.nt = 0;
-            ph.rest_off = 0;
-            ph.nr = (int)head;
-            hipStream_t keep = main;
-            main = ctx->stream;
-            launch_step(ph);
-            main = keep;
-            hipEventRecord(ev[2 * S + 3], ctx->stream);
-            g.na = 0;
-            g.rest_off = head;
-            g.nr = (int)(total - hu - head);
-            headed = true;
-          }
-        }
         launch_step(g, alg_h);
-        // launch s + 1 and step s + 1's helper read the tiles the head updated
-        if (headed) hipStreamWaitEvent(main, ev[2 * S + 3], 0);
         hipEventRecord(evL[2 * s], main);
-        if (ovl && s + 1 == std::min<int>(ctx->ovl_launches, S - 1)) {
-          // the overlapped prologue ends with launch s (0 by default, LFM_OVL_LAUNCHES): the pair
-          // takes over after it (its tall units waited for chain(s + 1), so the prologue's
-          // chains are done too)
+        if (ovl && s == 0) {
+          // the overlapped prologue ends with launch 0: the pair takes over after it (its tall
+          // units waited for chain(1), so the prologue's chains are done too)
           main = ctx->m3;
           side = ctx->s3;
-          hipStreamWaitEvent(main, evL[2 * s], 0);
-          hipStreamWaitEvent(side, evL[2 * s], 0);
+          hipStreamWaitEvent(main, evL[0], 0);
+          hipStreamWaitEvent(side, evL[0], 0);
         }
         helped = hu > 0;
         if (hu > 0) {

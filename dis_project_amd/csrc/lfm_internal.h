@@ -50,9 +50,6 @@ struct lfm_ctx {
   hipStream_t m3 = nullptr;      // schedule 3: bulk stream (CUs outside the chain's)
   hipStream_t s3 = nullptr;      // schedule 3: factor-chain stream (LFM_SIDE_CUS CUs)
   int side_req = 32;             // LFM_SIDE_CUS at creation: the reservation to (re)create
-  // LFM_S1_MASK_CUS (A/B, schedule-1 contexts): the context's streams leave CUs [0, k) alone —
-  // a schedule-1 filler beside a schedule-3 context, off its factor chain's CUs
-  int s1_mask = 0;
   int cus = 256;                 // compute units of the device
   std::vector<hipEvent_t> evs;   // cross-stream dependency events (timing disabled)
   std::string err;
@@ -151,16 +148,10 @@ struct lfm_ctx {
   hipEvent_t ovl_done = nullptr;     // twin: recorded on m3 after its finalize
   hipEvent_t ovl_res = nullptr;      // twin: its result copied to the host (primary's stream)
   int ovl_on = 1;                    // LFM_OVERLAP: 0 evaluates lfm_mll_multi_f64's sets one by one
-  int64_t ovl_at = 5120;             // LFM_OVL_AT: the tail starts at the first step whose
+  int64_t ovl_at = 6144;             // LFM_OVL_AT: the tail starts at the first step whose
                                      // trailing matrix has fewer rows than this
-  int ovl_reserve = 64;              // LFM_OVL_RESERVE: main CUs the overlap stream leaves to the
+  int ovl_reserve = 96;              // LFM_OVL_RESERVE: main CUs the overlap stream leaves to the
                                      // previous evaluation's tail
-  int ovl_prio = 0;                  // LFM_OVL_PRIO: the tail's launches at wave priority 2
-  int ovl_chains = 0;                // LFM_OVL_CHAINS: the prologue's chains on the reserve's CUs
-  int ovl_launches = 1;              // LFM_OVL_LAUNCHES: step launches in the prologue
-  int ovl_head = 0;                  // LFM_OVL_HEAD: percent of the next launch's rest units
-                                     // run on the overlap stream behind the prologue
-  hipStream_t ovl_chain_stream = nullptr;  // primary (twins borrow it): CU-masked to the reserve
 };
 
 // ---------------------------------------------------------------- helpers

@@ -460,33 +460,12 @@ class ConcurrentEvaluator:
     others at their next pull, and is re-raised in the caller once every worker has returned,
     so no worker thread outlives the call on these non-thread-safe contexts."""
 
-    def __init__(self, ctx: _lib.Context, data, negative: bool = False, workers: int = 3,
-                 mixed: bool = False):
+    def __init__(self, ctx: _lib.Context, data, negative: bool = False, workers: int = 3):
         self.ctx, self._restore = ctx, ctx.schedule
         self.own, self.evs, self.pool = [], [], None
         try:
-            if mixed:
-                # (A/B, DESIGN.md §5) worker 0 keeps the caller's schedule-3 context; the others
-                # are schedule-1 fillers whose streams avoid its factor chain's CUs
-                # (LFM_S1_MASK_CUS, read at context creation), soaking up the main CUs the
-                # schedule-3 evaluation leaves idle (its chain-bound tail, launch ramps)
-                import os
-
-                keep = {k: os.environ.get(k) for k in ("LFM_SCHED", "LFM_S1_MASK_CUS")}
-                os.environ["LFM_SCHED"] = "1"
-                os.environ["LFM_S1_MASK_CUS"] = os.environ.get("LFM_SIDE_CUS", "32")
-                try:
-                    for _ in range(max(1, int(workers)) - 1):
-                        self.own.append(_lib.Context(ctx.device))
-                finally:
-                    for k, v in keep.items():
-                        if v is None:
-                            os.environ.pop(k, None)
-                        else:
-                            os.environ[k] = v
-            else:
-                ctx.schedule = 1
-            for _ in range(0 if mixed else max(1, int(workers)) - 1):
+            ctx.schedule = 1
+            for _ in range(max(1, int(workers)) - 1):
                 c = _lib.Context(ctx.device)
                 self.own.append(c)
                 c.schedule = 1

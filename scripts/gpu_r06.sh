@@ -7,7 +7,13 @@
 #            lines interleaved, two rounds
 #   rehearse two ranks sharing the card, gloo exchange: c5 (16 rounds per rank) and c5fit
 #            (the 15 fits partitioned)
+#   overlap  the restart pipeline's tests and c3 lines off / on at several tail starts / reserves
+#   ovltrace rocprofv3 kernel traces of the c3 step with the pipeline off / on
 #   c2 c3 c5 c5fit   one bench line each (the default step counts of the round's profile set)
+# The studies `mixed` (schedule-1 fillers, bench --mixed) and `overlap2`-`overlap4` (pipeline
+# priority, prologue chains on the reserve, two prologue launches, a head of launch 1 on the
+# overlap stream) ran at commits 4b52ebb / a3c0876 / 292617b / 5183b09; their knobs measured
+# slower or equal and were removed (profiles/r06_ab.txt).
 set -u
 export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -35,15 +41,6 @@ for study in "$@"; do
       $S r06_reh_c5fit 300 $R --master-port 29533 bench.py --gpus 2 --workload c5fit --steps 5 --warmup 1 \
         --share-gpus --gather gloo --no-cpu-baseline || exit $?
       ;;
-    mixed)
-      # C3: one schedule-3 evaluation at a time against it plus 1 / 2 schedule-1 fillers off the
-      # chain's CUs (bench.py --mixed), interleaved, two rounds
-      for r in 1 2; do
-        $S r06_mixed0_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --workers 1 --no-cpu-baseline || exit $?
-        $S r06_mixed1_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --mixed 1 --no-cpu-baseline || exit $?
-        $S r06_mixed2_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --mixed 2 --no-cpu-baseline || exit $?
-      done
-      ;;
     overlap)
       # C3's restart pipeline (lfm_mll_multi_f64): its tests, then c3 lines with it off / on at
       # several tail starts and reserves, interleaved, two rounds
@@ -52,36 +49,6 @@ for study in "$@"; do
         for v in "LFM_OVERLAP=0" "LFM_OVERLAP=1" "LFM_OVL_AT=8192" "LFM_OVL_AT=4096" "LFM_OVL_RESERVE=32" "LFM_OVL_RESERVE=128"; do
           tag=${v//=/_}
           env $v $S r06_ovl_${tag}_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --no-cpu-baseline || exit $?
-        done
-      done
-      ;;
-    overlap2)
-      # the pipeline's variants: tail launches at wave priority 2, the prologue's chains beside
-      # its launches on the reserve's CUs, both; reserve 96; interleaved, two rounds
-      $S r06_ovl2_tests 400 env LFM_OVL_PRIO=1 LFM_OVL_CHAINS=1 python -u -m pytest tests/test_gpu_full.py -m gpu -x -v --timeout 200 --timeout-method thread -k pipeline || exit $?
-      for r in 1 2; do
-        for v in "LFM_OVERLAP=0" "LFM_OVERLAP=1" "LFM_OVL_PRIO=1" "LFM_OVL_CHAINS=1" "LFM_OVL_PRIO=1 LFM_OVL_CHAINS=1" "LFM_OVL_RESERVE=96"; do
-          tag=${v//=/_}; tag=${tag// /_}
-          env $v $S r06_ovl2_${tag}_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --no-cpu-baseline || exit $?
-        done
-      done
-      ;;
-    overlap3)
-      $S r06_ovl3_tests 400 env LFM_OVL_RESERVE=96 LFM_OVL_LAUNCHES=2 LFM_OVL_PRIO=1 python -u -m pytest tests/test_gpu_full.py -m gpu -x -v --timeout 200 --timeout-method thread -k pipeline || exit $?
-      for r in 1 2; do
-        for v in "LFM_OVERLAP=0" "LFM_OVL_RESERVE=96" "LFM_OVL_RESERVE=96 LFM_OVL_PRIO=1" "LFM_OVL_RESERVE=80" "LFM_OVL_RESERVE=112" "LFM_OVL_RESERVE=96 LFM_OVL_LAUNCHES=2" "LFM_OVL_RESERVE=96 LFM_OVL_AT=5120"; do
-          tag=${v//=/_}; tag=${tag// /_}
-          env $v $S r06_ovl3_${tag}_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --no-cpu-baseline || exit $?
-        done
-      done
-      ;;
-    overlap4)
-      # the head of the first post-prologue launch on the overlap stream (LFM_OVL_HEAD percent)
-      $S r06_ovl4_tests 400 env LFM_OVL_RESERVE=96 LFM_OVL_HEAD=50 python -u -m pytest tests/test_gpu_full.py -m gpu -x -v --timeout 200 --timeout-method thread -k pipeline || exit $?
-      for r in 1 2; do
-        for v in "LFM_OVERLAP=0" "LFM_OVL_HEAD=0" "LFM_OVL_HEAD=25" "LFM_OVL_HEAD=50" "LFM_OVL_HEAD=75" "LFM_OVL_HEAD=50 LFM_OVL_AT=8192"; do
-          tag=${v//=/_}; tag=${tag// /_}
-          env LFM_OVL_RESERVE=96 $v $S r06_ovl4_${tag}_$r 300 python -u bench.py --workload c3 --steps 4 --warmup 1 --no-cpu-baseline || exit $?
         done
       done
       ;;
