@@ -359,7 +359,7 @@ def cpu_baseline_c3(models, data, threads, gpu_values):
     }
 
 
-def cpu_baseline_c5(models, datasets, gpu_values, min_seconds=2.0):
+def cpu_baseline_c5(models, datasets, gpu_values, threads, min_seconds=2.0):
     """C5 on the CPU: the 15 problems evaluated sequentially on ONE core by the C++
     restatement, timed in full and repeated until min_seconds have passed (a step is 15
     evaluations of microseconds each); every value checks the GPU batch's."""
@@ -377,9 +377,10 @@ def cpu_baseline_c5(models, datasets, gpu_values, min_seconds=2.0):
     t = time.perf_counter() - t0
     ref = np.asarray(vals)
     rel = np.abs(ref - np.asarray(gpu_values)) / np.abs(ref)
-    # the same problems across the allowed cores: one problem per OpenMP thread at a time
-    # (oracle/lfm_cpu.cpp lfm_cpu_mll_batch), many rounds in one parallel loop
-    thr = len(os.sched_getaffinity(0))
+    # the same problems across the box's CPU share (cpu_threads: OMP_NUM_THREADS, else the
+    # process's affinity): one problem per OpenMP thread at a time (oracle/lfm_cpu.cpp
+    # lfm_cpu_mll_batch), many rounds in one parallel loop
+    thr = threads
     genes = [m.num_genes for m in models]
     hyp = np.concatenate([np.concatenate([m.true_d, m.true_s, m.true_b]) for m in models] +
                          [np.array([[m.l, m.obs_stddev, m.jitter] for m in models]).reshape(-1)])
@@ -410,13 +411,13 @@ def cpu_baseline_c5(models, datasets, gpu_values, min_seconds=2.0):
             "cores": thr,
             "sample": (f"oracle/lfm_cpu.cpp lfm_cpu_mll_batch: {reps} rounds of the "
                        f"{len(models)} problems in one OpenMP loop, one problem per thread at a "
-                       f"time on {thr} threads (this process's CPU affinity of {os.cpu_count()} "
-                       f"host CPUs), {tt:.2f} s"),
+                       f"time on {thr} threads of {os.cpu_count()} host CPUs (the box's CPU "
+                       f"share), {tt:.2f} s"),
         },
     }
 
 
-def cpu_baseline_c5fit(models, datasets, raw0, iters, gpu_final, min_seconds=2.0):
+def cpu_baseline_c5fit(models, datasets, raw0, iters, gpu_final, threads, min_seconds=2.0):
     """The C5 fit on the CPU: oracle/lfm_cpu.cpp's JaxTrainer.fit (value and gradient by dual
     numbers of the reference's erf formulas, explicit Sigma^{-1}, the same Adam loop) of the 15
     problems sequentially on ONE core, repeated until min_seconds have passed; the final losses
@@ -444,9 +445,9 @@ def cpu_baseline_c5fit(models, datasets, raw0, iters, gpu_final, min_seconds=2.0
     ref = np.asarray(finals)
     rel = np.abs(ref - np.asarray(gpu_final)) / np.abs(ref)
     per_step = len(models) * iters
-    # the same fits across the allowed cores: one problem per OpenMP thread at a time
+    # the same fits across the box's CPU share: one problem per OpenMP thread at a time
     # (lfm_cpu_fit_batch), repeated until min_seconds have passed
-    thr = len(os.sched_getaffinity(0))
+    thr = threads
     xs, ys = [d.X for d in datasets], [d.y for d in datasets]
     r0 = []
     off = 0
@@ -478,8 +479,8 @@ def cpu_baseline_c5fit(models, datasets, raw0, iters, gpu_final, min_seconds=2.0
             "unit": "problem training steps/s",
             "cores": thr,
             "sample": (f"oracle/lfm_cpu.cpp lfm_cpu_fit_batch: the {len(models)} fits in one "
-                       f"OpenMP loop, one problem per thread at a time on {thr} threads (this "
-                       f"process's CPU affinity of {os.cpu_count()} host CPUs; at most "
+                       f"OpenMP loop, one problem per thread at a time on {thr} threads of "
+                       f"{os.cpu_count()} host CPUs (the box's CPU share; at most "
                        f"{len(models)} busy), {trounds} rounds in {tt:.2f} s"),
         },
     }
@@ -1179,10 +1180,10 @@ def main(argv=None):
             cb = cpu_baseline_c3(models, datasets[0], thr, res[0])
             bad = not cb["gpu_vs_cpu_rel"] <= PARITY_RTOL
         elif a.workload == "c5":
-            cb = cpu_baseline_c5(models, datasets, res[0])
+            cb = cpu_baseline_c5(models, datasets, res[0], thr)
             bad = not cb["gpu_vs_cpu_rel"] <= PARITY_RTOL
         elif a.workload == "c5fit":
-            cb = cpu_baseline_c5fit(models, datasets, raw0, a.fit_iters, res[0])
+            cb = cpu_baseline_c5fit(models, datasets, raw0, a.fit_iters, res[0], thr)
             bad = not cb["gpu_vs_cpu_rel"] <= PARITY_RTOL
         else:
             check = np.array([0, 4, 256, 32768, n - 4, 4 * 5000, 4 * 9999, 4 * 16000])
