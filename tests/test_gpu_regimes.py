@@ -191,6 +191,62 @@ def test_stalled_schedule3_falls_back_to_schedule1(monkeypatch, call):
     assert abs(got - ref) <= MLL_RTOL * abs(ref), (got, ref)
 
 
+def test_stalled_restart_pipeline_reruns_every_set(monkeypatch):
+    """C3's restart pipeline (lfm_mll_multi_f64) with every device-side wait forced to run out
+    (LFM_DEBUG_SPIN_LIMIT=0): the pipelined sets stall, the call drains both workspaces and
+    evaluates every uncollected set again one by one, each with lfm_mll_f64_data's own
+    schedule-1 re-run — a status of 0 and the oracle's MLL to 1e-9 for every finite set, the
+    non-PD set still NaN with LFM_E_NOT_PD, bounded in time, the stalls counted."""
+    import time
+
+    from dis_project_amd import _lib, configs
+
+    work = configs.grid_workload("pipe_stall", 10, 256, seed_params=5, seed_y=6)  # N = 2560
+    x = np.ascontiguousarray(work.data.X)
+    y = np.ascontiguousarray(work.data.y.reshape(-1))
+    n = x.shape[0]
+    base = work.model
+    models = [base, base.replace(l=2.0), base.replace(jitter=-50.0, obs_stddev=0.0),
+              base.replace(obs_stddev=0.5)]
+    monkeypatch.setenv("LFM_DEBUG_SPIN_LIMIT", "0")
+    for k in ("LFM_S3_FALLBACK", "LFM_SCHED", "LFM_OVERLAP"):
+        monkeypatch.delenv(k, raising=False)
+    ctx = _lib.Context(0)
+    dx, dy, data = _lib.c_void_p(), _lib.c_void_p(), _lib.c_void_p()
+    try:
+        assert ctx.schedule == 3
+        ctx.check(ctx.lib.lfm_dev_alloc(ctx.handle, x.nbytes, _lib.ctypes.byref(dx)))
+        ctx.check(ctx.lib.lfm_dev_alloc(ctx.handle, y.nbytes, _lib.ctypes.byref(dy)))
+        ctx.check(ctx.lib.lfm_memcpy_h2d(ctx.handle, dx, x.ctypes.data, x.nbytes))
+        ctx.check(ctx.lib.lfm_memcpy_h2d(ctx.handle, dy, y.ctypes.data, y.nbytes))
+        ctx.check(ctx.lib.lfm_data_create(ctx.handle, dx, dy, n, _lib.ctypes.byref(data)))
+        hps = [m.hyp() for m in models]
+        arr = (_lib.LfmHyp * len(hps))(*[hp.struct for hp in hps])
+        out = np.empty(len(models))
+        st = np.full(len(models), -7, np.int32)
+        t0 = time.monotonic()
+        rc = ctx.lib.lfm_mll_multi_f64(ctx.handle, data, len(hps), arr, 0, _lib.dptr(out),
+                                       _lib.dptr(st))
+        dt = time.monotonic() - t0
+        assert rc == _lib.LFM_E_NOT_PD, (rc, ctx.lib.lfm_last_error(ctx.handle))
+        assert dt < 20.0, dt
+        assert st[2] == _lib.LFM_E_NOT_PD and math.isnan(out[2])
+        assert np.all(st[[0, 1, 3]] == 0), st
+        # the pipeline's stall, then each finite set's own schedule-1 re-run
+        assert ctx.fallbacks >= 1 + 3, ctx.fallbacks
+        for k in (0, 1, 3):
+            m = models[k]
+            ref = O.mll(x, y, m.true_d, m.true_s, m.true_b, m.l, m.obs_stddev, m.jitter)
+            assert abs(out[k] - ref) <= MLL_RTOL * abs(ref), (k, out[k], ref)
+    finally:
+        if data:
+            ctx.lib.lfm_data_destroy(data)
+        for p in (dx, dy):
+            if p:
+                ctx.lib.lfm_dev_free(ctx.handle, p)
+        ctx.close()
+
+
 def test_not_pd_is_still_nan_on_the_blocked_path():
     """A genuinely non-PD Sigma (negative jitter) at N = 2560 keeps JAX's NaN semantics:
     LFM_E_NOT_PD with the first failing pivot, NaN from the shim."""
