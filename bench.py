@@ -1040,7 +1040,11 @@ def main(argv=None):
                     per_eval = rec.get("hbm_bytes_per_eval")
                     pmc_lpe = rec.get("launches", 0) / max(1, rec.get("evals", 1))
                     lpe = syrk["launches"] / prof_steps
-                    if rec.get("schedule") == "LFM_S3_EVENTS=2" and round(pmc_lpe) == round(lpe):
+                    if rec.get("n", 16384) != n:
+                        # the counters were collected on another configuration's launches
+                        tsrc = (f"none: the PMC record (profiles/syrk_traffic.json) is of "
+                                f"N = {rec.get('n', 16384)}, this run is N = {n}")
+                    elif rec.get("schedule") == "LFM_S3_EVENTS=2" and round(pmc_lpe) == round(lpe):
                         # the counters saw this schedule's own launches (serialised by events)
                         traffic = rec.get("hbm_bytes_per_launch")
                         tsrc = ("PMC (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction) "

@@ -93,7 +93,10 @@ def main():
         rec = {"round": rnd, "source": f"profiles/{rnd}_hbm.json (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                "kernels": [k for k, _ in syrk],
                "hbm_bytes_per_eval": total / evals, "evals": evals,
-               "hbm_bytes_per_launch": total / max(1, launches), "launches": launches}
+               "hbm_bytes_per_launch": total / max(1, launches), "launches": launches,
+               # the PMC passes run bench.py's default C2 line (bench.py uses the record only
+               # for a run of the same N)
+               "n": int(os.environ.get("PMC_N", "16384"))}
         # the last evaluation's step launches one by one (bytes, dispatch order): with
         # LFM_S3_EVENTS=2 these are the timed schedule's own launches
         fs, ws = series.get("FETCH_SIZE", []), series.get("WRITE_SIZE", [])

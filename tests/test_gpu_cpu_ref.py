@@ -49,3 +49,38 @@ def test_mll_n16384_gpu_vs_cpp(c2, case, rtol):
           f"(cpu gram {info['t_gram']:.1f} s, chol {info['t_chol']:.1f} s)")
     assert info["fail"] == -1
     assert abs(gpu - cpu) <= rtol * abs(cpu), (gpu, cpu)
+
+
+def test_mll_n32768_both_schedules_vs_cpp(monkeypatch):
+    """Twice configs[1]'s size: 128 genes x 256 timepoints, N = 32768 (an 8.6 GB factor), the
+    MLL on schedule 3 (the default) and on schedule 1 (LFM_SCHED=1, the look-ahead on every CU)
+    against the C++ restatement at 1e-9 relative, and the two schedules against each other."""
+    import os
+
+    from dis_project_amd import _lib, configs, farm
+    from oracle import lfm_cpu
+
+    lfm_cpu.load()
+    work = configs.grid_workload("synthetic_128x256_fp64", 128, 256, seed_params=2, seed_y=3)
+    assert work.n == 32768
+    m = work.model
+    got = {}
+    for sched in ("3", "1"):
+        monkeypatch.setenv("LFM_SCHED", sched)
+        ctx = _lib.Context(0)
+        ev = farm.ResidentEvaluator(ctx, work.data)
+        try:
+            got[sched] = float(ev([m])[0])
+            assert ctx.fallbacks == 0
+        finally:
+            ev.close()
+            ctx.close()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    cpu, info = lfm_cpu.mll(work.data.X, work.data.y, m.true_d, m.true_s, m.true_b, m.l,
+                            m.obs_stddev, m.jitter, threads=min(threads, 32))
+    print(f"n32768: gpu s3 {got['3']!r} s1 {got['1']!r} cpu {cpu!r} "
+          f"(cpu gram {info['t_gram']:.1f} s, chol {info['t_chol']:.1f} s)")
+    assert info["fail"] == -1
+    for s, v in got.items():
+        assert abs(v - cpu) <= 1e-9 * abs(cpu), (s, v, cpu)
+    assert abs(got["3"] - got["1"]) <= 1e-9 * abs(cpu)
