@@ -84,3 +84,36 @@ def test_mll_n32768_both_schedules_vs_cpp(monkeypatch):
     for s, v in got.items():
         assert abs(v - cpu) <= 1e-9 * abs(cpu), (s, v, cpu)
     assert abs(got["3"] - got["1"]) <= 1e-9 * abs(cpu)
+
+
+def test_mll_n65536_both_schedules_vs_cpp_golden(monkeypatch):
+    """Four times configs[1]'s size: 256 genes x 256 timepoints, N = 65536 (a 34 GB factor; the
+    C4 grid in fp64), on schedule 3 and schedule 1, against the C++ restatement's MLL on the same
+    seeded inputs (tests/golden/scale_n65536.json, made by scripts/scale_check.py on the GPU
+    box's host in 193 s — too long to repeat per run) at 1e-9 relative, and the schedules
+    against each other."""
+    import json
+    import os
+
+    from dis_project_amd import _lib, configs, farm
+
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "scale_n65536.json")))
+    work = configs.grid_workload("synthetic_256x256_fp64", g["genes"], g["timepoints"],
+                                 seed_params=g["seed_params"], seed_y=g["seed_y"])
+    assert work.n == g["N"] == 65536
+    ref = g["mll_cpu_port"]
+    got = {}
+    for sched in ("3", "1"):
+        monkeypatch.setenv("LFM_SCHED", sched)
+        ctx = _lib.Context(0)
+        ev = farm.ResidentEvaluator(ctx, work.data)
+        try:
+            got[sched] = float(ev([work.model])[0])
+            assert ctx.fallbacks == 0
+        finally:
+            ev.close()
+            ctx.close()
+    print(f"n65536: gpu s3 {got['3']!r} s1 {got['1']!r} cpu port {ref!r}")
+    for s, v in got.items():
+        assert abs(v - ref) <= 1e-9 * abs(ref), (s, v, ref)
+    assert abs(got["3"] - got["1"]) <= 1e-9 * abs(ref)
