@@ -141,3 +141,34 @@ def test_cpu_port_fit_matches_golden(case):
                              fix=bool(ref["fix_params"]))
         assert bad == 0
         np.testing.assert_allclose(h, ref["hist"][p], rtol=1e-11)
+
+
+def test_cpu_port_threaded_batches_equal_the_sequential_port():
+    """bench.py's threaded CPU baselines (cpu_baseline.threads of the c5 / c5fit lines): the
+    C++ port's batch entry points, one problem per OpenMP thread, give the sequential port's
+    bits — the MLL batch (also with many rounds in one parallel loop) and the fit batch."""
+    models, datasets = farm.workload("c5")
+    genes = [m.num_genes for m in models]
+    hyp = np.concatenate([np.concatenate([m.true_d, m.true_s, m.true_b]) for m in models] +
+                         [np.array([[m.l, m.obs_stddev, m.jitter] for m in models]).reshape(-1)])
+    seq = np.array([lfm_cpu.mll(d.X, d.y, m.true_d, m.true_s, m.true_b, m.l, m.obs_stddev,
+                                m.jitter, threads=1)[0] for m, d in zip(models, datasets)])
+    xs, ys = [d.X for d in datasets], [d.y for d in datasets]
+    for threads, reps in ((1, 1), (4, 1), (4, 7)):
+        got = lfm_cpu.mll_batch(xs, ys, genes, hyp, threads=threads, reps=reps)
+        np.testing.assert_array_equal(got, seq)
+    iters = 12
+    raws = []
+    for m in models:
+        r = TR.unconstrain(m)
+        raws.append(np.concatenate([r["true_d"], r["true_s"], r["true_b"],
+                                    [r["l"], r["obs_stddev"], m.jitter]]))
+    hseq = []
+    for r, d, G in zip(raws, datasets, genes):
+        h, bad = lfm_cpu.fit(d.X, d.y, G, r.copy(), iters)
+        assert bad == 0
+        hseq.append(h)
+    rb = [r.copy() for r in raws]
+    hist, bad = lfm_cpu.fit_batch(xs, ys, genes, rb, iters, threads=4)
+    assert bad == 0
+    np.testing.assert_array_equal(hist, np.array(hseq))
