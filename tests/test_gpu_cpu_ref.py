@@ -97,7 +97,8 @@ def test_mll_n65536_both_schedules_vs_cpp_golden(monkeypatch):
 
     from dis_project_amd import _lib, configs, farm
 
-    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "scale_n65536.json")))
+    with open(os.path.join(os.path.dirname(__file__), "golden", "scale_n65536.json")) as f:
+        g = json.load(f)
     work = configs.grid_workload("synthetic_256x256_fp64", g["genes"], g["timepoints"],
                                  seed_params=g["seed_params"], seed_y=g["seed_y"])
     assert work.n == g["N"] == 65536
